@@ -1,0 +1,41 @@
+# Builds the MI355X (gfx950) CRC32C engine and its C-ABI:
+#   libhdfs3_amd/lib/libhdfs3_crc.so   (include/hdfs3_crc.h)
+# and the test-only oracle (oracle/Makefile).
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CSRC     := libhdfs3_amd/csrc
+LIBDIR   := libhdfs3_amd/lib
+OBJDIR   := build/obj
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Iinclude -I$(CSRC)
+HOSTFLAGS:= -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
+
+LIB      := $(LIBDIR)/libhdfs3_crc.so
+OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc32c.o
+
+all: $(LIB) oracle
+
+$(OBJDIR)/crc32c_kernels.o: $(CSRC)/crc32c_kernels.hip $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/hdfs3_crc.o: $(CSRC)/hdfs3_crc.cpp include/hdfs3_crc.h $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(OBJDIR)/host_crc32c.o: $(CSRC)/host_crc32c.cpp $(CSRC)/crc32c_tables.h
+	@mkdir -p $(OBJDIR)
+	g++ $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle all
+	@if [ -d /root/reference/src/common ]; then $(MAKE) -C oracle ref; fi
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,326 @@
+#!/usr/bin/env python3
+"""Device-resident CRC32C throughput over 512 B HDFS chunks (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[1]): one 128 MiB HDFS block, 512 B chunks, verify on
+one MI355X. A *step* = one hdfs3_crc32c_verify_dev_async launch over one whole block
+(262,144 chunks, data + BE CRC array resident in HBM). Each rank rotates over
+`--blocks` distinct blocks (default 8 = 1 GiB + CRCs) so the 256 MiB Infinity Cache
+cannot serve repeats. Multi-GPU (config 4): independent blocks shard one set per
+GPU, no collectives on the data path (weak scaling); value = all ranks' payload
+bytes / max-over-ranks time.
+
+Also reported, in the same run:
+  roofline      alg bytes per launch (N*(C+4)) / average launch time
+                from HIP events on the launch stream, vs the 8.0 TB/s HBM peak;
+                `traffic` = DRAM bytes per launch from rocprofv3 PMC passes
+                (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate passes);
+  cpu_baseline  the reference CPU path (oracle/_ref HWCrc32c built from the
+                reference sources, else the oracle's crc_pcl restatement) timed on
+                this host on a bounded sample (rank 0, N=1 only).
+
+    python bench.py [--gpus N --steps K --warmup W --bpc 512 --mode verify]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "device-resident CRC32C GiB/s over 512 B HDFS chunks; % of HBM roofline"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--bpc", type=int, default=512)
+    p.add_argument("--mode", choices=["verify", "compute"], default="verify")
+    p.add_argument("--block-mib", type=int, default=128)
+    p.add_argument("--blocks", type=int, default=8)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-pmc", action="store_true")
+    p.add_argument("--sweep", action="store_true", help="extra diagnostics on stderr")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return p.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class Workload:
+    """Per-rank device arena: `blocks` blocks of data + their BE CRC arrays, in HBM."""
+
+    def __init__(self, torch, ctx, device, block_bytes, blocks, bpc, seed):
+        self.torch, self.ctx = torch, ctx
+        self.block_bytes, self.blocks, self.bpc = block_bytes, blocks, bpc
+        self.nchunks = block_bytes // bpc
+        g = torch.Generator(device=device)
+        g.manual_seed(seed)
+        self.data = torch.randint(0, 256, (blocks, block_bytes), dtype=torch.uint8, device=device, generator=g)
+        self.crc = torch.empty((blocks, 4 * self.nchunks), dtype=torch.uint8, device=device)
+        for b in range(blocks):  # stored CRCs written by the GPU compute path, checked below
+            ctx.compute_dev(self.data_ptr(b), block_bytes, bpc, self.crc_ptr(b))
+        ctx.synchronize()
+
+    def data_ptr(self, b):
+        return self.data[b].data_ptr()
+
+    def crc_ptr(self, b):
+        return self.crc[b].data_ptr()
+
+
+def check_against_oracle(work, ctx):
+    """Block 0's device-computed CRC array must equal the oracle's, word for word, and a
+    single flipped bit must be reported at its chunk (parity gate before timing)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from util import oracle_compute  # test infrastructure: used as the checker only
+
+    data = work.data[0].cpu().numpy()
+    got = work.crc[0].cpu().numpy()
+    want = oracle_compute(data, work.bpc)
+    if not np.array_equal(got, want):
+        bad = int(np.nonzero(got != want)[0][0]) // 4
+        raise SystemExit(f"PARITY FAILURE: device CRC of chunk {bad} differs from the oracle")
+    k = work.nchunks // 3
+    pos = k * work.bpc + 17
+    orig = work.data[0, pos].item()
+    work.data[0, pos] = orig ^ 0x20
+    work.torch.cuda.synchronize()
+    first = ctx.verify_dev(work.data_ptr(0), work.block_bytes, work.bpc, work.crc_ptr(0))
+    work.data[0, pos] = orig
+    work.torch.cuda.synchronize()
+    if first != k:
+        raise SystemExit(f"PARITY FAILURE: flipped bit in chunk {k} reported as {first}")
+    if ctx.verify_dev(work.data_ptr(0), work.block_bytes, work.bpc, work.crc_ptr(0)) != -1:
+        raise SystemExit("PARITY FAILURE: clean block reported bad")
+
+
+def run_steps(work, ctx, mode, n, result, events=None):
+    for s in range(n):
+        b = s % work.blocks
+        if events is not None:
+            events[2 * s].record()
+        if mode == "verify":
+            ctx.verify_dev_async(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b),
+                                 result.data_ptr() + 8 * (s % result.numel()))
+        else:
+            ctx.compute_dev(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b))
+        if events is not None:
+            events[2 * s + 1].record()
+
+
+def stream_read_ceiling(torch, work, ctx, reps=10):
+    """Achievable HBM read rate on the same 1 GiB arena (coalesced 16 B/lane stream)."""
+    from libhdfs3_amd import _native
+    lib = _native.lib()
+    sink = torch.zeros(4, dtype=torch.int32, device=work.data.device)
+    total = work.blocks * work.block_bytes
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    lib.hdfs3x_stream_read(ctx.ctx, work.data.data_ptr(), total, 0, sink.data_ptr())
+    e0.record()
+    for _ in range(reps):
+        lib.hdfs3x_stream_read(ctx.ctx, work.data.data_ptr(), total, 0, sink.data_ptr())
+    e1.record()
+    torch.cuda.synchronize()
+    return total * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+
+def lane_read_rate(torch, work, ctx, reps=10):
+    from libhdfs3_amd import _native
+    lib = _native.lib()
+    sink = torch.zeros(4, dtype=torch.int32, device=work.data.device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for r in range(reps):
+        b = r % work.blocks
+        lib.hdfs3x_lane_read(ctx.ctx, work.data_ptr(b), work.block_bytes, work.bpc, sink.data_ptr())
+    e1.record()
+    torch.cuda.synchronize()
+    return work.block_bytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+
+def cpu_baseline(work, seconds, bpc):
+    """Reference CPU path on this host, bounded sample of the same workload (one block)."""
+    import ctypes
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from util import PCL, oracle, ref_lib  # test infrastructure: baseline leg only
+
+    data = np.ascontiguousarray(work.data[0].cpu().numpy())
+    crc = np.ascontiguousarray(work.crc[0].cpu().numpy())
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    ref = ref_lib()
+    bad = ctypes.c_int64(0)
+    if ref is not None and ref.ref_hw_available():
+        kind, engine = "reference", "HWCrc32c (reference src/common/HWCrc32c.cpp, built by oracle/Makefile)"
+        fn = lambda reps: ref.ref_hw_bench_verify(data.ctypes.data, data.nbytes, bpc, crc.ctypes.data,
+                                                  threads, reps, ctypes.byref(bad))
+    else:
+        kind, engine = "port", "oracle crc_pcl restatement (3-way crc32q + pclmul, IntelAsmCrc32c behaviour)"
+        fn = lambda reps: oracle().oracle_bench_verify(PCL, data.ctypes.data, data.nbytes, bpc, crc.ctypes.data,
+                                                       threads, reps, ctypes.byref(bad))
+    t1 = fn(1)
+    reps = max(1, int(seconds / max(t1, 1e-6)))
+    t = fn(reps)
+    if bad.value != -1:
+        raise SystemExit(f"cpu baseline reported a bad chunk {bad.value} on a clean block")
+    gib = data.nbytes * reps / t / 2**30
+    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"{reps} x verify of one {data.nbytes >> 20} MiB block ({bpc} B chunks, "
+                      f"RemoteBlockReader::verifyChecksum loop) split over {threads} threads, {t:.1f} s; "
+                      f"engine: {engine}"}
+
+
+def pmc_traffic(args):
+    """DRAM bytes per verify launch: two rocprofv3 passes (FETCH_SIZE, WRITE_SIZE) over a
+    short child run; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 counts wide
+    streaming reads at half their bytes)."""
+    if not shutil.which("rocprofv3"):
+        return None, "rocprofv3 not on PATH"
+    out_root = os.path.join(REPO, "gpurun_out", "bench_pmc")
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(out_root, counter)
+        shutil.rmtree(d, ignore_errors=True)
+        cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--bpc", str(args.bpc),
+               "--mode", args.mode, "--block-mib", str(args.block_mib), "--blocks", str(args.blocks)]
+        try:
+            subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        except Exception as e:  # profiling is best effort; the value line does not depend on it
+            return None, f"rocprofv3 {counter} pass failed: {e}"
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if not files:
+            return None, f"no counter csv for {counter}"
+        per = []
+        with open(files[0]) as f:
+            for row in csv.DictReader(f):
+                if "crc32c_chunks_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    per.append(float(row["Counter_Value"]))
+        if not per:
+            return None, f"no crc32c_chunks_kernel rows for {counter}"
+        per = per[len(per) // 2:]  # steady state (skip the CRC-setup launches)
+        vals[counter] = sum(per) / len(per)
+    # rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB
+    fetch = vals["FETCH_SIZE"] * 1024 * 2
+    write = vals["WRITE_SIZE"] * 1024
+    return fetch + write, f"FETCH_SIZE {vals['FETCH_SIZE']:.0f} KiB x2 + WRITE_SIZE {vals['WRITE_SIZE']:.0f} KiB per launch"
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+
+    from libhdfs3_amd.engine import CrcContext
+    ctx = CrcContext(local)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    block_bytes = args.block_mib << 20
+    work = Workload(torch, ctx, device, block_bytes, args.blocks, args.bpc, seed=1234 + rank)
+
+    if args.pmc_child:
+        res = torch.zeros(64, dtype=torch.int64, device=device)
+        run_steps(work, ctx, args.mode, 16, res)
+        torch.cuda.synchronize()
+        return
+
+    check_against_oracle(work, ctx)
+
+    K, W = args.steps, args.warmup
+    result = torch.zeros(max(K, W, 1), dtype=torch.int64, device=device)
+    run_steps(work, ctx, args.mode, W, result)
+    result.zero_()
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_steps(work, ctx, args.mode, K, result, events)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if args.mode == "verify" and bool((result != 0).any().item()):
+        raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the timed region")
+
+    launch_ms = [events[2 * s].elapsed_time(events[2 * s + 1]) for s in range(K)]
+    avg_launch_s = sum(launch_ms) / K * 1e-3
+    payload = block_bytes
+    alg_bytes = work.nchunks * (args.bpc + 4)  # verify reads data + CRC; compute reads data, writes CRC
+    total_payload = payload * K * world
+    value = total_payload / elapsed / 2**30
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    achieved = alg_bytes / avg_launch_s / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                "alg_bytes_per_launch": alg_bytes, "avg_launch_us": round(avg_launch_s * 1e6, 2)}
+    extra = {}
+    if world == 1:
+        try:
+            extra["achievable_read_GBps"] = round(stream_read_ceiling(torch, work, ctx), 1)
+            roofline["achievable_read_GBps"] = extra["achievable_read_GBps"]
+        except Exception as e:
+            log("stream ceiling failed:", e)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(work, args.cpu_seconds, args.bpc)
+    if args.sweep and world == 1:
+        log(json.dumps({"lane_read_GBps": round(lane_read_rate(torch, work, ctx), 1)}))
+    if world == 1 and not args.no_pmc:
+        traffic, note = pmc_traffic(args)
+        roofline["traffic"] = int(traffic) if traffic else None
+        roofline["traffic_note"] = note
+
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": K,
+        "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (torch.randint bytes)",
+        "config": {"workload": f"{args.mode} of one {args.block_mib} MiB HDFS block per step, "
+                               f"{args.bpc} B chunks, device-resident (BASELINE.json configs[1])",
+                   "bpc": args.bpc, "block_bytes": block_bytes, "chunks_per_block": work.nchunks,
+                   "blocks_rotated_per_gpu": args.blocks, "mode": args.mode,
+                   "parallelism": f"{world} GPU(s), independent blocks one set per GPU, no collectives"},
+        "roofline": roofline, "cpu_baseline": cpu,
+    }
+    if cpu:
+        line["gpu_over_cpu"] = round(value / cpu["value"], 1)
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+/*
+ * hdfs3_crc.h — C-ABI of the MI355X-native per-chunk CRC32C engine for libhdfs3.
+ *
+ * This is the drop-in boundary for libhdfs3's checksum hot path. The reference
+ * has no plugin registry: the engine is picked by #ifdef behind the streaming
+ * `Checksum` ABC (src/common/Checksum.h:43-67) at three call sites, each of which
+ * runs a per-chunk reset/update/getValue loop on the CPU:
+ *
+ *   read/remote : RemoteBlockReader::verifyChecksum   src/client/RemoteBlockReader.cpp:306-326
+ *   read/local  : LocalBlockReader::readAndVerify     src/client/LocalBlockReader.cpp:138-163
+ *   write       : OutputStreamImpl::appendInternal +  src/client/OutputStreamImpl.cpp:298-359
+ *                 Packet::addChecksum                 src/client/Packet.cpp:73-81
+ *
+ * Every entry point below replaces one of those loops with a batched call on a
+ * gfx950 kernel. Conventions follow the reference C API
+ * (src/client/hdfs.h, src/client/Hdfs.cpp:75-80,826-881): plain pointers and
+ * sizes, return 0 on success and a negative errno-style code on failure, never
+ * throw across the boundary; the thread-local message is hdfs3_crc_last_error()
+ * (cf. hdfsGetLastError, hdfs.h:80).
+ *
+ * Checksum words are CRC32C (reflected poly 0x82F63B78, init/xorout 0xFFFFFFFF)
+ * stored BIG-ENDIAN, one per bytesPerChecksum chunk (src/common/BigEndian.h:43-59).
+ * bpc must be a positive multiple of 4 (the reference requires a multiple of 512
+ * for writes, SessionConfig.cpp:112; readers accept any bpc > 0 from the
+ * datanode, so bpc % 4 != 0 is rejected with -EINVAL rather than mis-verified).
+ *
+ * Threading: one ctx per stream/thread, like one Checksum instance per reader or
+ * writer in the reference. Distinct contexts share nothing but the device.
+ */
+#ifndef HDFS3_CRC_H
+#define HDFS3_CRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDFS3_CRC_ABI_VERSION 1
+
+/* CHECKSUM_TYPE_CRC32C (src/common/Checksum.h:35) — the only type implemented. */
+#define HDFS3_CHECKSUM_TYPE_CRC32C 2
+
+typedef struct hdfs3_crc_ctx hdfs3_crc_ctx;
+
+/* One HDFS data-transfer packet inside a contiguous arena: the wire layout read by
+ * RemoteBlockReader::readNextPacket (RemoteBlockReader.cpp:240-245) is
+ * [ceil(dataLen/bpc) x BE32 CRC][dataLen bytes]; crc_off/data_off locate both. */
+typedef struct hdfs3_pkt_desc {
+    uint64_t data_off; /* byte offset of the packet's data region in the arena   */
+    uint64_t crc_off;  /* byte offset of the packet's BE32 CRC region            */
+    uint32_t data_len; /* PacketHeaderProto.dataLen (datatransfer.proto:143-150)  */
+    uint32_t reserved; /* must be 0                                               */
+} hdfs3_pkt_desc;
+
+int hdfs3_crc_abi_version(void);
+const char *hdfs3_crc_last_error(void);
+
+/* ---- context --------------------------------------------------------------
+ * Owns the HIP stream (unless one is attached), the 4 KiB slice-table image in
+ * HBM, result slots and the pinned/device staging rings of the host-buffer API.
+ * Replaces the per-reader `shared_ptr<Checksum>` construction at
+ * RemoteBlockReader.cpp:169-184, LocalBlockReader.cpp:86-98, OutputStreamImpl.cpp:55-66. */
+int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out);
+void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx);
+/* Attach an external hipStream_t (e.g. a framework's current stream); NULL
+ * restores the ctx-owned stream. */
+int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream);
+void *hdfs3_crc_ctx_get_stream(hdfs3_crc_ctx *ctx);
+int hdfs3_crc_ctx_synchronize(hdfs3_crc_ctx *ctx);
+/* Number of checksum kernels this ctx has launched (lets callers/tests prove the
+ * GPU path ran). */
+uint64_t hdfs3_crc_ctx_kernel_launches(hdfs3_crc_ctx *ctx);
+
+/* ---- host-buffer API (H2D + kernel + D2H through the ctx's pinned ring) ------
+ * compute: Packet::addChecksum per chunk (Packet.cpp:73-81) for ceil(len/bpc)
+ * chunks, last one possibly short (OutputStreamImpl.cpp:410-419 flush path).
+ * verify: *first_bad_chunk = index of the first mismatching chunk or -1.
+ *   check_short_tail = 0: RemoteBlockReader semantics (a short tail chunk's
+ *   mismatch is ignored, RemoteBlockReader.cpp:319); 1: LocalBlockReader
+ *   semantics (tail checked, LocalBlockReader.cpp:149-161).
+ * A mismatch is NOT an error (return 0); callers raise ChecksumException
+ * (src/common/Exception.h:116-125) from *first_bad_chunk >= 0. */
+int hdfs3_crc32c_compute(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc,
+                         void *crc_be_out);
+int hdfs3_crc32c_verify(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc,
+                        const void *crc_be, int check_short_tail, int64_t *first_bad_chunk);
+
+/* ---- device-resident API (pointers in HBM) ---------------------------------
+ * _dev: launched on the ctx stream; verify_dev waits for and returns the result.
+ * _async: nothing waits; the result lands in a caller-owned device u64 that must
+ * be ZERO before the launch: it stays 0 when every chunk matches, otherwise it
+ * holds ~first_bad_chunk (decode with hdfs3_crc_decode_result). */
+int hdfs3_crc32c_compute_dev(hdfs3_crc_ctx *ctx, const void *d_data, size_t len, uint32_t bpc,
+                             void *d_crc_be_out);
+int hdfs3_crc32c_verify_dev(hdfs3_crc_ctx *ctx, const void *d_data, size_t len, uint32_t bpc,
+                            const void *d_crc_be, int check_short_tail,
+                            int64_t *first_bad_chunk);
+int hdfs3_crc32c_verify_dev_async(hdfs3_crc_ctx *ctx, const void *d_data, size_t len,
+                                  uint32_t bpc, const void *d_crc_be, int check_short_tail,
+                                  uint64_t *d_result);
+int64_t hdfs3_crc_decode_result(uint64_t result_word);
+
+/* ---- packet-stream API -----------------------------------------------------
+ * n packets of one block in one arena (wire layout of a5/a6 in SURVEY.md §8a).
+ * Verifies every chunk of every packet; on mismatch reports the first bad packet
+ * (index into pk[]) and the chunk inside it, else both -1. The host variant
+ * stages the arena through the ctx ring; _dev takes an arena already in HBM and
+ * a host descriptor array. */
+int hdfs3_crc32c_verify_packets(hdfs3_crc_ctx *ctx, const void *arena, size_t arena_len,
+                                const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc,
+                                int check_short_tail, int64_t *bad_packet,
+                                int64_t *bad_chunk);
+int hdfs3_crc32c_verify_packets_dev(hdfs3_crc_ctx *ctx, const void *d_arena, size_t arena_len,
+                                    const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc,
+                                    int check_short_tail, int64_t *bad_packet,
+                                    int64_t *bad_chunk);
+/* compute side of the packet API (write path, OutputStreamImpl + Packet::getBuffer):
+ * fills each packet's CRC region in place. */
+int hdfs3_crc32c_compute_packets_dev(hdfs3_crc_ctx *ctx, void *d_arena, size_t arena_len,
+                                     const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc);
+
+/* ---- streaming shim ---------------------------------------------------------
+ * Checksum::update on a raw state (seed 0xFFFFFFFF = reset(), ~state = getValue()),
+ * for sub-chunk pieces only: the partial chunk a writer carries across append()
+ * calls (OutputStreamImpl.cpp:309-314). Host code; never used by the batch API. */
+uint32_t hdfs3_crc32c_update_host(uint32_t state, const void *p, size_t len);
+
+/* ---- device memory helpers for FFI callers without a HIP binding ---------- */
+int hdfs3_dev_malloc(void **d_ptr, size_t bytes);
+int hdfs3_dev_free(void *d_ptr);
+int hdfs3_host_malloc_pinned(void **h_ptr, size_t bytes);
+int hdfs3_host_free_pinned(void *h_ptr);
+int hdfs3_memcpy_h2d(hdfs3_crc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
+int hdfs3_memcpy_d2h(hdfs3_crc_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
+int hdfs3_memset_dev(hdfs3_crc_ctx *ctx, void *d_dst, int value, size_t bytes);
+int hdfs3_device_count(int *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HDFS3_CRC_H */

@@ -1,0 +1,103 @@
+"""ctypes binding of the C-ABI in include/hdfs3_crc.h (libhdfs3_amd/lib/libhdfs3_crc.so).
+
+This is exactly the binding a non-C caller of the drop-in boundary would write
+(INTEGRATION.md shows the same for C++). There is no fallback: if the HIP
+library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_int, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libhdfs3_crc.so")
+
+
+class Hdfs3CrcError(RuntimeError):
+    """A C-ABI call returned a negative errno code."""
+
+    def __init__(self, fn: str, rc: int, msg: str):
+        super().__init__(f"{fn} failed rc={rc} ({os.strerror(-rc) if rc < 0 else rc}): {msg}")
+        self.rc = rc
+
+
+class PktDesc(ctypes.Structure):
+    """hdfs3_pkt_desc (include/hdfs3_crc.h)."""
+
+    _fields_ = [("data_off", c_uint64), ("crc_off", c_uint64), ("data_len", c_uint32),
+                ("reserved", c_uint32)]
+
+
+# name -> (restype, argtypes); every symbol include/hdfs3_crc.h declares.
+PUBLIC_API = {
+    "hdfs3_crc_abi_version": (c_int, []),
+    "hdfs3_crc_last_error": (ctypes.c_char_p, []),
+    "hdfs3_crc_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "hdfs3_crc_ctx_destroy": (None, [c_void_p]),
+    "hdfs3_crc_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
+    "hdfs3_crc_ctx_get_stream": (c_void_p, [c_void_p]),
+    "hdfs3_crc_ctx_synchronize": (c_int, [c_void_p]),
+    "hdfs3_crc_ctx_kernel_launches": (c_uint64, [c_void_p]),
+    "hdfs3_crc32c_compute": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p]),
+    "hdfs3_crc32c_verify": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p, c_int,
+                                    POINTER(c_int64)]),
+    "hdfs3_crc32c_compute_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p]),
+    "hdfs3_crc32c_verify_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p, c_int,
+                                        POINTER(c_int64)]),
+    "hdfs3_crc32c_verify_dev_async": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p,
+                                              c_int, c_void_p]),
+    "hdfs3_crc_decode_result": (c_int64, [c_uint64]),
+    "hdfs3_crc32c_verify_packets": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PktDesc),
+                                            c_size_t, c_uint32, c_int, POINTER(c_int64),
+                                            POINTER(c_int64)]),
+    "hdfs3_crc32c_verify_packets_dev": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PktDesc),
+                                                c_size_t, c_uint32, c_int, POINTER(c_int64),
+                                                POINTER(c_int64)]),
+    "hdfs3_crc32c_compute_packets_dev": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PktDesc),
+                                                 c_size_t, c_uint32]),
+    "hdfs3_crc32c_update_host": (c_uint32, [c_uint32, c_void_p, c_size_t]),
+    "hdfs3_dev_malloc": (c_int, [POINTER(c_void_p), c_size_t]),
+    "hdfs3_dev_free": (c_int, [c_void_p]),
+    "hdfs3_host_malloc_pinned": (c_int, [POINTER(c_void_p), c_size_t]),
+    "hdfs3_host_free_pinned": (c_int, [c_void_p]),
+    "hdfs3_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "hdfs3_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "hdfs3_memset_dev": (c_int, [c_void_p, c_void_p, c_int, c_size_t]),
+    "hdfs3_device_count": (c_int, [POINTER(c_int)]),
+}
+
+# measurement hooks (bench.py only; not in the public header)
+BENCH_API = {
+    "hdfs3x_stream_read": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    "hdfs3x_lane_read": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p]),
+    "hdfs3x_grid_cap": (c_int, [c_void_p]),
+}
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: run `make` (or __graft_entry__.build()) first; "
+                          "libhdfs3_amd has no CPU fallback")
+    lib = ctypes.CDLL(path)
+    for table in (PUBLIC_API, BENCH_API):
+        for name, (res, args) in table.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+    return lib
+
+
+_LIB: ctypes.CDLL | None = None
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        _LIB = load()
+    return _LIB
+
+
+def check(fn: str, rc: int) -> int:
+    if rc < 0:
+        raise Hdfs3CrcError(fn, rc, lib().hdfs3_crc_last_error().decode(errors="replace"))
+    return rc

@@ -1,0 +1,525 @@
+// C-ABI of the MI355X CRC32C engine (include/hdfs3_crc.h).
+//
+// Error convention mirrors libhdfs3's C API (src/client/Hdfs.cpp:75-80,243-327):
+// no exception crosses extern "C"; failures return a negative errno code and
+// leave a thread-local message (hdfs3_crc_last_error, cf. hdfsGetLastError at
+// Hdfs.cpp:59,329).
+#include "hdfs3_crc.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+#include "crc32c_kernels.h"
+#include "crc32c_tables.h"
+
+namespace hdfs3crc {
+uint32_t host_update(uint32_t state, const void *p, size_t n);
+}
+
+using namespace hdfs3crc;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    const int code = e == hipErrorOutOfMemory ? -ENOMEM
+                     : e == hipErrorInvalidValue ? -EINVAL
+                     : e == hipErrorNoDevice || e == hipErrorInvalidDevice ? -ENODEV
+                                                                           : -EIO;
+    return fail(code, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                  \
+    do {                                               \
+        hipError_t e_ = (expr);                        \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+// Staging segment of the host-buffer API: 16 MiB of payload per H2D transfer.
+constexpr size_t kSegmentBytes = 16u << 20;
+
+struct Slot {
+    uint8_t *h_data = nullptr, *h_crc = nullptr;  // pinned
+    uint8_t *d_data = nullptr, *d_crc = nullptr;  // device
+    size_t data_cap = 0, crc_cap = 0;
+    hipEvent_t done = nullptr;
+    // compute: CRC bytes waiting in h_crc to be copied out once `done` fires
+    uint8_t *pending_out = nullptr;
+    size_t pending_bytes = 0;
+};
+
+}  // namespace
+
+struct hdfs3_crc_ctx {
+    int device = 0;
+    int grid_cap = 256;            // one 1024-thread workgroup per CU (128 KiB LDS image)
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t *d_tables = nullptr;  // 4 x 256 slice-table image
+    unsigned long long *d_result = nullptr;
+    unsigned long long *h_result = nullptr;  // pinned
+    DevPacket *d_pk = nullptr;
+    DevPacket *h_pk = nullptr;               // pinned
+    size_t pk_cap = 0;
+    Slot slot[2];
+    uint64_t launches = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int check_args(hdfs3_crc_ctx *ctx, uint32_t bpc) {
+    if (!ctx) return fail(-EINVAL, "null hdfs3_crc_ctx");
+    if (bpc == 0 || (bpc & 3u)) return fail(-EINVAL, "bytes per checksum %u must be a positive multiple of 4", bpc);
+    return 0;
+}
+
+int grow_slot(Slot &s, size_t data_bytes, size_t crc_bytes) {
+    if (data_bytes > s.data_cap) {
+        if (s.h_data) (void)hipHostFree(s.h_data);
+        if (s.d_data) (void)hipFree(s.d_data);
+        s.h_data = s.d_data = nullptr;
+        s.data_cap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_data), data_bytes, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d_data), data_bytes));
+        s.data_cap = data_bytes;
+    }
+    if (crc_bytes > s.crc_cap) {
+        if (s.h_crc) (void)hipHostFree(s.h_crc);
+        if (s.d_crc) (void)hipFree(s.d_crc);
+        s.h_crc = s.d_crc = nullptr;
+        s.crc_cap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_crc), crc_bytes, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d_crc), crc_bytes));
+        s.crc_cap = crc_bytes;
+    }
+    return 0;
+}
+
+int grow_pk(hdfs3_crc_ctx *ctx, size_t n) {
+    if (n <= ctx->pk_cap) return 0;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->d_pk) (void)hipFree(ctx->d_pk);
+    if (ctx->h_pk) (void)hipHostFree(ctx->h_pk);
+    ctx->d_pk = nullptr;
+    ctx->h_pk = nullptr;
+    ctx->pk_cap = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&ctx->d_pk), n * sizeof(DevPacket)));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_pk), n * sizeof(DevPacket), hipHostMallocDefault));
+    ctx->pk_cap = n;
+    return 0;
+}
+
+int finish_pending(Slot &s) {
+    if (s.pending_out) {
+        HIP_TRY(hipEventSynchronize(s.done));
+        std::memcpy(s.pending_out, s.h_crc, s.pending_bytes);
+        s.pending_out = nullptr;
+        s.pending_bytes = 0;
+    }
+    return 0;
+}
+
+int launch(hdfs3_crc_ctx *ctx, const ChunkLaunch &a, bool verify) {
+    HIP_TRY(launch_chunks(a, verify, ctx->d_tables, ctx->grid_cap, ctx->stream));
+    ++ctx->launches;
+    return 0;
+}
+
+// Host-buffer pipeline shared by compute and verify: segments of whole chunks
+// alternate between two pinned/device slots, so the CPU copy into pinned memory
+// of segment i+1 overlaps the DMA and kernel of segment i.
+int host_pipeline(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc,
+                  const void *crc_in, void *crc_out, int check_short_tail,
+                  int64_t *first_bad) {
+    const bool verify = crc_in != nullptr;
+    const size_t seg = (kSegmentBytes / bpc > 0 ? kSegmentBytes / bpc : 1) * size_t(bpc);
+    const size_t seg_crc = (seg / bpc) * 4;
+    if (verify) {
+        HIP_TRY(hipMemsetAsync(ctx->d_result, 0, sizeof(unsigned long long), ctx->stream));
+    }
+    const uint8_t *src = static_cast<const uint8_t *>(data);
+    size_t off = 0;
+    for (int k = 0; off < len; ++k) {
+        Slot &s = ctx->slot[k & 1];
+        const size_t n = len - off < seg ? len - off : seg;
+        const size_t nc = (n + bpc - 1) / bpc;
+        const size_t chunk0 = off / bpc;
+        if (s.done) HIP_TRY(hipEventSynchronize(s.done));
+        if (int rc = finish_pending(s)) return rc;
+        if (int rc = grow_slot(s, seg, seg_crc)) return rc;
+        std::memcpy(s.h_data, src + off, n);
+        HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, n, hipMemcpyHostToDevice, ctx->stream));
+        ChunkLaunch a{};
+        a.data = s.d_data;
+        a.len = n;
+        a.bpc = bpc;
+        a.chunk_base = chunk0;
+        a.check_short_tail = check_short_tail;
+        if (verify) {
+            std::memcpy(s.h_crc, static_cast<const uint8_t *>(crc_in) + 4 * chunk0, 4 * nc);
+            HIP_TRY(hipMemcpyAsync(s.d_crc, s.h_crc, 4 * nc, hipMemcpyHostToDevice, ctx->stream));
+            a.crc_be = s.d_crc;
+            a.result = ctx->d_result;
+        } else {
+            a.out_be = s.d_crc;
+        }
+        if (int rc = launch(ctx, a, verify)) return rc;
+        if (!verify) {
+            HIP_TRY(hipMemcpyAsync(s.h_crc, s.d_crc, 4 * nc, hipMemcpyDeviceToHost, ctx->stream));
+            s.pending_out = static_cast<uint8_t *>(crc_out) + 4 * chunk0;
+            s.pending_bytes = 4 * nc;
+        }
+        if (!s.done) HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(s.done, ctx->stream));
+        off += n;
+    }
+    if (verify) {
+        HIP_TRY(hipMemcpyAsync(ctx->h_result, ctx->d_result, sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (Slot &s : ctx->slot)
+        if (int rc = finish_pending(s)) return rc;
+    if (verify && first_bad) *first_bad = hdfs3_crc_decode_result(*ctx->h_result);
+    return 0;
+}
+
+int packets_common(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len,
+                   const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc, bool verify,
+                   int check_short_tail, int64_t *bad_packet, int64_t *bad_chunk) {
+    for (size_t i = 0; i < n; ++i) {
+        const hdfs3_pkt_desc &d = pk[i];
+        const uint64_t chunks = (uint64_t(d.data_len) + bpc - 1) / bpc;
+        if (d.data_off > arena_len || d.data_len > arena_len - d.data_off ||
+            d.crc_off > arena_len || 4 * chunks > arena_len - d.crc_off)
+            return fail(-EINVAL, "packet %zu lies outside the %zu-byte arena", i, arena_len);
+    }
+    if (int rc = grow_pk(ctx, n)) return rc;
+    // the previous call's descriptors may still be in flight from h_pk
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (size_t i = 0; i < n; ++i)
+        ctx->h_pk[i] = DevPacket{pk[i].data_off, pk[i].crc_off, pk[i].data_len, 0};
+    HIP_TRY(hipMemcpyAsync(ctx->d_pk, ctx->h_pk, n * sizeof(DevPacket), hipMemcpyHostToDevice,
+                           ctx->stream));
+    if (verify) HIP_TRY(hipMemsetAsync(ctx->d_result, 0, sizeof(unsigned long long), ctx->stream));
+    HIP_TRY(launch_packets(d_arena, ctx->d_pk, n, bpc, verify, check_short_tail, ctx->d_result,
+                           ctx->d_tables, ctx->grid_cap, ctx->stream));
+    ++ctx->launches;
+    if (verify) {
+        HIP_TRY(hipMemcpyAsync(ctx->h_result, ctx->d_result, sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (verify) {
+        const unsigned long long r = *ctx->h_result;
+        const uint64_t key = r ? ~r : 0;
+        if (bad_packet) *bad_packet = r ? int64_t(key >> 32) : -1;
+        if (bad_chunk) *bad_chunk = r ? int64_t(key & 0xFFFFFFFFu) : -1;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hdfs3_crc_abi_version(void) { return HDFS3_CRC_ABI_VERSION; }
+
+const char *hdfs3_crc_last_error(void) { return g_err; }
+
+int hdfs3_device_count(int *count) {
+    if (!count) return fail(-EINVAL, "null count");
+    HIP_TRY(hipGetDeviceCount(count));
+    return 0;
+}
+
+int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out) {
+    if (!out) return fail(-EINVAL, "null out");
+    *out = nullptr;
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(-ENODEV, "device %d not present (%d visible)", device, ndev);
+    hdfs3_crc_ctx *ctx = new (std::nothrow) hdfs3_crc_ctx();
+    if (!ctx) return fail(-ENOMEM, "ctx allocation");
+    ctx->device = device;
+    DeviceGuard g(device);
+    auto bail = [&](int rc) {
+        hdfs3_crc_ctx_destroy(ctx);
+        return rc;
+    };
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return bail(fail(-EIO, "hipGetDeviceProperties(%d) failed", device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return bail(fail(-ENODEV, "device %d is %s; this build targets gfx950 (MI355X) only",
+                         device, prop.gcnArchName));
+    ctx->grid_cap = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(-EIO, "hipStreamCreate failed"));
+    ctx->stream = ctx->own_stream;
+    uint32_t t[kSlices][kTableEntries];
+    build_slice_tables(t);
+    if (hipMalloc(reinterpret_cast<void **>(&ctx->d_tables), sizeof(t)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&ctx->d_result), sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&ctx->h_result), sizeof(unsigned long long),
+                      hipHostMallocDefault) != hipSuccess)
+        return bail(fail(-ENOMEM, "device allocation for ctx failed"));
+    if (hipMemcpy(ctx->d_tables, t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(-EIO, "table upload failed"));
+    *out = ctx;
+    return 0;
+}
+
+void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx) {
+    if (!ctx) return;
+    DeviceGuard g(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (Slot &s : ctx->slot) {
+        if (s.h_data) (void)hipHostFree(s.h_data);
+        if (s.h_crc) (void)hipHostFree(s.h_crc);
+        if (s.d_data) (void)hipFree(s.d_data);
+        if (s.d_crc) (void)hipFree(s.d_crc);
+        if (s.done) (void)hipEventDestroy(s.done);
+    }
+    if (ctx->d_pk) (void)hipFree(ctx->d_pk);
+    if (ctx->h_pk) (void)hipHostFree(ctx->h_pk);
+    if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+    if (ctx->d_result) (void)hipFree(ctx->d_result);
+    if (ctx->h_result) (void)hipHostFree(ctx->h_result);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream) {
+    if (!ctx) return fail(-EINVAL, "null ctx");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    return 0;
+}
+
+void *hdfs3_crc_ctx_get_stream(hdfs3_crc_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
+
+int hdfs3_crc_ctx_synchronize(hdfs3_crc_ctx *ctx) {
+    if (!ctx) return fail(-EINVAL, "null ctx");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+uint64_t hdfs3_crc_ctx_kernel_launches(hdfs3_crc_ctx *ctx) { return ctx ? ctx->launches : 0; }
+
+int64_t hdfs3_crc_decode_result(uint64_t r) { return r ? int64_t(~r) : -1; }
+
+int hdfs3_crc32c_compute(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc,
+                         void *crc_be_out) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (len == 0) return 0;
+    if (!data || !crc_be_out) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    return host_pipeline(ctx, data, len, bpc, nullptr, crc_be_out, 0, nullptr);
+}
+
+int hdfs3_crc32c_verify(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc,
+                        const void *crc_be, int check_short_tail, int64_t *first_bad_chunk) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (first_bad_chunk) *first_bad_chunk = -1;
+    if (len == 0) return 0;
+    if (!data || !crc_be) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    return host_pipeline(ctx, data, len, bpc, crc_be, nullptr, check_short_tail, first_bad_chunk);
+}
+
+int hdfs3_crc32c_compute_dev(hdfs3_crc_ctx *ctx, const void *d_data, size_t len, uint32_t bpc,
+                             void *d_crc_be_out) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (len == 0) return 0;
+    if (!d_data || !d_crc_be_out) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    ChunkLaunch a{};
+    a.data = static_cast<const uint8_t *>(d_data);
+    a.len = len;
+    a.bpc = bpc;
+    a.out_be = static_cast<uint8_t *>(d_crc_be_out);
+    return launch(ctx, a, false);
+}
+
+int hdfs3_crc32c_verify_dev_async(hdfs3_crc_ctx *ctx, const void *d_data, size_t len,
+                                  uint32_t bpc, const void *d_crc_be, int check_short_tail,
+                                  uint64_t *d_result) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (len == 0) return 0;
+    if (!d_data || !d_crc_be || !d_result) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    ChunkLaunch a{};
+    a.data = static_cast<const uint8_t *>(d_data);
+    a.len = len;
+    a.bpc = bpc;
+    a.crc_be = static_cast<const uint8_t *>(d_crc_be);
+    a.result = reinterpret_cast<unsigned long long *>(d_result);
+    a.check_short_tail = check_short_tail;
+    return launch(ctx, a, true);
+}
+
+int hdfs3_crc32c_verify_dev(hdfs3_crc_ctx *ctx, const void *d_data, size_t len, uint32_t bpc,
+                            const void *d_crc_be, int check_short_tail, int64_t *first_bad_chunk) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (first_bad_chunk) *first_bad_chunk = -1;
+    if (len == 0) return 0;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipMemsetAsync(ctx->d_result, 0, sizeof(unsigned long long), ctx->stream));
+    if (int rc = hdfs3_crc32c_verify_dev_async(ctx, d_data, len, bpc, d_crc_be, check_short_tail,
+                                               reinterpret_cast<uint64_t *>(ctx->d_result)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->h_result, ctx->d_result, sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (first_bad_chunk) *first_bad_chunk = hdfs3_crc_decode_result(*ctx->h_result);
+    return 0;
+}
+
+int hdfs3_crc32c_verify_packets(hdfs3_crc_ctx *ctx, const void *arena, size_t arena_len,
+                                const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc,
+                                int check_short_tail, int64_t *bad_packet, int64_t *bad_chunk) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (bad_packet) *bad_packet = -1;
+    if (bad_chunk) *bad_chunk = -1;
+    if (n == 0) return 0;
+    if (!arena || !pk) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    Slot &s = ctx->slot[0];
+    if (s.done) HIP_TRY(hipEventSynchronize(s.done));
+    if (int rc = finish_pending(s)) return rc;
+    if (int rc = grow_slot(s, arena_len, 4)) return rc;
+    std::memcpy(s.h_data, arena, arena_len);
+    HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, arena_len, hipMemcpyHostToDevice, ctx->stream));
+    return packets_common(ctx, s.d_data, arena_len, pk, n, bpc, true, check_short_tail, bad_packet,
+                          bad_chunk);
+}
+
+int hdfs3_crc32c_verify_packets_dev(hdfs3_crc_ctx *ctx, const void *d_arena, size_t arena_len,
+                                    const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc,
+                                    int check_short_tail, int64_t *bad_packet,
+                                    int64_t *bad_chunk) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (bad_packet) *bad_packet = -1;
+    if (bad_chunk) *bad_chunk = -1;
+    if (n == 0) return 0;
+    if (!d_arena || !pk) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    return packets_common(ctx, static_cast<const uint8_t *>(d_arena), arena_len, pk, n, bpc, true,
+                          check_short_tail, bad_packet, bad_chunk);
+}
+
+int hdfs3_crc32c_compute_packets_dev(hdfs3_crc_ctx *ctx, void *d_arena, size_t arena_len,
+                                     const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (n == 0) return 0;
+    if (!d_arena || !pk) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    return packets_common(ctx, static_cast<const uint8_t *>(d_arena), arena_len, pk, n, bpc, false,
+                          0, nullptr, nullptr);
+}
+
+uint32_t hdfs3_crc32c_update_host(uint32_t state, const void *p, size_t len) {
+    return len ? host_update(state, p, len) : state;
+}
+
+int hdfs3_dev_malloc(void **d_ptr, size_t bytes) {
+    if (!d_ptr) return fail(-EINVAL, "null out");
+    HIP_TRY(hipMalloc(d_ptr, bytes));
+    return 0;
+}
+
+int hdfs3_dev_free(void *d_ptr) {
+    HIP_TRY(hipFree(d_ptr));
+    return 0;
+}
+
+int hdfs3_host_malloc_pinned(void **h_ptr, size_t bytes) {
+    if (!h_ptr) return fail(-EINVAL, "null out");
+    HIP_TRY(hipHostMalloc(h_ptr, bytes, hipHostMallocDefault));
+    return 0;
+}
+
+int hdfs3_host_free_pinned(void *h_ptr) {
+    HIP_TRY(hipHostFree(h_ptr));
+    return 0;
+}
+
+int hdfs3_memcpy_h2d(hdfs3_crc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes) {
+    if (!ctx) return fail(-EINVAL, "null ctx");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int hdfs3_memcpy_d2h(hdfs3_crc_ctx *ctx, void *h_dst, const void *d_src, size_t bytes) {
+    if (!ctx) return fail(-EINVAL, "null ctx");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int hdfs3_memset_dev(hdfs3_crc_ctx *ctx, void *d_dst, int value, size_t bytes) {
+    if (!ctx) return fail(-EINVAL, "null ctx");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipMemsetAsync(d_dst, value, bytes, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+}  // extern "C"
+
+// ---- measurement hooks (not part of hdfs3_crc.h; used by bench.py only) -------
+extern "C" {
+
+// Coalesced read-only stream over [d, d+len): the achievable HBM read ceiling.
+int hdfs3x_stream_read(hdfs3_crc_ctx *ctx, const void *d, size_t len, int grid, void *d_sink) {
+    if (!ctx) return fail(-EINVAL, "null ctx");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(launch_stream_read(static_cast<const uint8_t *>(d), len, static_cast<uint32_t *>(d_sink),
+                               grid > 0 ? grid : ctx->grid_cap * 8, ctx->stream));
+    return 0;
+}
+
+// The CRC kernel's chunk-per-lane access pattern without the table arithmetic.
+int hdfs3x_lane_read(hdfs3_crc_ctx *ctx, const void *d, size_t len, uint32_t bpc, void *d_sink) {
+    if (!ctx) return fail(-EINVAL, "null ctx");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(launch_lane_read(static_cast<const uint8_t *>(d), len, bpc, static_cast<uint32_t *>(d_sink),
+                             ctx->grid_cap, ctx->stream));
+    return 0;
+}
+
+int hdfs3x_grid_cap(hdfs3_crc_ctx *ctx) { return ctx ? ctx->grid_cap : 0; }
+
+}  // extern "C"

@@ -1,0 +1,185 @@
+"""Pythonic handle over the C-ABI (include/hdfs3_crc.h), for tests and the bench.
+
+Mirrors the batch semantics of the reference loops it replaces:
+  verify(..., check_short_tail=False)  RemoteBlockReader::verifyChecksum
+                                       (src/client/RemoteBlockReader.cpp:306-326)
+  verify(..., check_short_tail=True)   LocalBlockReader::readAndVerify
+                                       (src/client/LocalBlockReader.cpp:138-163)
+  compute(...)                         OutputStreamImpl::appendInternal + Packet::addChecksum
+                                       (src/client/OutputStreamImpl.cpp:298-359, Packet.cpp:73-81)
+Every call runs on the GPU; there is no host fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_int, c_int64, c_void_p
+
+import numpy as np
+
+from . import _native
+from ._native import PktDesc, check
+
+
+def _ptr(a: np.ndarray) -> int:
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    n = c_int(0)
+    check("hdfs3_device_count", _native.lib().hdfs3_device_count(byref(n)))
+    return n.value
+
+
+class DeviceBuffer:
+    """Raw HBM allocation owned by Python (hdfs3_dev_malloc/free)."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        p = c_void_p()
+        check("hdfs3_dev_malloc", _native.lib().hdfs3_dev_malloc(byref(p), max(self.nbytes, 1)))
+        self.ptr = p.value
+
+    def free(self) -> None:
+        if self.ptr:
+            _native.lib().hdfs3_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class CrcContext:
+    """One hdfs3_crc_ctx: like one Checksum instance per reader/writer in the reference."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _native.lib()
+        p = c_void_p()
+        check("hdfs3_crc_ctx_create", self._lib.hdfs3_crc_ctx_create(device, byref(p)))
+        self.ctx = p.value
+        self.device = device
+
+    def close(self) -> None:
+        if self.ctx:
+            self._lib.hdfs3_crc_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- plumbing ---------------------------------------------------------------
+    @property
+    def kernel_launches(self) -> int:
+        return int(self._lib.hdfs3_crc_ctx_kernel_launches(self.ctx))
+
+    def set_stream(self, hip_stream: int | None) -> None:
+        check("hdfs3_crc_ctx_set_stream", self._lib.hdfs3_crc_ctx_set_stream(self.ctx, hip_stream))
+
+    def synchronize(self) -> None:
+        check("hdfs3_crc_ctx_synchronize", self._lib.hdfs3_crc_ctx_synchronize(self.ctx))
+
+    def upload(self, host: np.ndarray, dev: DeviceBuffer | None = None, offset: int = 0) -> DeviceBuffer:
+        host = np.ascontiguousarray(host)
+        if dev is None:
+            dev = DeviceBuffer(host.nbytes)
+        assert offset + host.nbytes <= dev.nbytes
+        check("hdfs3_memcpy_h2d",
+              self._lib.hdfs3_memcpy_h2d(self.ctx, dev.ptr + offset, _ptr(host), host.nbytes))
+        return dev
+
+    def download(self, dev: DeviceBuffer | int, nbytes: int, offset: int = 0) -> np.ndarray:
+        out = np.empty(nbytes, dtype=np.uint8)
+        base = dev.ptr if isinstance(dev, DeviceBuffer) else int(dev)
+        check("hdfs3_memcpy_d2h", self._lib.hdfs3_memcpy_d2h(self.ctx, _ptr(out), base + offset, nbytes))
+        return out
+
+    def memset(self, dev: DeviceBuffer | int, value: int, nbytes: int, offset: int = 0) -> None:
+        base = dev.ptr if isinstance(dev, DeviceBuffer) else int(dev)
+        check("hdfs3_memset_dev", self._lib.hdfs3_memset_dev(self.ctx, base + offset, value, nbytes))
+
+    # -- host-buffer API ----------------------------------------------------------
+    def compute(self, data: np.ndarray, bpc: int) -> np.ndarray:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        n = (data.nbytes + bpc - 1) // bpc
+        out = np.zeros(4 * n, dtype=np.uint8)
+        check("hdfs3_crc32c_compute",
+              self._lib.hdfs3_crc32c_compute(self.ctx, _ptr(data), data.nbytes, bpc, _ptr(out)))
+        return out
+
+    def verify(self, data: np.ndarray, bpc: int, crc_be: np.ndarray, check_short_tail: bool = False) -> int:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        crc_be = np.ascontiguousarray(crc_be, dtype=np.uint8)
+        bad = c_int64(-2)
+        check("hdfs3_crc32c_verify",
+              self._lib.hdfs3_crc32c_verify(self.ctx, _ptr(data), data.nbytes, bpc, _ptr(crc_be),
+                                            int(check_short_tail), byref(bad)))
+        return bad.value
+
+    # -- device-resident API --------------------------------------------------------
+    def compute_dev(self, d_data: int, nbytes: int, bpc: int, d_out: int) -> None:
+        check("hdfs3_crc32c_compute_dev",
+              self._lib.hdfs3_crc32c_compute_dev(self.ctx, d_data, nbytes, bpc, d_out))
+
+    def verify_dev(self, d_data: int, nbytes: int, bpc: int, d_crc: int, check_short_tail: bool = False) -> int:
+        bad = c_int64(-2)
+        check("hdfs3_crc32c_verify_dev",
+              self._lib.hdfs3_crc32c_verify_dev(self.ctx, d_data, nbytes, bpc, d_crc,
+                                                int(check_short_tail), byref(bad)))
+        return bad.value
+
+    def verify_dev_async(self, d_data: int, nbytes: int, bpc: int, d_crc: int, d_result: int,
+                         check_short_tail: bool = False) -> None:
+        check("hdfs3_crc32c_verify_dev_async",
+              self._lib.hdfs3_crc32c_verify_dev_async(self.ctx, d_data, nbytes, bpc, d_crc,
+                                                      int(check_short_tail), d_result))
+
+    def decode_result(self, word: int) -> int:
+        return int(self._lib.hdfs3_crc_decode_result(word))
+
+    # -- packet-stream API ------------------------------------------------------------
+    @staticmethod
+    def _descs(pk) -> ctypes.Array:
+        arr = (PktDesc * len(pk))()
+        for i, (data_off, crc_off, data_len) in enumerate(pk):
+            arr[i].data_off, arr[i].crc_off, arr[i].data_len, arr[i].reserved = data_off, crc_off, data_len, 0
+        return arr
+
+    def verify_packets(self, arena: np.ndarray, pk, bpc: int, check_short_tail: bool = False):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        d = self._descs(pk)
+        bp, bc = c_int64(-2), c_int64(-2)
+        check("hdfs3_crc32c_verify_packets",
+              self._lib.hdfs3_crc32c_verify_packets(self.ctx, _ptr(arena), arena.nbytes, d, len(pk), bpc,
+                                                    int(check_short_tail), byref(bp), byref(bc)))
+        return bp.value, bc.value
+
+    def verify_packets_dev(self, d_arena: int, arena_len: int, pk, bpc: int, check_short_tail: bool = False):
+        d = self._descs(pk)
+        bp, bc = c_int64(-2), c_int64(-2)
+        check("hdfs3_crc32c_verify_packets_dev",
+              self._lib.hdfs3_crc32c_verify_packets_dev(self.ctx, d_arena, arena_len, d, len(pk), bpc,
+                                                        int(check_short_tail), byref(bp), byref(bc)))
+        return bp.value, bc.value
+
+    def compute_packets_dev(self, d_arena: int, arena_len: int, pk, bpc: int) -> None:
+        d = self._descs(pk)
+        check("hdfs3_crc32c_compute_packets_dev",
+              self._lib.hdfs3_crc32c_compute_packets_dev(self.ctx, d_arena, arena_len, d, len(pk), bpc))
+
+
+def update_host(state: int, data: bytes | np.ndarray) -> int:
+    """Checksum::update on a raw state (sub-chunk streaming shim)."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
+    return int(_native.lib().hdfs3_crc32c_update_host(state, _ptr(buf) if buf.nbytes else None, buf.nbytes))

@@ -1,0 +1,88 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads, exports every symbol
+include/hdfs3_crc.h declares, and fails loudly (no silent CPU fallback) without a GPU.
+No compute calls are made here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from util import REPO, read_checksum1, read_checksum2
+
+HEADER = os.path.join(REPO, "include", "hdfs3_crc.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hdfs3_\w+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    for must in ["hdfs3_crc_ctx_create", "hdfs3_crc32c_verify", "hdfs3_crc32c_compute",
+                 "hdfs3_crc32c_verify_dev", "hdfs3_crc32c_verify_packets", "hdfs3_crc_last_error"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from libhdfs3_amd import _native
+
+    lib = _native.load()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    # the Python binding covers exactly the header
+    assert sorted(_native.PUBLIC_API) == declared_functions()
+
+
+def test_library_is_gfx950_code_object():
+    from libhdfs3_amd import _native
+
+    blob = open(_native.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_abi_version_and_errors_without_device():
+    from libhdfs3_amd import _native
+
+    lib = _native.load()
+    assert lib.hdfs3_crc_abi_version() == 1
+    p = ctypes.c_void_p()
+    # invalid arguments are rejected before any device work
+    assert lib.hdfs3_crc32c_verify(None, None, 0, 512, None, 0, None) == -22  # -EINVAL
+    assert lib.hdfs3_crc32c_compute(None, None, 16, 0, None) == -22
+    if os.environ.get("HIP_VISIBLE_DEVICES", None) == "" or not os.path.exists("/dev/kfd"):
+        rc = lib.hdfs3_crc_ctx_create(0, ctypes.byref(p))
+        assert rc < 0 and p.value is None
+        assert lib.hdfs3_crc_last_error()
+
+
+def test_engine_refuses_without_gpu_instead_of_falling_back():
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("a GPU is visible; covered by -m gpu tests")
+    from libhdfs3_amd._native import Hdfs3CrcError
+    from libhdfs3_amd.engine import CrcContext
+
+    with pytest.raises(Hdfs3CrcError):
+        CrcContext(0)
+
+
+def test_streaming_host_shim_matches_reference_fixtures():
+    # hdfs3_crc32c_update_host = Checksum::update on a raw state (sub-chunk pieces only)
+    from libhdfs3_amd.engine import update_host
+
+    for want, s in read_checksum1():
+        assert (~update_host(0xFFFFFFFF, s)) & 0xFFFFFFFF == want
+    result, lines = read_checksum2()
+    st = 0xFFFFFFFF
+    for s in lines:
+        st = update_host(st, s)
+    assert (~st) & 0xFFFFFFFF == result
+
+
+def test_missing_library_raises(tmp_path):
+    from libhdfs3_amd import _native
+
+    with pytest.raises(ImportError):
+        _native.load(str(tmp_path / "nope.so"))

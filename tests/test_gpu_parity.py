@@ -1,0 +1,220 @@
+"""GPU parity tests: the HIP path (through the C-ABI) vs the oracle and the reference's fixtures.
+
+Bar: bit-exact CRC32C words and identical first-bad-chunk indices. Small cases are
+compared word for word with the oracle; BASELINE.json's full sizes (128 MiB block,
+1 GiB stream, bpc 512/2048/4096) are compared word for word as well (the C oracle
+is fast enough) plus compute->verify round trips and single-bit corruption.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from util import (GOLDEN, oracle, oracle_compute, oracle_verify, ptr, read_checksum1, read_checksum2,
+                  splitmix_bytes)
+
+pytestmark = pytest.mark.gpu
+
+GOLD = np.load(os.path.join(GOLDEN, "ref_hwcrc32c.npz"))
+META = json.load(open(os.path.join(GOLDEN, "ref_hwcrc32c.json")))
+
+
+def test_reference_kats_checksum1_on_gpu(gpu_ctx):
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    cases = read_checksum1()
+    dbuf = DeviceBuffer(4096 + 64)
+    dout = DeviceBuffer(64)
+    for want, s in cases:
+        a = np.frombuffer(s, dtype=np.uint8)
+        # host API: one short chunk
+        assert gpu_ctx.compute(a, 4096).view(">u4")[0] == want
+        # device API at the 8 alignments of TestChecksum.cpp:92-99 (generic kernel)
+        for j in range(8):
+            gpu_ctx.upload(a, dbuf, offset=j)
+            gpu_ctx.compute_dev(dbuf.ptr + j, len(s), 4096, dout.ptr)
+            assert gpu_ctx.download(dout, 4).view(">u4")[0] == want, (len(s), j)
+
+
+def test_reference_checksum2_streamed_total_on_gpu(gpu_ctx):
+    # the streamed total is one CRC over the concatenation of every line
+    result, lines = read_checksum2()
+    blob = np.frombuffer(b"".join(lines), dtype=np.uint8)
+    assert gpu_ctx.compute(blob, (blob.nbytes + 3) // 4 * 4).view(">u4")[0] == result
+
+
+@pytest.mark.parametrize("bpc", [512, 2048, 4096])
+def test_bpc_fixture_host_and_device(gpu_ctx, bpc):
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    big = splitmix_bytes(1 << 20, META["seeds"]["bpc"])
+    want = GOLD[f"bpc{bpc}"]
+    assert np.array_equal(gpu_ctx.compute(big, bpc), want)
+    d = gpu_ctx.upload(big)
+    dc = DeviceBuffer(want.nbytes)
+    gpu_ctx.compute_dev(d.ptr, big.nbytes, bpc, dc.ptr)
+    assert np.array_equal(gpu_ctx.download(dc, want.nbytes), want)
+    assert gpu_ctx.verify(big, bpc, want, False) == -1
+    assert gpu_ctx.verify_dev(d.ptr, big.nbytes, bpc, dc.ptr, True) == -1
+
+
+def test_packet_fixture_verify_semantics(gpu_ctx):
+    pkt = splitmix_bytes(65536, META["seeds"]["packet"])
+    crc = GOLD["pkt_crc"]
+    v = META["verify"]
+    assert gpu_ctx.verify(pkt, 512, crc, False) == v["clean_remote"]
+    bad = pkt.copy()
+    bad[META["packet"]["flip_byte"]] ^= META["packet"]["flip_mask"]
+    assert gpu_ctx.verify(bad, 512, crc, False) == v["flip77_remote"]
+    assert gpu_ctx.verify(bad, 512, crc, True) == v["flip77_local"]
+    n = META["packet"]["tail_len"]
+    tail = GOLD["tail_crc"]
+    corrupt = tail.copy()
+    corrupt[4 * 127] ^= 0xFF
+    assert np.array_equal(gpu_ctx.compute(pkt[:n], 512), tail)
+    assert gpu_ctx.verify(pkt[:n], 512, tail, True) == v["tail_clean_local"]
+    assert gpu_ctx.verify(pkt[:n], 512, corrupt, False) == v["tail_corrupt_remote"]
+    assert gpu_ctx.verify(pkt[:n], 512, corrupt, True) == v["tail_corrupt_local"]
+
+
+@pytest.mark.parametrize("bpc", [4, 12, 64, 500, 512, 516, 1024, 2048, 4096, 65536])
+def test_ragged_lengths_vs_oracle(gpu_ctx, bpc):
+    rng = np.random.default_rng(bpc)
+    for n in [0, 1, 3, bpc - 1, bpc, bpc + 1, 3 * bpc + 7] + [int(x) for x in rng.integers(0, 300_000, 6)]:
+        if n < 0:
+            continue
+        data = splitmix_bytes(n, 1000 + n)
+        want = oracle_compute(data, bpc)
+        got = gpu_ctx.compute(data, bpc)
+        assert np.array_equal(got, want), (bpc, n)
+        assert gpu_ctx.verify(data, bpc, want, True) == -1
+        if n:
+            k = int(rng.integers(0, n))
+            bad = data.copy()
+            bad[k] ^= 0x40
+            for tail in (False, True):
+                assert gpu_ctx.verify(bad, bpc, want, tail) == oracle_verify(bad, bpc, want, tail), (bpc, n, k, tail)
+
+
+@pytest.mark.parametrize("offset", [1, 2, 3, 4, 8, 12])
+def test_unaligned_device_pointers(gpu_ctx, offset):
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    data = splitmix_bytes(513 * 97 + 5, offset)
+    d = DeviceBuffer(data.nbytes + 64)
+    gpu_ctx.upload(data, d, offset=offset)
+    for bpc in (512, 2048, 516):
+        want = oracle_compute(data, bpc)
+        dc = DeviceBuffer(want.nbytes + 8)
+        gpu_ctx.compute_dev(d.ptr + offset, data.nbytes, bpc, dc.ptr + 1)  # unaligned CRC array too
+        assert np.array_equal(gpu_ctx.download(dc, want.nbytes, offset=1), want), (offset, bpc)
+        assert gpu_ctx.verify_dev(d.ptr + offset, data.nbytes, bpc, dc.ptr + 1, True) == -1
+
+
+def _wire_arena(n_pkts, bpc, rng, short_last=True):
+    """Build an arena of HDFS data packets in wire order: [31 B header][BE CRCs][data]
+    (RemoteBlockReader.cpp:240-245); descriptors point at the CRC and data regions."""
+    parts, descs, off = [], [], 0
+    for p in range(n_pkts):
+        data_len = 65536 if not (short_last and p == n_pkts - 1) else int(rng.integers(1, 65536))
+        data = splitmix_bytes(data_len, 77 + p)
+        crc = oracle_compute(data, bpc)
+        hdr = np.zeros(31, np.uint8)
+        crc_off = off + 31
+        data_off = crc_off + crc.nbytes
+        parts += [hdr, crc, data]
+        descs.append((data_off, crc_off, data_len))
+        off = data_off + data_len
+    return np.concatenate(parts), descs
+
+
+@pytest.mark.parametrize("bpc", [512, 4096])
+def test_packets_api(gpu_ctx, bpc):
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    rng = np.random.default_rng(bpc)
+    arena, pk = _wire_arena(17, bpc, rng)
+    assert gpu_ctx.verify_packets(arena, pk, bpc) == (-1, -1)
+    bad = arena.copy()
+    d_off, _, _ = pk[5]
+    bad[d_off + 3 * bpc + 11] ^= 1
+    bad[pk[9][0] + 2] ^= 1
+    assert gpu_ctx.verify_packets(bad, pk, bpc) == (5, 3)
+    # corrupt the short tail chunk's CRC of the last packet: remote ignores, local flags
+    last = len(pk) - 1
+    data_off, crc_off, data_len = pk[last]
+    nchunks = (data_len + bpc - 1) // bpc
+    if data_len % bpc:
+        t = arena.copy()
+        t[crc_off + 4 * (nchunks - 1)] ^= 0x10
+        assert gpu_ctx.verify_packets(t, pk, bpc, False) == (-1, -1)
+        assert gpu_ctx.verify_packets(t, pk, bpc, True) == (last, nchunks - 1)
+    # device-resident arena + compute in place (write path)
+    d = gpu_ctx.upload(arena)
+    assert gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc) == (-1, -1)
+    wiped = arena.copy()
+    for data_off, crc_off, data_len in pk:
+        wiped[crc_off:data_off] = 0
+    d2 = gpu_ctx.upload(wiped)
+    gpu_ctx.compute_packets_dev(d2.ptr, wiped.nbytes, pk, bpc)
+    assert np.array_equal(gpu_ctx.download(d2, arena.nbytes), arena)
+
+
+@pytest.mark.parametrize("bpc", [512, 2048, 4096])
+def test_full_size_stream_1gib_roundtrip(gpu_ctx, bpc):
+    """Config 3: 1 GiB stream, compute (write) then verify (read); every CRC word checked."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    n = 1 << 30
+    data = splitmix_bytes(n, 0xB10C + bpc)
+    d = gpu_ctx.upload(data)
+    nc = n // bpc
+    dc = DeviceBuffer(4 * nc)
+    gpu_ctx.compute_dev(d.ptr, n, bpc, dc.ptr)
+    got = gpu_ctx.download(dc, 4 * nc)
+    assert np.array_equal(got, oracle_compute(data, bpc))
+    assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, False) == -1
+    for k in (0, nc // 2 + 3, nc - 1):
+        pos = k * bpc + (k % bpc)
+        flipped = np.array([data[pos] ^ 0x80], dtype=np.uint8)
+        gpu_ctx.upload(flipped, d, offset=pos)
+        assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, False) == k
+        gpu_ctx.upload(data[pos:pos + 1], d, offset=pos)
+    assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, True) == -1
+
+
+def test_block_128mib_async_result_and_launch_count(gpu_ctx):
+    """Config 2: one 128 MiB block, 512 B chunks, device-resident async verify."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    n = 128 << 20
+    data = splitmix_bytes(n, 0x128)
+    crc = oracle_compute(data, 512)
+    d = gpu_ctx.upload(data)
+    dc = gpu_ctx.upload(crc)
+    res = DeviceBuffer(8 * 4)
+    gpu_ctx.memset(res, 0, 32)
+    before = gpu_ctx.kernel_launches
+    gpu_ctx.verify_dev_async(d.ptr, n, 512, dc.ptr, res.ptr)
+    bad = crc.copy()
+    bad[4 * 1000 + 2] ^= 4
+    bad[4 * 200000] ^= 4
+    dbad = gpu_ctx.upload(bad)
+    gpu_ctx.verify_dev_async(d.ptr, n, 512, dbad.ptr, res.ptr + 8)
+    gpu_ctx.synchronize()
+    words = gpu_ctx.download(res, 32).view(np.uint64)
+    assert gpu_ctx.decode_result(int(words[0])) == -1 and words[0] == 0
+    assert gpu_ctx.decode_result(int(words[1])) == 1000
+    assert gpu_ctx.kernel_launches == before + 2
+
+
+def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
+    """CRC32C detects every single-bit error: flip each of the 4096 bits of chunk 3."""
+    data = splitmix_bytes(8 * 512, 5)
+    crc = oracle_compute(data, 512)
+    for byte in range(0, 512, 7):
+        for bit in (0, 3, 7):
+            bad = data.copy()
+            bad[3 * 512 + byte] ^= 1 << bit
+            assert gpu_ctx.verify(bad, 512, crc, True) == 3
