@@ -236,7 +236,11 @@ def main():
 
     from libhdfs3_amd.engine import CrcContext
     ctx = CrcContext(local)
-    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    # One explicit stream for the kernels and the HIP events that time them (the
+    # default stream's handle is 0, which the C-ABI reads as "use the ctx stream").
+    stream = torch.cuda.Stream(device=device)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
 
     block_bytes = args.block_mib << 20
     work = Workload(torch, ctx, device, block_bytes, args.blocks, args.bpc, seed=1234 + rank)

@@ -32,7 +32,7 @@ struct DevPacket {
 };
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
-                         int grid_cap, hipStream_t stream);
+                         const uint32_t *d_fold, int grid_cap, hipStream_t stream);
 
 hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_t n,
                           uint32_t bpc, bool verify, int check_short_tail,

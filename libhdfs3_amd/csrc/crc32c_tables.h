@@ -27,4 +27,49 @@ inline void build_slice_tables(uint32_t out[kSlices][kTableEntries]) {
             out[k][i] = out[0][out[k - 1][i] & 0xFFu] ^ (out[k - 1][i] >> 8);
 }
 
+// GF(2)-linear "advance the raw CRC state over n zero bytes" as a 32x32 bit matrix
+// stored by columns: shift(x) = XOR of cols[i] over the set bits i of x. Used to fold
+// partial CRCs of consecutive segments: crc(A||B) = shift_|B|(crc(A)) ^ crc0(B).
+inline uint32_t advance_bytes(const uint32_t t0[kTableEntries], uint32_t s, uint64_t n) {
+    while (n--) s = t0[s & 0xFFu] ^ (s >> 8);
+    return s;
+}
+
+inline uint32_t apply_cols(const uint32_t cols[32], uint32_t x) {
+    uint32_t y = 0;
+    for (int i = 0; i < 32; ++i)
+        if ((x >> i) & 1u) y ^= cols[i];
+    return y;
+}
+
+inline void shift_cols(const uint32_t t0[kTableEntries], uint64_t n, uint32_t cols[32]) {
+    for (int i = 0; i < 32; ++i) cols[i] = advance_bytes(t0, 1u << i, n);
+}
+
+// Lane-fold matrices for the round kernel: for G lanes per chunk (64-byte segments),
+// lane j's partial state is advanced over (G-1-j)*64 bytes. Sets for G = 8,16,32,64
+// are packed at word offsets kFoldOffset[g]*32; the 4096-byte advance (round-to-round
+// combine for bpc > 4096) follows at kFoldAdvance4096.
+constexpr int kFoldGs[4] = {8, 16, 32, 64};
+constexpr int kFoldOffset[4] = {0, 8, 24, 56};
+constexpr int kFoldAdvance4096 = 120 * 32;
+constexpr int kFoldWords = kFoldAdvance4096 + 32;
+
+inline int fold_set_index(int g) { return g == 8 ? 0 : g == 16 ? 1 : g == 32 ? 2 : 3; }
+
+inline void build_fold_matrices(const uint32_t t0[kTableEntries], uint32_t out[kFoldWords]) {
+    uint32_t f64[32];
+    shift_cols(t0, 64, f64);
+    for (int s = 0; s < 4; ++s) {
+        const int g = kFoldGs[s];
+        uint32_t m[32];
+        for (int i = 0; i < 32; ++i) m[i] = 1u << i;  // identity: lane g-1 needs no advance
+        for (int j = g - 1; j >= 0; --j) {
+            for (int i = 0; i < 32; ++i) out[(kFoldOffset[s] + j) * 32 + i] = m[i];
+            for (int i = 0; i < 32; ++i) m[i] = apply_cols(f64, m[i]);
+        }
+    }
+    shift_cols(t0, 4096, out + kFoldAdvance4096);
+}
+
 }  // namespace hdfs3crc

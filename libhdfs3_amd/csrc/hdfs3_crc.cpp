@@ -71,6 +71,7 @@ struct hdfs3_crc_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     uint32_t *d_tables = nullptr;  // 4 x 256 slice-table image
+    uint32_t *d_fold = nullptr;    // lane-fold GF(2) matrices (crc32c_tables.h)
     unsigned long long *d_result = nullptr;
     unsigned long long *h_result = nullptr;  // pinned
     DevPacket *d_pk = nullptr;
@@ -146,7 +147,7 @@ int finish_pending(Slot &s) {
 }
 
 int launch(hdfs3_crc_ctx *ctx, const ChunkLaunch &a, bool verify) {
-    HIP_TRY(launch_chunks(a, verify, ctx->d_tables, ctx->grid_cap, ctx->stream));
+    HIP_TRY(launch_chunks(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
     ++ctx->launches;
     return 0;
 }
@@ -292,6 +293,12 @@ int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out) {
         return bail(fail(-ENOMEM, "device allocation for ctx failed"));
     if (hipMemcpy(ctx->d_tables, t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(-EIO, "table upload failed"));
+    static uint32_t fold[kFoldWords];
+    static std::once_flag fold_once;
+    std::call_once(fold_once, [&] { build_fold_matrices(t[0], fold); });
+    if (hipMalloc(reinterpret_cast<void **>(&ctx->d_fold), sizeof(fold)) != hipSuccess ||
+        hipMemcpy(ctx->d_fold, fold, sizeof(fold), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(-ENOMEM, "fold-matrix upload failed"));
     *out = ctx;
     return 0;
 }
@@ -310,6 +317,7 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx) {
     if (ctx->d_pk) (void)hipFree(ctx->d_pk);
     if (ctx->h_pk) (void)hipHostFree(ctx->h_pk);
     if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+    if (ctx->d_fold) (void)hipFree(ctx->d_fold);
     if (ctx->d_result) (void)hipFree(ctx->d_result);
     if (ctx->h_result) (void)hipHostFree(ctx->h_result);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
