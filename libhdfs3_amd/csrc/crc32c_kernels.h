@@ -39,6 +39,9 @@ hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_
                           unsigned long long *result, const uint32_t *d_tables, int grid_cap,
                           hipStream_t stream);
 
+// Measurement knob: selects kernel variants for in-process A/B (0 = production).
+void set_variant(int v);
+
 // Measurement-only kernels (bench/profiling): HBM read ceiling and the CRC
 // kernel's access pattern without the table arithmetic.
 hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,

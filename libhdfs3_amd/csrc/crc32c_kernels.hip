@@ -315,6 +315,18 @@ __device__ __forceinline__ uint32_t gf2_apply(const uint32_t (&col)[32], uint32_
     return y;
 }
 
+// Same product, 4 independent accumulators and one v_bitop3 (y ^ (m & col), truth
+// table 0x78 over {S0,S1,S2}) per bit: 64 VALU in chains of 8 instead of 96 in one chain.
+__device__ __forceinline__ uint32_t gf2_apply4(const uint32_t (&col)[32], uint32_t x) {
+    uint32_t y[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t m = uint32_t(int32_t(x << (31 - i)) >> 31);
+        y[i & 3] = __builtin_amdgcn_bitop3_b32(y[i & 3], m, col[i], 0x78);
+    }
+    return xor3(y[0], y[1], y[2]) ^ y[3];
+}
+
 template <int DPP>
 __device__ __forceinline__ uint32_t dpp_xor(uint32_t v) {
     return v ^ uint32_t(__builtin_amdgcn_update_dpp(0, int(v), DPP, 0xF, 0xF, false));
@@ -341,7 +353,7 @@ __device__ __forceinline__ uint32_t group_xor(uint32_t v) {
     return v;
 }
 
-template <int BPC, bool VERIFY>
+template <int BPC, bool VERIFY, int DEPTH, bool FOLD4>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_rounds_kernel(ChunkLaunch a,
                                                                       const uint32_t *__restrict__ g_tab,
                                                                       const uint32_t *__restrict__ g_fold) {
@@ -358,73 +370,94 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_rounds_kernel(ChunkLaunc
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
     const uint64_t nunits = a.len / kUnit;
     const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
-    uint64_t unit = uint64_t(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+    // this wave's rounds: k = 0..K-1 -> unit wave + (k / RPU) * nwaves, sub-round k % RPU
+    const uint64_t my_units = wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0;
+    const uint64_t K = my_units * kRoundsPerUnit;
     const bool crc_al4 = (reinterpret_cast<uintptr_t>(VERIFY ? a.crc_be : a.out_be) & 3u) == 0;
+    // byte offset of round k; rounds past the end re-read the wave's last round
+    // (cache-resident) so every prefetch stays unconditional
+    auto round_ptr = [&](uint64_t k) -> const uint8_t * {
+        if (K == 0) return a.data;  // host guarantees nunits >= 1; idle wave reads unit 0
+        const uint64_t kk = k < K ? k : K - 1;
+        return a.data + (wave + (kk / kRoundsPerUnit) * nwaves) * kUnit + (kk % kRoundsPerUnit) * kRoundBytes;
+    };
 
-    uint32_t tv[kFillPerThread];
-    fetch_tables(tv, g_tab);
-    Round cur;
-    {
-        const uint64_t u0 = unit < nunits ? unit : nunits - 1;  // host guarantees nunits >= 1
-        load_round(cur, a.data + u0 * kUnit, lane_off);
-    }
+    // small cache-resident reads first (tables, fold columns), then the first two
+    // rounds: the in-order vmcnt then lets the table fill proceed while rounds land
     uint32_t col[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) col[i] = g_fold[(kFoldOff[kFoldSet] + j) * 32 + i];
+    uint32_t tv[kFillPerThread];
+    fetch_tables(tv, g_tab);
+    __builtin_amdgcn_sched_barrier(0);
+    Round b0, b1, b2;
+    load_round(b0, round_ptr(0), lane_off);
+    if constexpr (DEPTH == 2) load_round(b1, round_ptr(1), lane_off);
     __builtin_amdgcn_sched_barrier(0);
     store_tables(lds, tv);
     lds_barrier();
     const Lut t(lds);
 
-    for (; unit < nunits; unit += nwaves) {
-        const uint8_t *ubase = a.data + unit * kUnit;
+    uint32_t acc = 0;
+    // One round: issue the stored CRC word and the prefetch of round k+DEPTH into
+    // `pf`, then consume `cur`.
+    auto step = [&](Round &cur, Round &pf, uint64_t k) {
+        const uint32_t r = uint32_t(k % kRoundsPerUnit);
+        const uint64_t unit = wave + (k / kRoundsPerUnit) * nwaves;
         const uint64_t chunk = unit * kChunksPerUnit + lane / G;
         uint32_t want = 0;
-        // every lane of the chunk reads its word (same address: one broadcast access),
-        // keeping the load out of a branch so it is not waited for on the spot
-        if constexpr (VERIFY) want = *reinterpret_cast<const uint32_t *>(a.crc_be + 4 * chunk);
-        const uint64_t next_unit = unit + nwaves < nunits ? unit + nwaves : unit;
-        uint32_t acc = 0;
-#pragma unroll 1
-        for (int r = 0; r < kRoundsPerUnit; ++r) {
-            Round nxt;
-            // next round: this unit's next one, else the next unit's first (this
-            // unit's first again when none is left, keeping the loads unconditional)
-            const uint8_t *nbase = r + 1 < kRoundsPerUnit ? ubase + (r + 1) * kRoundBytes
-                                                          : a.data + next_unit * kUnit;
-            load_round(nxt, nbase, lane_off);
-            __builtin_amdgcn_sched_barrier(0);
-            regroup(cur);
-            uint32_t x = ((j == 0 && r == 0) ? 0xFFFFFFFFu : 0u) ^ cur.w[0][0];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                x = t.word(x, cur.w[q][1]);
-                x = t.word(x, cur.w[q][2]);
-                x = t.word(x, cur.w[q][3]);
-                x = t.word(x, q < 3 ? cur.w[q < 3 ? q + 1 : 3][0] : 0u);
-            }
-            uint32_t y = group_xor<G>(gf2_apply(col, x));
-            if constexpr (kRoundsPerUnit > 1) {
-                if (r > 0) {
-                    uint32_t k4096[32];
-#pragma unroll
-                    for (int i = 0; i < 32; ++i) k4096[i] = g_fold[kFoldAdvance4096 + i];
-                    y ^= gf2_apply(k4096, acc);
-                }
-                acc = y;
-            } else {
-                acc = y;
-            }
-            cur = nxt;
+        if constexpr (VERIFY) {
+            // every lane of a chunk reads its word (one broadcast access), issued before
+            // the prefetch so that waiting for it never drains the prefetch (vmcnt is in-order)
+            want = *reinterpret_cast<const uint32_t *>(a.crc_be + 4 * chunk);
         }
-        const uint32_t c = ~acc;
-        if (j == 0) {
+        load_round(pf, round_ptr(k + DEPTH), lane_off);
+        __builtin_amdgcn_sched_barrier(0);
+        regroup(cur);
+        uint32_t x = ((j == 0 && r == 0) ? 0xFFFFFFFFu : 0u) ^ cur.w[0][0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            x = t.word(x, cur.w[q][1]);
+            x = t.word(x, cur.w[q][2]);
+            x = t.word(x, cur.w[q][3]);
+            x = t.word(x, q < 3 ? cur.w[q < 3 ? q + 1 : 3][0] : 0u);
+        }
+        uint32_t y = group_xor<G>(FOLD4 ? gf2_apply4(col, x) : gf2_apply(col, x));
+        if constexpr (kRoundsPerUnit > 1) {
+            if (r > 0) {
+                uint32_t k4096[32];
+#pragma unroll
+                for (int i = 0; i < 32; ++i) k4096[i] = g_fold[kFoldAdvance4096 + i];
+                y ^= gf2_apply(k4096, acc);
+            }
+        }
+        acc = y;
+        if (r == kRoundsPerUnit - 1 && j == 0) {
+            const uint32_t c = ~acc;
             if constexpr (VERIFY) {
                 if (__builtin_bswap32(want) != c)
                     atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
             } else {
                 *reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk) = __builtin_bswap32(c);
             }
+        }
+    };
+    // (DEPTH+1)-buffer ring unrolled so the buffers rotate by renaming (a loop-carried
+    // register copy would make the compiler wait for the youngest prefetch)
+    if constexpr (DEPTH == 2) {
+        for (uint64_t k = 0; k < K; k += 3) {
+            step(b0, b2, k);
+            if (k + 1 >= K) break;
+            step(b1, b0, k + 1);
+            if (k + 2 >= K) break;
+            step(b2, b1, k + 2);
+        }
+    } else {
+        for (uint64_t k = 0; k < K; k += 2) {
+            step(b0, b1, k);
+            if (k + 1 >= K) break;
+            step(b1, b0, k + 1);
         }
     }
 
@@ -434,6 +467,187 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_rounds_kernel(ChunkLaunc
     const uint64_t first_slow = nunits * kChunksPerUnit;
     const uint64_t nslow = nfull - first_slow + (a.len % BPC ? 1 : 0);
     const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
+    if (gtid < nslow) {
+        const uint64_t chunk = first_slow + gtid;
+        const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(a.len % BPC);
+        const uint32_t c = ~crc_run_any(t, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
+        if constexpr (VERIFY) {
+            if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(a.crc_be + 4 * chunk, crc_al4) != c)
+                atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
+        } else {
+            store_be32(a.out_be + 4 * chunk, c, crc_al4);
+        }
+    }
+}
+
+// ---- wave kernel: round kernel + LDS nibble fold + optional 2-chain interleave ----
+//
+// Same rounds/regroup as crc32c_rounds_kernel, two changes:
+//  * the lane fold M_j (advance over (G-1-j)*64 bytes) reads lane-specific nibble
+//    tables kept in the last 32 KiB of LDS (word ((k*16+e)*64 + lane): each lane its
+//    own bank): 8 lookups + ~19 VALU instead of a 32-column product in VGPRs;
+//  * PAIR = 2 consumes two rounds per step with their lookup chains software-
+//    pipelined (sched_barrier-pinned phases: chain 1's 4 reads fly while chain 0
+//    folds its previous 4), so each lane keeps two LDS round trips in flight.
+constexpr int kFoldLdsOff = kLdsBytes;                  // byte offset of the nibble tables
+constexpr int kLdsBytesWave = kLdsBytes + 32 * 1024;    // 160 KiB: the whole CU LDS
+
+struct NibFold {
+    const uint8_t *f;  // lds + kFoldLdsOff + lane*4
+    __device__ __forceinline__ explicit NibFold(const uint32_t *lds)
+        : f(reinterpret_cast<const uint8_t *>(lds) + kFoldLdsOff + 4 * (threadIdx.x & 63)) {}
+    __device__ __forceinline__ uint32_t ld(uint32_t off) const {
+        return *reinterpret_cast<const uint32_t *>(f + off);
+    }
+    __device__ __forceinline__ uint32_t apply(uint32_t x) const {
+        const uint32_t a0 = ld(((x << 8) & 0xF00u) + 0 * 4096);
+        const uint32_t a1 = ld(((x << 4) & 0xF00u) + 1 * 4096);
+        const uint32_t a2 = ld((x & 0xF00u) + 2 * 4096);
+        const uint32_t a3 = ld(((x >> 4) & 0xF00u) + 3 * 4096);
+        const uint32_t a4 = ld(((x >> 8) & 0xF00u) + 4 * 4096);
+        const uint32_t a5 = ld(((x >> 12) & 0xF00u) + 5 * 4096);
+        const uint32_t a6 = ld(((x >> 16) & 0xF00u) + 6 * 4096);
+        const uint32_t a7 = ld(((x >> 20) & 0xF00u) + 7 * 4096);
+        return xor3(xor3(a0, a1, a2), xor3(a3, a4, a5), a6 ^ a7);
+    }
+};
+
+// The 4 table reads of one word step, and their fold into the next state.
+struct Look {
+    uint32_t v[4];
+};
+__device__ __forceinline__ Look lookups(const Lut &t, uint32_t x) {
+    Look l;
+    l.v[0] = t.at<0>(3, x);
+    l.v[1] = t.at<1>(2, x);
+    l.v[2] = t.at<2>(1, x);
+    l.v[3] = t.at<3>(0, x);
+    return l;
+}
+__device__ __forceinline__ uint32_t combine(const Look &l, uint32_t next) {
+    return xor3(xor3(l.v[0], l.v[1], l.v[2]), l.v[3], next);
+}
+
+template <int BPC, bool VERIFY, int PAIR>
+__global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a,
+                                                                    const uint32_t *__restrict__ g_tab,
+                                                                    const uint32_t *__restrict__ g_nib) {
+    static_assert(BPC <= kRoundBytes, "one-round units only");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytesWave / 4];
+    constexpr int G = BPC / 64;
+    constexpr int kChunksPerUnit = kRoundBytes / BPC;
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t j = lane % G;
+    const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
+    const uint64_t nunits = a.len / kRoundBytes;
+    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
+    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+    const uint64_t K = wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0;
+    auto round_ptr = [&](uint64_t k) -> const uint8_t * {
+        if (K == 0) return a.data;
+        const uint64_t kk = k < K ? k : K - 1;
+        return a.data + (wave + kk * nwaves) * kRoundBytes;
+    };
+
+    // table + nibble-image words, then the first round(s), then the LDS fill
+    uint32_t tv[kFillPerThread];
+    fetch_tables(tv, g_tab);
+    const u32x4 n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
+    const u32x4 n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+    __builtin_amdgcn_sched_barrier(0);
+    Round b[2 * PAIR];
+#pragma unroll
+    for (int i = 0; i < PAIR; ++i) load_round(b[i], round_ptr(i), lane_off);
+    __builtin_amdgcn_sched_barrier(0);
+    store_tables(lds, tv);
+    {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * threadIdx.x;
+        dst[0] = n0;
+        dst[1] = n1;
+    }
+    lds_barrier();
+    const Lut t(lds);
+    const NibFold nf(lds);
+    const uint32_t init = j == 0 ? 0xFFFFFFFFu : 0u;
+
+    auto want_of = [&](uint64_t k) -> uint32_t {
+        if constexpr (VERIFY) {
+            const uint64_t kk = k < K ? k : K - 1;
+            const uint64_t chunk = (wave + kk * nwaves) * kChunksPerUnit + lane / G;
+            return *reinterpret_cast<const uint32_t *>(a.crc_be + 4 * chunk);
+        }
+        return 0;
+    };
+    auto finish = [&](uint64_t k, uint32_t y, uint32_t want) {
+        if (k >= K || j != 0) return;
+        const uint64_t chunk = (wave + k * nwaves) * kChunksPerUnit + lane / G;
+        const uint32_t c = ~y;
+        if constexpr (VERIFY) {
+            if (__builtin_bswap32(want) != c) atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
+        } else {
+            *reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk) = __builtin_bswap32(c);
+        }
+    };
+    // word i (0..15) of the lane's 64-byte segment after regroup
+    auto word = [](const Round &r, int i) -> uint32_t { return r.w[i >> 2][i & 3]; };
+
+    if constexpr (PAIR == 1) {
+        auto step = [&](Round &cur, Round &pf, uint64_t k) {
+            const uint32_t w = want_of(k);
+            load_round(pf, round_ptr(k + 1), lane_off);
+            __builtin_amdgcn_sched_barrier(0);
+            regroup(cur);
+            uint32_t x = init ^ word(cur, 0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x = combine(lookups(t, x), i < 15 ? word(cur, i < 15 ? i + 1 : 15) : 0u);
+            finish(k, group_xor<G>(nf.apply(x)), w);
+        };
+        for (uint64_t k = 0; k < K; k += 2) {
+            step(b[0], b[1], k);
+            if (k + 1 >= K) break;
+            step(b[1], b[0], k + 1);
+        }
+    } else {
+        auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint64_t k) {
+            const uint32_t w0 = want_of(k), w1 = want_of(k + 1);
+            load_round(p0, round_ptr(k + 2), lane_off);
+            load_round(p1, round_ptr(k + 3), lane_off);
+            __builtin_amdgcn_sched_barrier(0);
+            regroup(c0);
+            regroup(c1);
+            uint32_t x0 = init ^ word(c0, 0), x1 = init ^ word(c1, 0);
+            Look l0 = lookups(t, x0), l1;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                l1 = lookups(t, x1);
+                __builtin_amdgcn_sched_barrier(0);
+                x0 = combine(l0, i < 15 ? word(c0, i < 15 ? i + 1 : 15) : 0u);
+                __builtin_amdgcn_sched_barrier(0);
+                if (i < 15) l0 = lookups(t, x0);
+                __builtin_amdgcn_sched_barrier(0);
+                x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const uint32_t y0 = group_xor<G>(nf.apply(x0));
+            const uint32_t y1 = group_xor<G>(nf.apply(x1));
+            finish(k, y0, w0);
+            finish(k + 1, y1, w1);
+        };
+        for (uint64_t k = 0; k < K; k += 4) {
+            step(b[0], b[1], b[2], b[3], k);
+            if (k + 2 >= K) break;
+            step(b[2], b[3], b[0], b[1], k + 2);
+        }
+    }
+
+    // slow region: chunks after the last whole round, plus the short tail chunk
+    const uint64_t nfull = a.len / BPC;
+    const uint64_t first_slow = nunits * kChunksPerUnit;
+    const uint64_t nslow = nfull - first_slow + (a.len % BPC ? 1 : 0);
+    const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
+    const bool crc_al4 = (reinterpret_cast<uintptr_t>(VERIFY ? a.crc_be : a.out_be) & 3u) == 0;
     if (gtid < nslow) {
         const uint64_t chunk = first_slow + gtid;
         const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(a.len % BPC);
@@ -569,16 +783,61 @@ hipError_t launch_t(const ChunkLaunch &a, const uint32_t *tab, int grid, hipStre
     return hipGetLastError();
 }
 
-template <int BPC, bool V>
-hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
-                    hipStream_t s) {
+int g_variant = 0;  // measurement knob (hdfs3x_set_variant); 0 = production choice
+
+template <int BPC, bool V, int DEPTH, bool FOLD4>
+hipError_t launch_r3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
+                     hipStream_t s) {
     constexpr uint64_t kUnit = BPC <= kRoundBytes ? kRoundBytes : BPC;
     const uint64_t units = a.len / kUnit;
     const uint64_t need = (units + kWavesPerBlock - 1) / kWavesPerBlock;
     const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
-    hipLaunchKernelGGL((crc32c_rounds_kernel<BPC, V>), dim3(grid), dim3(kBlockThreads), 0, s, a, tab,
-                       fold);
+    hipLaunchKernelGGL((crc32c_rounds_kernel<BPC, V, DEPTH, FOLD4>), dim3(grid), dim3(kBlockThreads), 0, s,
+                       a, tab, fold);
     return hipGetLastError();
+}
+
+template <int BPC, bool V, int PAIR>
+hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
+                       hipStream_t s) {
+    if constexpr (BPC > kRoundBytes) {
+        return launch_r3<BPC, V, 1, true>(a, tab, fold, grid_cap, s);
+    } else {
+        constexpr int G = BPC / 64;
+        constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
+        const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
+        const uint64_t units = a.len / kRoundBytes;
+        const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
+        const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
+        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR>), dim3(grid), dim3(kBlockThreads), 0, s, a, tab,
+                           nib);
+        return hipGetLastError();
+    }
+}
+
+template <int BPC, bool V>
+hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
+                    hipStream_t s) {
+    // Production path (variant 0): the wave kernel with the LDS nibble fold and two
+    // software-pipelined chains per lane (bpc <= 4096), the round kernel above that.
+    // Other values select earlier designs for in-process A/B (tools/ab.py).
+    switch (g_variant) {
+    case 1: return launch_r3<BPC, V, 1, false>(a, tab, fold, grid_cap, s);   // first round kernel
+    case 2: return launch_r3<BPC, V, 1, true>(a, tab, fold, grid_cap, s);    // + bitop3 fold
+    case 3: return launch_r3<BPC, V, 2, true>(a, tab, fold, grid_cap, s);    // + 2-deep prefetch
+    case 4: return launch_wave<BPC, V, 1>(a, tab, fold, grid_cap, s);        // nibble fold, 1 chain
+    case 9: {  // diagnostic: full grid, LDS fill + barrier, no rounds (per-launch fixed cost)
+        ChunkLaunch e = a;
+        e.len = 0;
+        constexpr int G = BPC <= kRoundBytes ? BPC / 64 : 64;
+        constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
+        if constexpr (BPC <= kRoundBytes)
+            hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, 1>), dim3(grid_cap), dim3(kBlockThreads), 0, s, e,
+                               tab, fold + kFoldWords + set * kFoldNibbleWords);
+        return hipGetLastError();
+    }
+    default: return launch_wave<BPC, V, 2>(a, tab, fold, grid_cap, s);
+    }
 }
 
 template <int BPC>
@@ -632,6 +891,8 @@ hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_
                            result, d_tables);
     return hipGetLastError();
 }
+
+void set_variant(int v) { g_variant = v; }
 
 hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,
                               hipStream_t stream) {

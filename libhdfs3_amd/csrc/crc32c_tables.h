@@ -72,4 +72,19 @@ inline void build_fold_matrices(const uint32_t t0[kTableEntries], uint32_t out[k
     shift_cols(t0, 4096, out + kFoldAdvance4096);
 }
 
+// Lane-specific fold as LDS nibble tables (the round kernels' fold): for each of the
+// 64 lanes of a wave, lane j = lane % G, nibble k (0..7) and value e (0..15), the entry
+// M_j(e << 4k). Word index ((k * 16 + e) * 64 + lane): every lane reads its own bank.
+constexpr int kFoldNibbleWords = 8 * 16 * 64;  // 32 KiB per G
+
+inline void build_fold_nibbles(const uint32_t fold[kFoldWords], int set, uint32_t out[kFoldNibbleWords]) {
+    const int g = kFoldGs[set];
+    for (int lane = 0; lane < 64; ++lane) {
+        const uint32_t *cols = fold + (kFoldOffset[set] + lane % g) * 32;
+        for (int k = 0; k < 8; ++k)
+            for (uint32_t e = 0; e < 16; ++e)
+                out[(k * 16 + e) * 64 + lane] = apply_cols(cols, e << (4 * k));
+    }
+}
+
 }  // namespace hdfs3crc

@@ -293,9 +293,13 @@ int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out) {
         return bail(fail(-ENOMEM, "device allocation for ctx failed"));
     if (hipMemcpy(ctx->d_tables, t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(-EIO, "table upload failed"));
-    static uint32_t fold[kFoldWords];
+    // fold image: kFoldWords matrix columns, then 4 nibble-table sets (G = 8,16,32,64)
+    static uint32_t fold[kFoldWords + 4 * kFoldNibbleWords];
     static std::once_flag fold_once;
-    std::call_once(fold_once, [&] { build_fold_matrices(t[0], fold); });
+    std::call_once(fold_once, [&] {
+        build_fold_matrices(t[0], fold);
+        for (int set = 0; set < 4; ++set) build_fold_nibbles(fold, set, fold + kFoldWords + set * kFoldNibbleWords);
+    });
     if (hipMalloc(reinterpret_cast<void **>(&ctx->d_fold), sizeof(fold)) != hipSuccess ||
         hipMemcpy(ctx->d_fold, fold, sizeof(fold), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(-ENOMEM, "fold-matrix upload failed"));
@@ -529,5 +533,8 @@ int hdfs3x_lane_read(hdfs3_crc_ctx *ctx, const void *d, size_t len, uint32_t bpc
 }
 
 int hdfs3x_grid_cap(hdfs3_crc_ctx *ctx) { return ctx ? ctx->grid_cap : 0; }
+
+// Process-wide kernel-variant knob for in-process A/B measurements (tools/ab.py).
+void hdfs3x_set_variant(int v) { set_variant(v); }
 
 }  // extern "C"

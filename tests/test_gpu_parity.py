@@ -218,3 +218,32 @@ def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
             bad = data.copy()
             bad[3 * 512 + byte] ^= 1 << bit
             assert gpu_ctx.verify(bad, 512, crc, True) == 3
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("bpc", [512, 1024, 2048, 4096, 8192])
+def test_every_kernel_variant_matches_oracle(gpu_ctx, variant, bpc):
+    """All kernel designs kept for A/B (hdfs3x_set_variant) are parity-checked too:
+    whole rounds, the slow region (len not a multiple of the 4 KiB round) and the tail."""
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    lib = _native.lib()
+    try:
+        lib.hdfs3x_set_variant(variant)
+        for n in (4096 * 37, 4096 * 64 * 17 + 3 * bpc, 4096 * 300 + bpc * 2 + 77, bpc * 65 + 5):
+            data = splitmix_bytes(n, variant * 1000 + bpc + n)
+            want = oracle_compute(data, bpc)
+            d = gpu_ctx.upload(data)
+            dc = DeviceBuffer(want.nbytes)
+            gpu_ctx.compute_dev(d.ptr, n, bpc, dc.ptr)
+            assert np.array_equal(gpu_ctx.download(dc, want.nbytes), want), (variant, bpc, n)
+            assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, True) == -1
+            nc = (n + bpc - 1) // bpc
+            for k in (0, nc // 2, nc - 2):
+                pos = k * bpc + 1
+                gpu_ctx.upload(np.array([data[pos] ^ 4], np.uint8), d, offset=pos)
+                assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, False) == k, (variant, bpc, n, k)
+                gpu_ctx.upload(data[pos:pos + 1], d, offset=pos)
+    finally:
+        lib.hdfs3x_set_variant(0)
