@@ -268,10 +268,12 @@ struct Round {
     uint32_t w[4][4];  // [load register][dword]
 };
 
+template <bool NT = false>
 __device__ __forceinline__ void load_round(Round &r, const uint8_t *base, uint32_t lane_off) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const u32x4 v = ld16(base + 1024 * t + lane_off);
+        const u32x4 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + 1024 * t + lane_off))
+                           : ld16(base + 1024 * t + lane_off);
         r.w[t][0] = v.x;
         r.w[t][1] = v.y;
         r.w[t][2] = v.z;
@@ -528,7 +530,7 @@ __device__ __forceinline__ uint32_t combine(const Look &l, uint32_t next) {
     return xor3(xor3(l.v[0], l.v[1], l.v[2]), l.v[3], next);
 }
 
-template <int BPC, bool VERIFY, int PAIR>
+template <int BPC, bool VERIFY, int PAIR, bool NT = false>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a,
                                                                     const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
@@ -558,7 +560,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     __builtin_amdgcn_sched_barrier(0);
     Round b[2 * PAIR];
 #pragma unroll
-    for (int i = 0; i < PAIR; ++i) load_round(b[i], round_ptr(i), lane_off);
+    for (int i = 0; i < PAIR; ++i) load_round<NT>(b[i], round_ptr(i), lane_off);
     __builtin_amdgcn_sched_barrier(0);
     store_tables(lds, tv);
     {
@@ -595,7 +597,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     if constexpr (PAIR == 1) {
         auto step = [&](Round &cur, Round &pf, uint64_t k) {
             const uint32_t w = want_of(k);
-            load_round(pf, round_ptr(k + 1), lane_off);
+            load_round<NT>(pf, round_ptr(k + 1), lane_off);
             __builtin_amdgcn_sched_barrier(0);
             regroup(cur);
             uint32_t x = init ^ word(cur, 0);
@@ -611,8 +613,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     } else {
         auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint64_t k) {
             const uint32_t w0 = want_of(k), w1 = want_of(k + 1);
-            load_round(p0, round_ptr(k + 2), lane_off);
-            load_round(p1, round_ptr(k + 3), lane_off);
+            load_round<NT>(p0, round_ptr(k + 2), lane_off);
+            load_round<NT>(p1, round_ptr(k + 3), lane_off);
             __builtin_amdgcn_sched_barrier(0);
             regroup(c0);
             regroup(c1);
@@ -693,6 +695,32 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_packets_kernel(
                 store_be32(arena_w + d.crc_off + 4ull * k, c, al4);
             }
         }
+    }
+}
+
+// Diagnostic kernels for the per-launch fixed cost (variants 10-12): same grid and
+// block as the production kernel; 10 = no LDS, 11 = 160 KiB LDS allocated but not
+// written, 12 = LDS fill (tables + nibble image) + barrier.
+template <int MODE>
+__global__ __launch_bounds__(kBlockThreads) void fixed_cost_kernel(const uint32_t *__restrict__ g_tab,
+                                                                   const uint32_t *__restrict__ g_nib,
+                                                                   uint32_t *sink) {
+    if constexpr (MODE == 10) {
+        if (threadIdx.x == 1u << 30) sink[0] = 1;
+    } else {
+        __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytesWave / 4];
+        if constexpr (MODE == 12) {
+            uint32_t tv[kFillPerThread];
+            fetch_tables(tv, g_tab);
+            const u32x4 n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
+            const u32x4 n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+            store_tables(lds, tv);
+            u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * threadIdx.x;
+            dst[0] = n0;
+            dst[1] = n1;
+        }
+        lds_barrier();
+        if (lds[threadIdx.x] == 0x9E3779B9u && threadIdx.x == 1u << 30) sink[0] = 1;
     }
 }
 
@@ -797,7 +825,7 @@ hipError_t launch_r3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *
     return hipGetLastError();
 }
 
-template <int BPC, bool V, int PAIR>
+template <int BPC, bool V, int PAIR, bool NT = false>
 hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                        hipStream_t s) {
     if constexpr (BPC > kRoundBytes) {
@@ -809,8 +837,8 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         const uint64_t units = a.len / kRoundBytes;
         const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
         const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
-        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR>), dim3(grid), dim3(kBlockThreads), 0, s, a, tab,
-                           nib);
+        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT>), dim3(grid), dim3(kBlockThreads), 0, s, a,
+                           tab, nib);
         return hipGetLastError();
     }
 }
@@ -818,14 +846,17 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
 template <int BPC, bool V>
 hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                     hipStream_t s) {
-    // Production path (variant 0): the wave kernel with the LDS nibble fold and two
-    // software-pipelined chains per lane (bpc <= 4096), the round kernel above that.
+    // Production path (variant 0): the wave kernel with the LDS nibble fold, two
+    // software-pipelined chains per lane and non-temporal data loads (streamed once;
+    // keeps the table/fold images cache-resident: 1 GiB verify 6.43 TB/s = the
+    // coalesced-read ceiling, tools/size_sweep.py) for bpc <= 4096; the round kernel above.
     // Other values select earlier designs for in-process A/B (tools/ab.py).
     switch (g_variant) {
     case 1: return launch_r3<BPC, V, 1, false>(a, tab, fold, grid_cap, s);   // first round kernel
     case 2: return launch_r3<BPC, V, 1, true>(a, tab, fold, grid_cap, s);    // + bitop3 fold
     case 3: return launch_r3<BPC, V, 2, true>(a, tab, fold, grid_cap, s);    // + 2-deep prefetch
     case 4: return launch_wave<BPC, V, 1>(a, tab, fold, grid_cap, s);        // nibble fold, 1 chain
+    case 5: return launch_wave<BPC, V, 2, false>(a, tab, fold, grid_cap, s); // 2 chains, default-policy loads
     case 9: {  // diagnostic: full grid, LDS fill + barrier, no rounds (per-launch fixed cost)
         ChunkLaunch e = a;
         e.len = 0;
@@ -836,7 +867,17 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
                                tab, fold + kFoldWords + set * kFoldNibbleWords);
         return hipGetLastError();
     }
-    default: return launch_wave<BPC, V, 2>(a, tab, fold, grid_cap, s);
+    case 10:
+        hipLaunchKernelGGL(fixed_cost_kernel<10>, dim3(grid_cap), dim3(kBlockThreads), 0, s, tab, fold, nullptr);
+        return hipGetLastError();
+    case 11:
+        hipLaunchKernelGGL(fixed_cost_kernel<11>, dim3(grid_cap), dim3(kBlockThreads), 0, s, tab, fold, nullptr);
+        return hipGetLastError();
+    case 12:
+        hipLaunchKernelGGL(fixed_cost_kernel<12>, dim3(grid_cap), dim3(kBlockThreads), 0, s, tab,
+                           fold + kFoldWords, nullptr);
+        return hipGetLastError();
+    default: return launch_wave<BPC, V, 2, true>(a, tab, fold, grid_cap, s);
     }
 }
 
