@@ -60,6 +60,28 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# ---- multi-GPU plumbing (config 4: independent blocks, one set per GPU, no collective
+# on the data path). Kept free of GPU calls so tests/test_multigpu.py can run it on
+# CPU ranks with the gloo backend.
+
+def rank_seed(rank: int) -> int:
+    """Each rank verifies its own distinct synthetic blocks."""
+    return 1234 + 7919 * rank
+
+
+def max_over_ranks(dist, value: float, device) -> float:
+    """Whole-job time = the slowest rank's time (barrier-bracketed region)."""
+    import torch
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate_rate(bytes_per_rank: int, world: int, elapsed_max: float) -> float:
+    """value = all ranks' payload bytes / max-over-ranks time, in GiB/s (weak scaling)."""
+    return bytes_per_rank * world / elapsed_max / 2**30
+
+
 class Workload:
     """Per-rank device arena: `blocks` blocks of data + their BE CRC arrays, in HBM."""
 
@@ -250,7 +272,7 @@ def main():
     ctx.set_stream(stream.cuda_stream)
 
     block_bytes = args.block_mib << 20
-    work = Workload(torch, ctx, device, block_bytes, args.blocks, args.bpc, seed=1234 + rank)
+    work = Workload(torch, ctx, device, block_bytes, args.blocks, args.bpc, seed=rank_seed(rank))
 
     if args.pmc_child:
         res = torch.zeros(64, dtype=torch.int64, device=device)
@@ -274,9 +296,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed = max_over_ranks(dist, elapsed, device)
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the timed region")
     # (2) roofline pass: the same K launches, each bracketed by HIP events on the launch
@@ -292,8 +312,7 @@ def main():
     avg_launch_s = sum(launch_ms) / K * 1e-3
     payload = block_bytes
     alg_bytes = work.nchunks * (args.bpc + 4)  # verify reads data + CRC; compute reads data, writes CRC
-    total_payload = payload * K * world
-    value = total_payload / elapsed / 2**30
+    value = aggregate_rate(payload * K, world, elapsed)
 
     if rank != 0:
         if world > 1:

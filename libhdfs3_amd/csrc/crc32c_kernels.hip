@@ -281,6 +281,34 @@ __device__ __forceinline__ void load_round(Round &r, const uint8_t *base, uint32
     }
 }
 
+// Same, through a buffer resource built from the wave-uniform round base (scalar
+// registers, made provably uniform by readfirstlane: cdna_hip_programming.md T8/T20).
+// The lane's constant byte offset is the only VGPR operand, so no 64-bit VGPR address
+// temporaries exist that the allocator could alias with in-flight load destinations
+// (which made the compiler drain the previous round's loads before each prefetch).
+template <bool NT>
+__device__ __forceinline__ void load_round_buf(Round &r, const uint8_t *base, uint32_t lane_off) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(b));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(b >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, 4096, 0x00020000);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + 1024 * t, 0, NT ? 2 : 0);
+        r.w[t][0] = v.x;
+        r.w[t][1] = v.y;
+        r.w[t][2] = v.z;
+        r.w[t][3] = v.w;
+    }
+}
+
+template <bool NT, bool BUF>
+__device__ __forceinline__ void load_any(Round &r, const uint8_t *base, uint32_t lane_off) {
+    if constexpr (BUF) load_round_buf<NT>(r, base, lane_off);
+    else load_round<NT>(r, base, lane_off);
+}
+
 __device__ __forceinline__ void swap32(uint32_t &a, uint32_t &b) {
     const auto p = __builtin_amdgcn_permlane32_swap(a, b, false, false);
     a = p[0];
@@ -530,7 +558,7 @@ __device__ __forceinline__ uint32_t combine(const Look &l, uint32_t next) {
     return xor3(xor3(l.v[0], l.v[1], l.v[2]), l.v[3], next);
 }
 
-template <int BPC, bool VERIFY, int PAIR, bool NT = false>
+template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a,
                                                                     const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
@@ -544,12 +572,17 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
     const uint64_t nunits = a.len / kRoundBytes;
     const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
-    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+    // wave-uniform by construction; readfirstlane makes that provable to the compiler so
+    // the end-of-stream prefetch guards below are scalar branches, not exec masks
+    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t K = wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0;
+    // Prefetches past the wave's last round stay unconditional (a branch around them
+    // makes the waitcnt pass drain every load at the loop head) but read the 4 KiB slice
+    // table image instead: cache-resident, so they cost no HBM bytes (re-reading data
+    // would, since the non-temporal stream is not kept in L2).
     auto round_ptr = [&](uint64_t k) -> const uint8_t * {
-        if (K == 0) return a.data;
-        const uint64_t kk = k < K ? k : K - 1;
-        return a.data + (wave + kk * nwaves) * kRoundBytes;
+        return k < K ? a.data + (wave + k * nwaves) * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
     };
 
     // table + nibble-image words, then the first round(s), then the LDS fill
@@ -560,7 +593,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     __builtin_amdgcn_sched_barrier(0);
     Round b[2 * PAIR];
 #pragma unroll
-    for (int i = 0; i < PAIR; ++i) load_round<NT>(b[i], round_ptr(i), lane_off);
+    for (int i = 0; i < PAIR; ++i) load_any<NT, BUF>(b[i], round_ptr(i), lane_off);
     __builtin_amdgcn_sched_barrier(0);
     store_tables(lds, tv);
     {
@@ -597,7 +630,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     if constexpr (PAIR == 1) {
         auto step = [&](Round &cur, Round &pf, uint64_t k) {
             const uint32_t w = want_of(k);
-            load_round<NT>(pf, round_ptr(k + 1), lane_off);
+            load_any<NT, BUF>(pf, round_ptr(k + 1), lane_off);
             __builtin_amdgcn_sched_barrier(0);
             regroup(cur);
             uint32_t x = init ^ word(cur, 0);
@@ -613,8 +646,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     } else {
         auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint64_t k) {
             const uint32_t w0 = want_of(k), w1 = want_of(k + 1);
-            load_round<NT>(p0, round_ptr(k + 2), lane_off);
-            load_round<NT>(p1, round_ptr(k + 3), lane_off);
+            load_any<NT, BUF>(p0, round_ptr(k + 2), lane_off);
+            load_any<NT, BUF>(p1, round_ptr(k + 3), lane_off);
             __builtin_amdgcn_sched_barrier(0);
             regroup(c0);
             regroup(c1);
@@ -825,7 +858,7 @@ hipError_t launch_r3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *
     return hipGetLastError();
 }
 
-template <int BPC, bool V, int PAIR, bool NT = false>
+template <int BPC, bool V, int PAIR, bool NT = false, bool BUF = true>
 hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                        hipStream_t s) {
     if constexpr (BPC > kRoundBytes) {
@@ -837,8 +870,8 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         const uint64_t units = a.len / kRoundBytes;
         const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
         const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
-        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT>), dim3(grid), dim3(kBlockThreads), 0, s, a,
-                           tab, nib);
+        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF>), dim3(grid), dim3(kBlockThreads), 0,
+                           s, a, tab, nib);
         return hipGetLastError();
     }
 }
@@ -857,6 +890,7 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
     case 3: return launch_r3<BPC, V, 2, true>(a, tab, fold, grid_cap, s);    // + 2-deep prefetch
     case 4: return launch_wave<BPC, V, 1>(a, tab, fold, grid_cap, s);        // nibble fold, 1 chain
     case 5: return launch_wave<BPC, V, 2, false>(a, tab, fold, grid_cap, s); // 2 chains, default-policy loads
+    case 7: return launch_wave<BPC, V, 2, true, false>(a, tab, fold, grid_cap, s);  // nt via global_load
     case 9: {  // diagnostic: full grid, LDS fill + barrier, no rounds (per-launch fixed cost)
         ChunkLaunch e = a;
         e.len = 0;
