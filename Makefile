@@ -10,9 +10,11 @@ HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Iinclude -I$(CSRC
 HOSTFLAGS:= -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
 
 LIB      := $(LIBDIR)/libhdfs3_crc.so
-OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc32c.o
+LOOPBACK := $(LIBDIR)/libhdfs3_loopback.so
+OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc32c.o \
+            $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/client_block_reader.o
 
-all: $(LIB) oracle
+all: $(LIB) $(LOOPBACK) oracle
 
 $(OBJDIR)/crc32c_kernels.o: $(CSRC)/crc32c_kernels.hip $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
 	@mkdir -p $(OBJDIR)
@@ -26,6 +28,23 @@ $(OBJDIR)/host_crc32c.o: $(CSRC)/host_crc32c.cpp $(CSRC)/crc32c_tables.h
 	@mkdir -p $(OBJDIR)
 	g++ $(HOSTFLAGS) -c $< -o $@
 
+$(OBJDIR)/client_wire.o: $(CSRC)/client/wire.cpp $(CSRC)/client/wire.h
+	@mkdir -p $(OBJDIR)
+	g++ $(HOSTFLAGS) -c $< -o $@
+
+$(OBJDIR)/client_net.o: $(CSRC)/client/net.cpp $(CSRC)/client/net.h
+	@mkdir -p $(OBJDIR)
+	g++ $(HOSTFLAGS) -c $< -o $@
+
+$(OBJDIR)/client_block_reader.o: $(CSRC)/client/block_reader.cpp include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h $(CSRC)/client/wire.h $(CSRC)/client/net.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+# test/bench infrastructure: loopback datanode (tools/loopback)
+$(LOOPBACK): tools/loopback/loopback_datanode.cpp $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o
+	@mkdir -p $(LIBDIR)
+	g++ $(HOSTFLAGS) -shared -pthread -o $@ tools/loopback/loopback_datanode.cpp $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o
+
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS)
@@ -35,7 +54,7 @@ oracle:
 	@if [ -d /root/reference/src/common ]; then $(MAKE) -C oracle ref; fi
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(LOOPBACK)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

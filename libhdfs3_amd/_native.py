@@ -66,6 +66,29 @@ PUBLIC_API = {
     "hdfs3_device_count": (c_int, [POINTER(c_int)]),
 }
 
+class BlockId(ctypes.Structure):
+    """hdfs3_block_id (include/hdfs3_client.h)."""
+
+    _fields_ = [("pool_id", ctypes.c_char_p), ("block_id", c_uint64), ("generation_stamp", c_uint64),
+                ("num_bytes", c_uint64)]
+
+
+class ReaderOpts(ctypes.Structure):
+    """hdfs3_reader_opts (include/hdfs3_client.h)."""
+
+    _fields_ = [("device", c_int), ("verify", c_int), ("batch_packets", c_int), ("timeout_ms", c_int)]
+
+
+# every symbol include/hdfs3_client.h declares
+CLIENT_API = {
+    "hdfs3_block_reader_open": (c_int, [ctypes.c_char_p, c_int, POINTER(BlockId), c_int64, c_int64,
+                                        ctypes.c_char_p, POINTER(ReaderOpts), POINTER(c_void_p)]),
+    "hdfs3_block_reader_read": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),
+    "hdfs3_block_reader_available": (c_int64, [c_void_p]),
+    "hdfs3_block_reader_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint64), POINTER(c_uint64)]),
+    "hdfs3_block_reader_close": (c_int, [c_void_p]),
+}
+
 # measurement hooks (bench.py only; not in the public header)
 BENCH_API = {
     "hdfs3x_stream_read": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
@@ -80,7 +103,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         raise ImportError(f"{path} is missing: run `make` (or __graft_entry__.build()) first; "
                           "libhdfs3_amd has no CPU fallback")
     lib = ctypes.CDLL(path)
-    for table in (PUBLIC_API, BENCH_API):
+    for table in (PUBLIC_API, CLIENT_API, BENCH_API):
         for name, (res, args) in table.items():
             fn = getattr(lib, name)
             fn.restype = res
@@ -96,6 +119,31 @@ def lib() -> ctypes.CDLL:
     if _LIB is None:
         _LIB = load()
     return _LIB
+
+
+LOOPBACK_PATH = os.path.join(os.path.dirname(LIB_PATH), "libhdfs3_loopback.so")
+_LOOPBACK: ctypes.CDLL | None = None
+
+
+def loopback() -> ctypes.CDLL:
+    """Test/bench infrastructure: the loopback datanode (tools/loopback)."""
+    global _LOOPBACK
+    if _LOOPBACK is None:
+        if not os.path.exists(LOOPBACK_PATH):
+            raise ImportError(f"{LOOPBACK_PATH} is missing: run `make`")
+        lb = ctypes.CDLL(LOOPBACK_PATH)
+        lb.hdfs3_loopback_start.restype = c_int
+        lb.hdfs3_loopback_start.argtypes = [POINTER(c_int)]
+        lb.hdfs3_loopback_add_block.restype = c_int
+        lb.hdfs3_loopback_add_block.argtypes = [c_uint64, c_void_p, c_uint64, c_void_p, c_uint32, c_int]
+        lb.hdfs3_loopback_clear_blocks.restype = None
+        lb.hdfs3_loopback_set_packet_bytes.restype = None
+        lb.hdfs3_loopback_set_packet_bytes.argtypes = [c_int]
+        lb.hdfs3_loopback_served_bytes.restype = c_uint64
+        lb.hdfs3_loopback_last_status.restype = c_int
+        lb.hdfs3_loopback_stop.restype = c_int
+        _LOOPBACK = lb
+    return _LOOPBACK
 
 
 def check(fn: str, rc: int) -> int:

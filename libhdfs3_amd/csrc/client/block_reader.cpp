@@ -1,0 +1,410 @@
+// hdfs3_block_reader: RemoteBlockReader (src/client/RemoteBlockReader.cpp) with the
+// per-packet CPU verify replaced by batched GPU verification (include/hdfs3_client.h).
+//
+// Receive/verify pipeline: packets are read off the socket into one of two pinned
+// arenas (payload placed so each packet's data region is 16-byte aligned), the full
+// arena is copied to HBM and verified by the packet kernel asynchronously, and the next
+// arena is filled while the GPU works. Delivery to the caller only ever comes from a
+// batch whose verification has completed.
+#include "hdfs3_client.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <deque>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../ctx.h"
+#include "hdfs3_crc.h"
+#include "net.h"
+#include "wire.h"
+
+using namespace hdfs3crc;
+
+namespace {
+
+constexpr int kDefaultBatchPackets = 64;
+constexpr int kDefaultTimeoutMs = 60000;  // input.read.timeout default (SessionConfig.cpp)
+constexpr size_t kMaxResponse = 10u << 20;  // RemoteBlockReader.cpp:116
+
+struct PacketRef {
+    uint64_t data_off, crc_off;  // inside the arena
+    uint32_t data_len;
+    uint32_t skip;               // pendingAhead (RemoteBlockReader.cpp:264-266)
+    uint32_t deliver;            // bytes of this packet inside [start, end)
+};
+
+struct Batch {
+    uint8_t *h = nullptr, *d = nullptr;  // pinned / device arena
+    size_t cap = 0, used = 0;
+    DevPacket *h_desc = nullptr, *d_desc = nullptr;
+    size_t desc_cap = 0;
+    unsigned long long *d_res = nullptr, *h_res = nullptr;
+    hipEvent_t done = nullptr;
+    std::vector<PacketRef> pk;
+    bool launched = false, verified = false;
+    int64_t bad_pkt = -1;
+    size_t dpkt = 0, doff = 0;  // delivery cursor
+
+    void reset() {
+        used = 0;
+        pk.clear();
+        launched = verified = false;
+        bad_pkt = -1;
+        dpkt = doff = 0;
+    }
+    void release() {
+        if (h) (void)hipHostFree(h);
+        if (d) (void)hipFree(d);
+        if (h_desc) (void)hipHostFree(h_desc);
+        if (d_desc) (void)hipFree(d_desc);
+        if (h_res) (void)hipHostFree(h_res);
+        if (d_res) (void)hipFree(d_res);
+        if (done) (void)hipEventDestroy(done);
+        *this = Batch();
+    }
+};
+
+int hip_err(hipError_t e, const char *what) {
+    return fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIP_OK(expr)                                      \
+    do {                                                  \
+        hipError_t e_ = (expr);                           \
+        if (e_ != hipSuccess) return hip_err(e_, #expr);  \
+    } while (0)
+
+int grow(Batch &b, size_t cap, size_t descs) {
+    if (cap > b.cap) {
+        if (b.h) (void)hipHostFree(b.h);
+        if (b.d) (void)hipFree(b.d);
+        b.h = b.d = nullptr;
+        b.cap = 0;
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.h), cap, hipHostMallocDefault));
+        HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.d), cap));
+        b.cap = cap;
+    }
+    if (descs > b.desc_cap) {
+        if (b.h_desc) (void)hipHostFree(b.h_desc);
+        if (b.d_desc) (void)hipFree(b.d_desc);
+        b.h_desc = b.d_desc = nullptr;
+        b.desc_cap = 0;
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.h_desc), descs * sizeof(DevPacket), hipHostMallocDefault));
+        HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.d_desc), descs * sizeof(DevPacket)));
+        b.desc_cap = descs;
+    }
+    if (!b.d_res) {
+        HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.d_res), sizeof(unsigned long long)));
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.h_res), sizeof(unsigned long long), hipHostMallocDefault));
+        HIP_OK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+    }
+    return 0;
+}
+
+}  // namespace
+
+struct hdfs3_block_reader {
+    int fd = -1;
+    int timeout_ms = kDefaultTimeoutMs;
+    int batch_packets = kDefaultBatchPackets;
+    bool verify = true;
+    hdfs3_crc_ctx *ctx = nullptr;
+    wire::ExtendedBlock block;
+    int64_t start = 0, end_offset = 0;
+    int64_t recv_cursor = 0;   // "cursor" as seen by readNextPacket for the next packet
+    int64_t delivered = 0;     // bytes handed to the caller
+    int64_t last_seqno = -1;
+    uint32_t chunk_size = 0;
+    uint32_t checksum_size = 0;
+    bool range_done = false;   // every packet of the range (and the trailer) received
+    bool sent_status = false;
+    int error = 0;             // sticky failure (-errno)
+    std::string error_msg;
+    bool have_pending_hdr = false;
+    wire::PacketHeader pending_hdr;
+    Batch slot[2];
+    std::deque<int> queue;     // launched batches in order, front = delivering
+    int next_slot = 0;
+    uint64_t packets = 0, batches = 0;
+
+    int sticky(int code, const std::string &msg) {
+        error = code;
+        error_msg = msg;
+        return fail(code, "%s", msg.c_str());
+    }
+
+    // RemoteBlockReader::checkResponse (:112-203)
+    int check_response() {
+        std::string resp;
+        if (int rc = net::read_delimited(fd, resp, kMaxResponse, timeout_ms))
+            return sticky(rc, "RemoteBlockReader: failed to read BlockOpResponseProto");
+        wire::BlockOpResponse r;
+        if (!wire::decode_block_op_response(resp.data(), resp.size(), r))
+            return sticky(-EPROTO, "RemoteBlockReader cannot parse BlockOpResponseProto from Datanode response");
+        if (r.status != wire::kSuccess)
+            return sticky(-EIO, "RemoteBlockReader: Datanode return an error when sending read request: " +
+                                    (r.message.empty() ? std::string("check Datanode's log") : r.message));
+        if (!r.has_checksum_info) return sticky(-EPROTO, "RemoteBlockReader: response lacks ReadOpChecksumInfoProto");
+        chunk_size = r.bytes_per_checksum;
+        switch (r.checksum_type) {
+        case wire::kChecksumNull: verify = false; checksum_size = 0; break;
+        case wire::kChecksumCrc32c: checksum_size = 4; break;
+        case wire::kChecksumCrc32:
+            return sticky(-ENOTSUP, "CHECKSUM_CRC32 (zlib) is not implemented on the GPU path (DESIGN.md §7)");
+        default: return sticky(-EPROTO, "RemoteBlockReader cannot recognize checksum type");
+        }
+        if (chunk_size == 0 || (checksum_size && (chunk_size & 3u)))
+            return sticky(-EPROTO, "RemoteBlockReader invalid chunk size");
+        const int64_t first = int64_t(r.chunk_offset);
+        if (first < 0 || first > start || first <= start - int64_t(chunk_size))
+            return sticky(-EPROTO, "RemoteBlockReader invalid first chunk offset");
+        return 0;
+    }
+
+    int read_header(wire::PacketHeader &h) {
+        if (have_pending_hdr) {
+            h = pending_hdr;
+            have_pending_hdr = false;
+            return 0;
+        }
+        uint8_t buf[wire::kPacketHeaderSize];
+        if (int rc = net::read_fully(fd, buf, sizeof(buf), timeout_ms))
+            return sticky(rc, "RemoteBlockReader: failed to read block header");
+        if (!h.decode(buf, sizeof(buf))) return sticky(-EPROTO, "Invalid PacketHeader");
+        return 0;
+    }
+
+    // readNextPacket (:226-277) for up to batch_packets packets into `b`
+    int receive(Batch &b) {
+        b.reset();
+        while (int(b.pk.size()) < batch_packets && !range_done) {
+            wire::PacketHeader h;
+            if (int rc = read_header(h)) return rc;
+            if (!h.sanity_check(last_seqno))
+                return sticky(-EIO, "RemoteBlockReader: Packet failed on sanity check");
+            if (h.data_len <= 0) {  // the empty last packet ends the block
+                last_seqno = h.seqno;
+                range_done = true;
+                break;
+            }
+            const uint64_t chunks = (uint64_t(h.data_len) + chunk_size - 1) / chunk_size;
+            const uint64_t crc_len = chunks * checksum_size;
+            if (int64_t(h.packet_len) != 4 + int64_t(h.data_len) + int64_t(crc_len))
+                return sticky(-EIO, "Invalid Packet, packetLen does not match dataLen and checksums");
+            const uint64_t size = crc_len + uint64_t(h.data_len);
+            uint64_t off = ((b.used + crc_len + 15) & ~uint64_t(15)) - crc_len;
+            if (off + size > b.cap) {
+                if (!b.pk.empty()) {  // close this batch; the header opens the next
+                    pending_hdr = h;
+                    have_pending_hdr = true;
+                    break;
+                }
+                if (int rc = grow(b, size + 64, size_t(batch_packets))) return sticky(rc, "arena growth failed");
+                off = ((crc_len + 15) & ~uint64_t(15)) - crc_len;
+            }
+            if (int rc = net::read_fully(fd, b.h + off, size, timeout_ms))
+                return sticky(rc, "RemoteBlockReader: failed to read packet payload");
+            last_seqno = h.seqno;
+            ++packets;
+            int64_t ahead = recv_cursor - h.offset_in_block;
+            ahead = ahead > 0 ? ahead : 0;
+            const int64_t useful = std::max<int64_t>(0, std::min<int64_t>(h.data_len - ahead, end_offset - recv_cursor));
+            b.pk.push_back(PacketRef{off + crc_len, off, uint32_t(h.data_len), uint32_t(ahead), uint32_t(useful)});
+            b.used = off + size;
+            const int64_t reached = recv_cursor + h.data_len - ahead;
+            recv_cursor = reached;
+            if (reached >= end_offset) {
+                // readTrailingEmptyPacket (:279-287): the datanode follows with an empty last packet
+                wire::PacketHeader t;
+                if (int rc = read_header(t)) return rc;
+                if (t.last_packet_in_block && t.data_len == 0) last_seqno = t.seqno;
+                range_done = true;
+            }
+        }
+        return 0;
+    }
+
+    int launch(Batch &b) {
+        b.launched = true;
+        ++batches;
+        if (!verify || b.pk.empty()) {
+            b.verified = true;
+            return 0;
+        }
+        for (size_t i = 0; i < b.pk.size(); ++i)
+            b.h_desc[i] = DevPacket{b.pk[i].data_off, b.pk[i].crc_off, b.pk[i].data_len, 0};
+        HIP_OK(hipMemcpyAsync(b.d, b.h, b.used, hipMemcpyHostToDevice, ctx->stream));
+        HIP_OK(hipMemcpyAsync(b.d_desc, b.h_desc, b.pk.size() * sizeof(DevPacket), hipMemcpyHostToDevice,
+                              ctx->stream));
+        HIP_OK(hipMemsetAsync(b.d_res, 0, sizeof(unsigned long long), ctx->stream));
+        HIP_OK(launch_packets(b.d, b.d_desc, b.pk.size(), chunk_size, true, /*check_short_tail=*/0, b.d_res,
+                              ctx->d_tables, ctx->grid_cap, ctx->stream));
+        ++ctx->launches;
+        HIP_OK(hipMemcpyAsync(b.h_res, b.d_res, sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_OK(hipEventRecord(b.done, ctx->stream));
+        return 0;
+    }
+
+    int wait(Batch &b) {
+        if (b.verified) return 0;
+        HIP_OK(hipEventSynchronize(b.done));
+        const unsigned long long r = *b.h_res;
+        if (r) b.bad_pkt = int64_t((~r) >> 32);
+        b.verified = true;
+        return 0;
+    }
+
+    // fill + launch one more batch if the range still has packets
+    int pump() {
+        if (range_done || queue.size() >= 2) return 0;
+        Batch &b = slot[next_slot];
+        if (int rc = grow(b, std::max<size_t>(b.cap, size_t(batch_packets) * (65536 + 16 * 1024)), size_t(batch_packets)))
+            return sticky(rc, "arena allocation failed");
+        if (int rc = receive(b)) return rc;
+        if (b.pk.empty() && range_done) return 0;
+        if (int rc = launch(b)) return sticky(rc, hdfs3_crc_last_error());
+        queue.push_back(next_slot);
+        next_slot ^= 1;
+        return 0;
+    }
+
+    // sendStatus (:289-304), once every packet of the range verified
+    void maybe_send_status() {
+        if (sent_status || !range_done || !queue.empty() || error) return;
+        const std::string msg = wire::encode_client_read_status(verify ? wire::kChecksumOk : wire::kSuccess);
+        if (net::write_delimited(fd, msg, timeout_ms) == 0) sent_status = true;
+    }
+
+    int32_t read(uint8_t *out, int32_t len) {
+        if (error) return fail(error, "%s", error_msg.c_str());
+        if (len <= 0 || !out) return fail(-EINVAL, "invalid read buffer");
+        int32_t total = 0;
+        while (total < len) {
+            if (queue.empty()) {
+                if (int rc = pump()) return total ? total : rc;
+                if (queue.empty()) break;  // range exhausted
+            }
+            // keep the next batch receiving while this one verifies on the GPU
+            if (int rc = pump()) return total ? total : rc;
+            Batch &b = slot[queue.front()];
+            if (int rc = wait(b)) return total ? total : sticky(rc, hdfs3_crc_last_error());
+            const size_t limit = b.bad_pkt >= 0 ? size_t(b.bad_pkt) : b.pk.size();
+            while (total < len && b.dpkt < limit) {
+                const PacketRef &p = b.pk[b.dpkt];
+                const size_t avail = p.deliver - b.doff;
+                const size_t n = std::min<size_t>(avail, size_t(len - total));
+                std::memcpy(out + total, b.h + p.data_off + p.skip + b.doff, n);
+                total += int32_t(n);
+                b.doff += n;
+                delivered += int64_t(n);
+                if (b.doff == p.deliver) {
+                    ++b.dpkt;
+                    b.doff = 0;
+                }
+            }
+            if (b.dpkt == limit) {
+                if (b.bad_pkt >= 0) {
+                    sticky(-EIO, "ChecksumException: RemoteBlockReader: checksum not match for Block: " +
+                                     std::to_string(block.block_id) + " (packet " +
+                                     std::to_string(b.bad_pkt) + " of a GPU batch)");
+                    return total ? total : error;
+                }
+                queue.pop_front();
+                maybe_send_status();
+            }
+        }
+        return total;
+    }
+
+    int64_t available() const {
+        int64_t a = 0;
+        for (int s : queue) {
+            const Batch &b = slot[s];
+            if (!b.verified) continue;
+            const size_t limit = b.bad_pkt >= 0 ? size_t(b.bad_pkt) : b.pk.size();
+            for (size_t i = b.dpkt; i < limit; ++i) a += b.pk[i].deliver - (i == b.dpkt ? b.doff : 0);
+        }
+        return a;
+    }
+
+    ~hdfs3_block_reader() {
+        if (ctx) (void)hipStreamSynchronize(ctx->stream);
+        for (Batch &b : slot) b.release();
+        if (ctx) hdfs3_crc_ctx_destroy(ctx);
+        net::close_fd(fd);
+    }
+};
+
+extern "C" {
+
+int hdfs3_block_reader_open(const char *host, int port, const hdfs3_block_id *blk, int64_t start,
+                            int64_t len, const char *client_name, const hdfs3_reader_opts *opts,
+                            hdfs3_block_reader **out) {
+    if (!out || !host || !blk || start < 0 || len < 0) return fail(-EINVAL, "invalid argument");
+    *out = nullptr;
+    hdfs3_block_reader *r = new (std::nothrow) hdfs3_block_reader();
+    if (!r) return fail(-ENOMEM, "reader allocation");
+    const int device = opts ? opts->device : 0;
+    r->verify = opts ? opts->verify != 0 : true;
+    if (opts && opts->batch_packets > 0) r->batch_packets = opts->batch_packets;
+    if (opts && opts->timeout_ms > 0) r->timeout_ms = opts->timeout_ms;
+    r->block.pool_id = blk->pool_id ? blk->pool_id : "";
+    r->block.block_id = blk->block_id;
+    r->block.generation_stamp = blk->generation_stamp;
+    r->block.num_bytes = blk->num_bytes;
+    r->start = r->recv_cursor = start;
+    r->end_offset = start + len;
+    if (int rc = hdfs3_crc_ctx_create(device, &r->ctx)) {
+        delete r;
+        return rc;
+    }
+    r->fd = net::connect_tcp(host, port, r->timeout_ms);
+    if (r->fd < 0) {
+        const int rc = r->fd;
+        delete r;
+        return fail(rc, "RemoteBlockReader: Failed to connect to %s:%d", host, port);
+    }
+    wire::ReadBlockRequest req;
+    req.block = r->block;
+    req.client_name = client_name ? client_name : "libhdfs3_amd";
+    req.offset = uint64_t(start);
+    req.len = uint64_t(len);
+    const std::string frame = wire::encode_read_block(req);
+    if (int rc = net::write_fully(r->fd, frame.data(), frame.size(), r->timeout_ms)) {
+        delete r;
+        return fail(rc, "DataTransferProtocolSender cannot send read request to datanode");
+    }
+    if (int rc = r->check_response()) {
+        delete r;
+        return rc;
+    }
+    *out = r;
+    return 0;
+}
+
+int32_t hdfs3_block_reader_read(hdfs3_block_reader *r, void *buf, int32_t len) {
+    if (!r) return fail(-EINVAL, "null reader");
+    return r->read(static_cast<uint8_t *>(buf), len);
+}
+
+int64_t hdfs3_block_reader_available(hdfs3_block_reader *r) { return r ? r->available() : 0; }
+
+int hdfs3_block_reader_stats(hdfs3_block_reader *r, uint32_t *bpc, uint64_t *packets, uint64_t *gpu_batches) {
+    if (!r) return fail(-EINVAL, "null reader");
+    if (bpc) *bpc = r->chunk_size;
+    if (packets) *packets = r->packets;
+    if (gpu_batches) *gpu_batches = r->batches;
+    return 0;
+}
+
+int hdfs3_block_reader_close(hdfs3_block_reader *r) {
+    delete r;
+    return 0;
+}
+
+}  // extern "C"

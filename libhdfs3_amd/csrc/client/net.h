@@ -1,0 +1,28 @@
+// Blocking TCP I/O with poll() timeouts: the subset of src/network/TcpSocket.cpp
+// (readFully/writeFully, :64-133,334) and BufferedSocketReader.cpp:63-146 (varint
+// reads) the checksum path needs. Errors are returned, never thrown.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace hdfs3crc {
+namespace net {
+
+// connect to host:port; returns fd >= 0 or -errno
+int connect_tcp(const char *host, int port, int timeout_ms);
+// listening socket on 127.0.0.1:port (0 = ephemeral); *bound_port receives the port
+int listen_tcp(int port, int *bound_port);
+// 0 on success, -errno on failure (-ETIMEDOUT, -ECONNRESET on EOF)
+int read_fully(int fd, void *buf, size_t n, int timeout_ms);
+int write_fully(int fd, const void *buf, size_t n, int timeout_ms);
+// protobuf varint32 length prefix, as BufferedSocketReader::readVarint32
+int read_varint32(int fd, uint32_t *out, int timeout_ms);
+// read a varint-length-prefixed message (bounded by max_len, RemoteBlockReader.cpp:116)
+int read_delimited(int fd, std::string &out, size_t max_len, int timeout_ms);
+int write_delimited(int fd, const std::string &msg, int timeout_ms);
+void close_fd(int fd);
+
+}  // namespace net
+}  // namespace hdfs3crc

@@ -1,0 +1,321 @@
+// Hand-encoded protobuf subset for the checksum path; see wire.h for the reference map.
+#include "wire.h"
+
+#include <cstring>
+
+namespace hdfs3crc {
+namespace wire {
+
+void put_varint(std::string &out, uint64_t v) {
+    while (v >= 0x80) {
+        out.push_back(char(uint8_t(v) | 0x80));
+        v >>= 7;
+    }
+    out.push_back(char(v));
+}
+
+void put_tag(std::string &out, int field, int wiretype) { put_varint(out, (uint64_t(field) << 3) | wiretype); }
+
+void put_fixed64(std::string &out, uint64_t v) {
+    for (int i = 0; i < 8; ++i) out.push_back(char(uint8_t(v >> (8 * i))));
+}
+
+void put_fixed32(std::string &out, uint32_t v) {
+    for (int i = 0; i < 4; ++i) out.push_back(char(uint8_t(v >> (8 * i))));
+}
+
+void put_bytes(std::string &out, int field, const std::string &s) {
+    put_tag(out, field, 2);
+    put_varint(out, s.size());
+    out += s;
+}
+
+void put_uint(std::string &out, int field, uint64_t v) {
+    put_tag(out, field, 0);
+    put_varint(out, v);
+}
+
+uint64_t Reader::varint() {
+    uint64_t v = 0;
+    for (int shift = 0; shift < 64; shift += 7) {
+        if (p >= end) {
+            ok = false;
+            return 0;
+        }
+        const uint8_t b = *p++;
+        v |= uint64_t(b & 0x7F) << shift;
+        if (!(b & 0x80)) return v;
+    }
+    ok = false;
+    return 0;
+}
+
+uint64_t Reader::fixed64() {
+    if (end - p < 8) {
+        ok = false;
+        return 0;
+    }
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v |= uint64_t(p[i]) << (8 * i);
+    p += 8;
+    return v;
+}
+
+uint32_t Reader::fixed32() {
+    if (end - p < 4) {
+        ok = false;
+        return 0;
+    }
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i) v |= uint32_t(p[i]) << (8 * i);
+    p += 4;
+    return v;
+}
+
+std::string Reader::bytes() {
+    const uint64_t n = varint();
+    if (!ok || uint64_t(end - p) < n) {
+        ok = false;
+        return {};
+    }
+    std::string s(reinterpret_cast<const char *>(p), size_t(n));
+    p += n;
+    return s;
+}
+
+void Reader::skip(int wiretype) {
+    switch (wiretype) {
+    case 0: varint(); break;
+    case 1: fixed64(); break;
+    case 2: bytes(); break;
+    case 5: fixed32(); break;
+    default: ok = false;
+    }
+}
+
+// ---- PacketHeader -------------------------------------------------------------
+
+void PacketHeader::encode(uint8_t out[kPacketHeaderSize]) const {
+    std::string proto;
+    put_tag(proto, 1, 1);
+    put_fixed64(proto, uint64_t(offset_in_block));
+    put_tag(proto, 2, 1);
+    put_fixed64(proto, uint64_t(seqno));
+    put_tag(proto, 3, 0);
+    put_varint(proto, last_packet_in_block ? 1 : 0);
+    put_tag(proto, 4, 5);
+    put_fixed32(proto, uint32_t(data_len));
+    wr_be32(out, uint32_t(packet_len));
+    wr_be16(out + 4, uint16_t(proto.size()));
+    std::memcpy(out + 6, proto.data(), proto.size());  // 25 bytes: total 31
+}
+
+bool PacketHeader::decode(const uint8_t *buf, size_t n) {
+    if (n < 6) return false;
+    packet_len = int32_t(rd_be32(buf));
+    const int proto_len = int16_t(rd_be16(buf + 4));
+    // PacketHeader.cpp:105-110: packetLen >= 4, protoLen >= 0, proto inside the buffer
+    if (packet_len < 4 || proto_len < 0 || 6 + size_t(proto_len) > n) return false;
+    Reader r(buf + 6, size_t(proto_len));
+    bool seen[5] = {false, false, false, false, false};
+    while (r.more()) {
+        const uint64_t key = r.varint();
+        const int field = int(key >> 3), wt = int(key & 7);
+        if (field == 1 && wt == 1) offset_in_block = int64_t(r.fixed64()), seen[1] = true;
+        else if (field == 2 && wt == 1) seqno = int64_t(r.fixed64()), seen[2] = true;
+        else if (field == 3 && wt == 0) last_packet_in_block = r.varint() != 0, seen[3] = true;
+        else if (field == 4 && wt == 5) data_len = int32_t(r.fixed32()), seen[4] = true;
+        else if (field == 5 && wt == 0) sync_block = r.varint() != 0;
+        else r.skip(wt);
+    }
+    // required fields (datatransfer.proto:144-148)
+    return r.ok && seen[1] && seen[2] && seen[3] && seen[4];
+}
+
+bool PacketHeader::sanity_check(int64_t last_seqno) const {
+    if (data_len <= 0 && !last_packet_in_block) return false;   // only the last may be empty
+    if (last_packet_in_block && data_len != 0) return false;    // the last carries no data
+    if (seqno != last_seqno + 1) return false;                  // seqnos increase by one
+    return true;
+}
+
+// ---- requests / responses -----------------------------------------------------
+
+static std::string encode_extended_block(const ExtendedBlock &b) {
+    std::string s;
+    put_bytes(s, 1, b.pool_id);
+    put_uint(s, 2, b.block_id);
+    put_uint(s, 3, b.generation_stamp);
+    put_uint(s, 4, b.num_bytes);
+    return s;
+}
+
+std::string encode_read_block(const ReadBlockRequest &r) {
+    // TokenProto with empty fields (all four are required; security is out of scope)
+    std::string token;
+    put_bytes(token, 1, "");
+    put_bytes(token, 2, "");
+    put_bytes(token, 3, "");
+    put_bytes(token, 4, "");
+    std::string base;
+    put_bytes(base, 1, encode_extended_block(r.block));
+    put_bytes(base, 2, token);
+    std::string client_header;
+    put_bytes(client_header, 1, base);
+    put_bytes(client_header, 2, r.client_name);
+    std::string op;
+    put_bytes(op, 1, client_header);
+    put_uint(op, 2, r.offset);
+    put_uint(op, 3, r.len);
+    if (!r.send_checksums) put_uint(op, 4, 0);
+
+    std::string out;
+    out.push_back(char(kDataTransferVersion >> 8));
+    out.push_back(char(kDataTransferVersion & 0xFF));
+    out.push_back(char(kOpReadBlock));
+    put_varint(out, op.size());
+    out += op;
+    return out;
+}
+
+static bool decode_extended_block(const std::string &s, ExtendedBlock &b) {
+    Reader r(s.data(), s.size());
+    while (r.more()) {
+        const uint64_t key = r.varint();
+        const int field = int(key >> 3), wt = int(key & 7);
+        if (field == 1 && wt == 2) b.pool_id = r.bytes();
+        else if (field == 2 && wt == 0) b.block_id = r.varint();
+        else if (field == 3 && wt == 0) b.generation_stamp = r.varint();
+        else if (field == 4 && wt == 0) b.num_bytes = r.varint();
+        else r.skip(wt);
+    }
+    return r.ok;
+}
+
+bool decode_read_block(const void *proto, size_t n, ReadBlockRequest &out) {
+    Reader r(proto, n);
+    while (r.more()) {
+        const uint64_t key = r.varint();
+        const int field = int(key >> 3), wt = int(key & 7);
+        if (field == 1 && wt == 2) {
+            const std::string ch = r.bytes();
+            Reader h(ch.data(), ch.size());
+            while (h.more()) {
+                const uint64_t k2 = h.varint();
+                const int f2 = int(k2 >> 3), w2 = int(k2 & 7);
+                if (f2 == 1 && w2 == 2) {
+                    const std::string base = h.bytes();
+                    Reader b(base.data(), base.size());
+                    while (b.more()) {
+                        const uint64_t k3 = b.varint();
+                        const int f3 = int(k3 >> 3), w3 = int(k3 & 7);
+                        if (f3 == 1 && w3 == 2) {
+                            if (!decode_extended_block(b.bytes(), out.block)) return false;
+                        } else {
+                            b.skip(w3);
+                        }
+                    }
+                    if (!b.ok) return false;
+                } else if (f2 == 2 && w2 == 2) {
+                    out.client_name = h.bytes();
+                } else {
+                    h.skip(w2);
+                }
+            }
+            if (!h.ok) return false;
+        } else if (field == 2 && wt == 0) {
+            out.offset = r.varint();
+        } else if (field == 3 && wt == 0) {
+            out.len = r.varint();
+        } else if (field == 4 && wt == 0) {
+            out.send_checksums = r.varint() != 0;
+        } else {
+            r.skip(wt);
+        }
+    }
+    return r.ok;
+}
+
+std::string encode_block_op_response(const BlockOpResponse &r) {
+    std::string out;
+    put_uint(out, 1, uint64_t(r.status));
+    if (r.has_checksum_info) {
+        std::string cs;
+        put_uint(cs, 1, uint64_t(r.checksum_type));
+        put_uint(cs, 2, r.bytes_per_checksum);
+        std::string info;
+        put_bytes(info, 1, cs);
+        put_uint(info, 2, r.chunk_offset);
+        put_bytes(out, 4, info);
+    }
+    if (!r.message.empty()) put_bytes(out, 5, r.message);
+    return out;
+}
+
+bool decode_block_op_response(const void *proto, size_t n, BlockOpResponse &out) {
+    Reader r(proto, n);
+    bool have_status = false;
+    while (r.more()) {
+        const uint64_t key = r.varint();
+        const int field = int(key >> 3), wt = int(key & 7);
+        if (field == 1 && wt == 0) {
+            out.status = int(r.varint());
+            have_status = true;
+        } else if (field == 4 && wt == 2) {
+            const std::string info = r.bytes();
+            Reader i(info.data(), info.size());
+            while (i.more()) {
+                const uint64_t k2 = i.varint();
+                const int f2 = int(k2 >> 3), w2 = int(k2 & 7);
+                if (f2 == 1 && w2 == 2) {
+                    const std::string cs = i.bytes();
+                    Reader c(cs.data(), cs.size());
+                    while (c.more()) {
+                        const uint64_t k3 = c.varint();
+                        const int f3 = int(k3 >> 3), w3 = int(k3 & 7);
+                        if (f3 == 1 && w3 == 0) out.checksum_type = int(c.varint());
+                        else if (f3 == 2 && w3 == 0) out.bytes_per_checksum = uint32_t(c.varint());
+                        else c.skip(w3);
+                    }
+                    if (!c.ok) return false;
+                } else if (f2 == 2 && w2 == 0) {
+                    out.chunk_offset = i.varint();
+                } else {
+                    i.skip(w2);
+                }
+            }
+            if (!i.ok) return false;
+            out.has_checksum_info = true;
+        } else if (field == 5 && wt == 2) {
+            out.message = r.bytes();
+        } else {
+            r.skip(wt);
+        }
+    }
+    return r.ok && have_status;
+}
+
+std::string encode_client_read_status(int status) {
+    std::string out;
+    put_uint(out, 1, uint64_t(status));
+    return out;
+}
+
+bool decode_client_read_status(const void *proto, size_t n, int &status) {
+    Reader r(proto, n);
+    bool have = false;
+    while (r.more()) {
+        const uint64_t key = r.varint();
+        const int field = int(key >> 3), wt = int(key & 7);
+        if (field == 1 && wt == 0) {
+            status = int(r.varint());
+            have = true;
+        } else {
+            r.skip(wt);
+        }
+    }
+    return r.ok && have;
+}
+
+}  // namespace wire
+}  // namespace hdfs3crc

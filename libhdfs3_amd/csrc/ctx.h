@@ -1,0 +1,47 @@
+// Internal: the hdfs3_crc_ctx definition, shared by the C-ABI (hdfs3_crc.cpp) and the
+// block reader (client/block_reader.cpp). Not installed.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "crc32c_kernels.h"
+
+namespace hdfs3crc {
+
+// Sets the thread-local message returned by hdfs3_crc_last_error(); returns `code`.
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+
+// Staging segment of the host-buffer API: 16 MiB of payload per H2D transfer.
+constexpr size_t kSegmentBytes = 16u << 20;
+
+struct Slot {
+    uint8_t *h_data = nullptr, *h_crc = nullptr;  // pinned
+    uint8_t *d_data = nullptr, *d_crc = nullptr;  // device
+    size_t data_cap = 0, crc_cap = 0;
+    hipEvent_t done = nullptr;
+    // compute: CRC bytes waiting in h_crc to be copied out once `done` fires
+    uint8_t *pending_out = nullptr;
+    size_t pending_bytes = 0;
+};
+
+}  // namespace hdfs3crc
+
+struct hdfs3_crc_ctx {
+    int device = 0;
+    int grid_cap = 256;            // one 1024-thread workgroup per CU (128 KiB LDS image)
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t *d_tables = nullptr;  // 4 x 256 slice-table image
+    uint32_t *d_fold = nullptr;    // lane-fold GF(2) matrices (crc32c_tables.h)
+    unsigned long long *d_result = nullptr;
+    unsigned long long *h_result = nullptr;  // pinned
+    hdfs3crc::DevPacket *d_pk = nullptr;
+    hdfs3crc::DevPacket *h_pk = nullptr;               // pinned
+    size_t pk_cap = 0;
+    hdfs3crc::Slot slot[2];
+    uint64_t launches = 0;
+};
+

@@ -17,6 +17,7 @@
 
 #include "crc32c_kernels.h"
 #include "crc32c_tables.h"
+#include "ctx.h"
 
 namespace hdfs3crc {
 uint32_t host_update(uint32_t state, const void *p, size_t n);
@@ -24,7 +25,7 @@ uint32_t host_update(uint32_t state, const void *p, size_t n);
 
 using namespace hdfs3crc;
 
-namespace {
+namespace hdfs3crc {
 
 thread_local char g_err[512] = "";
 
@@ -35,6 +36,10 @@ int fail(int code, const char *fmt, ...) {
     va_end(ap);
     return code;
 }
+
+}  // namespace hdfs3crc
+
+namespace {
 
 int hip_fail(hipError_t e, const char *what) {
     const int code = e == hipErrorOutOfMemory ? -ENOMEM
@@ -50,36 +55,7 @@ int hip_fail(hipError_t e, const char *what) {
         if (e_ != hipSuccess) return hip_fail(e_, #expr); \
     } while (0)
 
-// Staging segment of the host-buffer API: 16 MiB of payload per H2D transfer.
-constexpr size_t kSegmentBytes = 16u << 20;
-
-struct Slot {
-    uint8_t *h_data = nullptr, *h_crc = nullptr;  // pinned
-    uint8_t *d_data = nullptr, *d_crc = nullptr;  // device
-    size_t data_cap = 0, crc_cap = 0;
-    hipEvent_t done = nullptr;
-    // compute: CRC bytes waiting in h_crc to be copied out once `done` fires
-    uint8_t *pending_out = nullptr;
-    size_t pending_bytes = 0;
-};
-
 }  // namespace
-
-struct hdfs3_crc_ctx {
-    int device = 0;
-    int grid_cap = 256;            // one 1024-thread workgroup per CU (128 KiB LDS image)
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    uint32_t *d_tables = nullptr;  // 4 x 256 slice-table image
-    uint32_t *d_fold = nullptr;    // lane-fold GF(2) matrices (crc32c_tables.h)
-    unsigned long long *d_result = nullptr;
-    unsigned long long *h_result = nullptr;  // pinned
-    DevPacket *d_pk = nullptr;
-    DevPacket *h_pk = nullptr;               // pinned
-    size_t pk_cap = 0;
-    Slot slot[2];
-    uint64_t launches = 0;
-};
 
 namespace {
 

@@ -183,3 +183,60 @@ def update_host(state: int, data: bytes | np.ndarray) -> int:
     """Checksum::update on a raw state (sub-chunk streaming shim)."""
     buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
     return int(_native.lib().hdfs3_crc32c_update_host(state, _ptr(buf) if buf.nbytes else None, buf.nbytes))
+
+
+class BlockReader:
+    """hdfs3_block_reader (include/hdfs3_client.h): RemoteBlockReader with batched GPU verify."""
+
+    def __init__(self, host: str, port: int, block_id: int, start: int, length: int, *, device: int = 0,
+                 verify: bool = True, batch_packets: int = 64, timeout_ms: int = 60000,
+                 pool_id: bytes = b"BP-loopback", generation_stamp: int = 1, num_bytes: int = 0):
+        self._lib = _native.lib()
+        blk = _native.BlockId(pool_id, block_id, generation_stamp, num_bytes)
+        opts = _native.ReaderOpts(device, int(verify), batch_packets, timeout_ms)
+        p = c_void_p()
+        check("hdfs3_block_reader_open",
+              self._lib.hdfs3_block_reader_open(host.encode(), port, byref(blk), start, length, b"libhdfs3_amd",
+                                                byref(opts), byref(p)))
+        self.r = p.value
+
+    def read_into(self, out: np.ndarray, offset: int = 0, n: int | None = None) -> int:
+        """RemoteBlockReader::read into out[offset:offset+n]; returns bytes (0 = end of range)."""
+        n = out.nbytes - offset if n is None else n
+        got = self._lib.hdfs3_block_reader_read(self.r, out.ctypes.data + offset, min(n, 0x7FFFFFFF))
+        if got < 0:
+            check("hdfs3_block_reader_read", got)
+        return got
+
+    def read_all(self, length: int, chunk: int = 1 << 20) -> np.ndarray:
+        out = np.empty(length, dtype=np.uint8)
+        pos = 0
+        while pos < length:
+            got = self.read_into(out, pos, min(chunk, length - pos))
+            if got == 0:
+                break
+            pos += got
+        return out[:pos]
+
+    def stats(self):
+        from ctypes import c_uint32, c_uint64
+        bpc, pk, b = c_uint32(), c_uint64(), c_uint64()
+        check("hdfs3_block_reader_stats", self._lib.hdfs3_block_reader_stats(self.r, byref(bpc), byref(pk), byref(b)))
+        return {"bytes_per_checksum": bpc.value, "packets": pk.value, "gpu_batches": b.value}
+
+    def close(self):
+        if self.r:
+            self._lib.hdfs3_block_reader_close(self.r)
+            self.r = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

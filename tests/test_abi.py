@@ -11,10 +11,11 @@ import pytest
 from util import REPO, read_checksum1, read_checksum2
 
 HEADER = os.path.join(REPO, "include", "hdfs3_crc.h")
+CLIENT_HEADER = os.path.join(REPO, "include", "hdfs3_client.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(hdfs3_\w+)\s*\(", src)))
 
@@ -34,6 +35,9 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # the Python binding covers exactly the header
     assert sorted(_native.PUBLIC_API) == declared_functions()
+    client = declared_functions(CLIENT_HEADER)
+    assert client and not [n for n in client if not hasattr(lib, n)]
+    assert sorted(_native.CLIENT_API) == client
 
 
 def test_library_is_gfx950_code_object():

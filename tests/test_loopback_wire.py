@@ -1,0 +1,104 @@
+"""CPU tests of the data-transfer wire path: the loopback datanode (C++, the product's
+wire codec) against an independent Python client (tests/dtp.py). Checks the OP_READ_BLOCK
+framing, BlockOpResponseProto/ChecksumProto, packet headers (31 bytes, seqno, offsets,
+packetLen = dataLen + CRC bytes + 4), chunk-aligned first packet, the empty last packet,
+the final CHECKSUM_OK status, and every CRC word against the oracle."""
+import numpy as np
+import pytest
+
+from dtp import Conn, packet_header, parse_packet_header
+from util import oracle_compute, ptr, splitmix_bytes
+
+
+@pytest.fixture(scope="module")
+def datanode():
+    from libhdfs3_amd import _native
+
+    lb = _native.loopback()
+    import ctypes
+    port = ctypes.c_int(0)
+    assert lb.hdfs3_loopback_start(ctypes.byref(port)) == 0
+    keep = []
+
+    def add(block_id, data, bpc, crc=None, ctype=2):
+        crc = oracle_compute(data, bpc) if crc is None else crc
+        keep.append((data, crc))
+        assert lb.hdfs3_loopback_add_block(block_id, ptr(data), data.nbytes, ptr(crc), bpc, ctype) == 0
+        return crc
+
+    yield lb, port.value, add
+    lb.hdfs3_loopback_stop()
+
+
+def test_packet_header_layout_matches_reference_size():
+    h = packet_header(4 + 512 + 4, 4096, 3, False, 512)
+    assert len(h) == 31  # PacketHeader::GetPkgHeaderSize (PacketHeader.cpp:38-45)
+    assert parse_packet_header(h) == {"packet_len": 520, "offset": 4096, "seqno": 3, "last": False,
+                                      "data_len": 512}
+
+
+@pytest.mark.parametrize("bpc", [512, 4096])
+def test_full_block_read(datanode, bpc):
+    lb, port, add = datanode
+    data = splitmix_bytes(1 << 20, bpc)
+    crc = add(100 + bpc, data, bpc)
+    c = Conn(port)
+    resp, packets = c.read_block(100 + bpc, 0, data.nbytes)
+    c.send_status(6)
+    c.close()
+    assert resp[1][0] == 0
+    got, words = bytearray(), bytearray()
+    for i, (h, cb, d) in enumerate(packets):
+        assert h["seqno"] == i
+        if h["last"]:
+            assert h["data_len"] == 0 and h["packet_len"] == 4 and i == len(packets) - 1
+            continue
+        assert h["offset"] == len(got)
+        assert h["packet_len"] == 4 + h["data_len"] + len(cb)
+        got += d
+        words += cb
+    assert bytes(got) == data.tobytes()
+    assert bytes(words) == crc.tobytes()
+    # every CRC word as the datanode served it checks out against the oracle
+    assert np.array_equal(np.frombuffer(bytes(words), np.uint8), oracle_compute(data, bpc))
+
+
+def test_ranged_read_aligns_back_to_chunk(datanode):
+    lb, port, add = datanode
+    data = splitmix_bytes(300_000 + 77, 9)  # short last chunk
+    add(7, data, 512)
+    c = Conn(port)
+    resp, packets = c.read_block(7, 1000, 5000)
+    c.send_status(6)
+    c.close()
+    from dtp import parse
+    info = parse(resp[4][0])
+    assert info[2][0] == 1000 - 1000 % 512  # ReadOpChecksumInfoProto.chunkOffset
+    first = packets[0][0]
+    assert first["offset"] == 512 and first["offset"] <= 1000
+    end = packets[-2][0]["offset"] + packets[-2][0]["data_len"]
+    assert end >= 6000 and end % 512 == 0
+
+
+def test_unknown_block_is_an_error_response(datanode):
+    lb, port, add = datanode
+    c = Conn(port)
+    resp, packets = c.read_block(999_999, 0, 10)
+    c.close()
+    assert resp[1][0] != 0 and not packets
+
+
+def test_status_reaches_datanode(datanode):
+    import time
+    lb, port, add = datanode
+    data = splitmix_bytes(70_000, 3)
+    add(55, data, 512)
+    c = Conn(port)
+    c.read_block(55, 0, data.nbytes)
+    c.send_status(6)
+    c.close()
+    for _ in range(100):
+        if lb.hdfs3_loopback_last_status() == 6:
+            break
+        time.sleep(0.01)
+    assert lb.hdfs3_loopback_last_status() == 6  # DT_PROTO_CHECKSUM_OK
