@@ -12,7 +12,8 @@ HOSTFLAGS:= -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
 LIB      := $(LIBDIR)/libhdfs3_crc.so
 LOOPBACK := $(LIBDIR)/libhdfs3_loopback.so
 OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc32c.o \
-            $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/client_block_reader.o
+            $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/client_block_reader.o \
+            $(OBJDIR)/client_input_stream.o
 
 all: $(LIB) $(LOOPBACK) oracle
 
@@ -36,7 +37,11 @@ $(OBJDIR)/client_net.o: $(CSRC)/client/net.cpp $(CSRC)/client/net.h
 	@mkdir -p $(OBJDIR)
 	g++ $(HOSTFLAGS) -c $< -o $@
 
-$(OBJDIR)/client_block_reader.o: $(CSRC)/client/block_reader.cpp include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h $(CSRC)/client/wire.h $(CSRC)/client/net.h
+$(OBJDIR)/client_block_reader.o: $(CSRC)/client/block_reader.cpp $(CSRC)/client/block_reader.h include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h $(CSRC)/client/wire.h $(CSRC)/client/net.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(OBJDIR)/client_input_stream.o: $(CSRC)/client/input_stream.cpp $(CSRC)/client/block_reader.h include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 

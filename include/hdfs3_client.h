@@ -62,6 +62,54 @@ int hdfs3_block_reader_stats(hdfs3_block_reader *r, uint32_t *bytes_per_checksum
                              uint64_t *packets, uint64_t *gpu_batches);
 int hdfs3_block_reader_close(hdfs3_block_reader *r);
 
+/* ------------------------------------------------------------------------------------
+ * Input stream: the hdfsRead / hdfsPread / hdfsSeek / hdfsTell / hdfsAvailable surface
+ * (Hdfs.cpp:788-862, 924-941) over InputStreamImpl's block walk and replica failover
+ * (InputStreamImpl.cpp:322-450, 583-815, 1120-1160), reading every block through
+ * hdfs3_block_reader. The namenode lookup (getBlockLocations) is outside the checksum
+ * path: the caller passes the LocatedBlocks it would have received.
+ *
+ * Error convention of these five calls is hdfs.h's, not the -errno of the rest of this
+ * header, so they drop in behind hdfsRead & co unchanged: -1 with errno set
+ *   EIO       every replica failed (ChecksumException or I/O) — the reference's
+ *             HdfsIOException "all nodes have been tried" (InputStreamImpl.cpp:369-383)
+ *   EOVERFLOW seek past the end of file (HdfsEndOfStream, Hdfs.cpp:276-277)
+ *   EINVAL    bad arguments (PARAMETER_ASSERT)
+ * and the message in hdfs3_crc_last_error(). read returns 0 at end of file.
+ * ---------------------------------------------------------------------------------- */
+typedef struct hdfs3_input_stream hdfs3_input_stream;
+
+typedef struct hdfs3_datanode {  /* DatanodeInfo transfer address */
+    const char *host;
+    int port;
+} hdfs3_datanode;
+
+typedef struct hdfs3_located_block {  /* LocatedBlockProto (hdfs.proto) */
+    hdfs3_block_id block;             /* block.num_bytes = bytes of the block in the file */
+    int64_t offset;                   /* file offset of the block's first byte            */
+    const hdfs3_datanode *replicas;   /* in the namenode's preference order               */
+    int n_replicas;
+} hdfs3_located_block;
+
+/* Blocks must be in file order and contiguous (offset[i+1] = offset[i] + num_bytes[i]);
+ * the table and host strings are copied. One GPU context per stream. 0 or -errno. */
+int hdfs3_input_open(const hdfs3_located_block *blocks, int n_blocks, const char *client_name,
+                     const hdfs3_reader_opts *opts, hdfs3_input_stream **out);
+/* hdfsRead: up to len bytes from the cursor, never crossing a block boundary (readOneBlock) */
+int32_t hdfs3_input_read(hdfs3_input_stream *s, void *buf, int32_t len);
+/* hdfsPread: reads [pos, pos+len) clipped to the file, across blocks; cursor unchanged.
+ * pos outside the file returns -1 (preadInternal, InputStreamImpl.cpp:815-830). */
+int32_t hdfs3_input_pread(hdfs3_input_stream *s, int64_t pos, void *buf, int32_t len);
+/* hdfsSeek: a forward seek of <= 128 KiB inside the current block skips through the open
+ * reader (InputStreamImpl.cpp:1146-1152); anything else reopens at the target. */
+int hdfs3_input_seek(hdfs3_input_stream *s, int64_t pos);
+int64_t hdfs3_input_tell(hdfs3_input_stream *s);
+int hdfs3_input_available(hdfs3_input_stream *s);
+int64_t hdfs3_input_length(hdfs3_input_stream *s);
+/* replica failovers and block readers opened so far (diagnostics) */
+int hdfs3_input_stats(hdfs3_input_stream *s, uint64_t *failovers, uint64_t *readers_opened);
+int hdfs3_input_close(hdfs3_input_stream *s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,6 +79,19 @@ class ReaderOpts(ctypes.Structure):
     _fields_ = [("device", c_int), ("verify", c_int), ("batch_packets", c_int), ("timeout_ms", c_int)]
 
 
+class Datanode(ctypes.Structure):
+    """hdfs3_datanode (include/hdfs3_client.h)."""
+
+    _fields_ = [("host", ctypes.c_char_p), ("port", c_int)]
+
+
+class LocatedBlock(ctypes.Structure):
+    """hdfs3_located_block (include/hdfs3_client.h)."""
+
+    _fields_ = [("block", BlockId), ("offset", c_int64), ("replicas", POINTER(Datanode)),
+                ("n_replicas", c_int)]
+
+
 # every symbol include/hdfs3_client.h declares
 CLIENT_API = {
     "hdfs3_block_reader_open": (c_int, [ctypes.c_char_p, c_int, POINTER(BlockId), c_int64, c_int64,
@@ -87,6 +100,16 @@ CLIENT_API = {
     "hdfs3_block_reader_available": (c_int64, [c_void_p]),
     "hdfs3_block_reader_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint64), POINTER(c_uint64)]),
     "hdfs3_block_reader_close": (c_int, [c_void_p]),
+    "hdfs3_input_open": (c_int, [POINTER(LocatedBlock), c_int, ctypes.c_char_p, POINTER(ReaderOpts),
+                                 POINTER(c_void_p)]),
+    "hdfs3_input_read": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),
+    "hdfs3_input_pread": (ctypes.c_int32, [c_void_p, c_int64, c_void_p, ctypes.c_int32]),
+    "hdfs3_input_seek": (c_int, [c_void_p, c_int64]),
+    "hdfs3_input_tell": (c_int64, [c_void_p]),
+    "hdfs3_input_available": (c_int, [c_void_p]),
+    "hdfs3_input_length": (c_int64, [c_void_p]),
+    "hdfs3_input_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "hdfs3_input_close": (c_int, [c_void_p]),
 }
 
 # measurement hooks (bench.py only; not in the public header)
@@ -102,7 +125,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise ImportError(f"{path} is missing: run `make` (or __graft_entry__.build()) first; "
                           "libhdfs3_amd has no CPU fallback")
-    lib = ctypes.CDLL(path)
+    lib = ctypes.CDLL(path, use_errno=True)  # the hdfs.h-style calls report through errno
     for table in (PUBLIC_API, CLIENT_API, BENCH_API):
         for name, (res, args) in table.items():
             fn = getattr(lib, name)
@@ -135,13 +158,13 @@ def loopback() -> ctypes.CDLL:
         lb.hdfs3_loopback_start.restype = c_int
         lb.hdfs3_loopback_start.argtypes = [POINTER(c_int)]
         lb.hdfs3_loopback_add_block.restype = c_int
-        lb.hdfs3_loopback_add_block.argtypes = [c_uint64, c_void_p, c_uint64, c_void_p, c_uint32, c_int]
-        lb.hdfs3_loopback_clear_blocks.restype = None
-        lb.hdfs3_loopback_set_packet_bytes.restype = None
-        lb.hdfs3_loopback_set_packet_bytes.argtypes = [c_int]
-        lb.hdfs3_loopback_served_bytes.restype = c_uint64
-        lb.hdfs3_loopback_last_status.restype = c_int
-        lb.hdfs3_loopback_stop.restype = c_int
+        lb.hdfs3_loopback_add_block.argtypes = [c_int, c_uint64, c_void_p, c_uint64, c_void_p, c_uint32, c_int]
+        for fn, args, res in [("clear_blocks", [c_int], c_int), ("set_packet_bytes", [c_int, c_int], c_int),
+                              ("set_fail_after", [c_int, c_int64], c_int), ("served_bytes", [c_int], c_uint64),
+                              ("requests", [c_int], c_uint64), ("last_status", [c_int], c_int),
+                              ("stop", [c_int], c_int)]:
+            f = getattr(lb, "hdfs3_loopback_" + fn)
+            f.argtypes, f.restype = args, res
         _LOOPBACK = lb
     return _LOOPBACK
 

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../ctx.h"
+#include "block_reader.h"
 #include "hdfs3_crc.h"
 #include "net.h"
 #include "wire.h"
@@ -114,6 +115,7 @@ struct hdfs3_block_reader {
     int batch_packets = kDefaultBatchPackets;
     bool verify = true;
     hdfs3_crc_ctx *ctx = nullptr;
+    bool own_ctx = true;       // false when borrowed from an input stream
     wire::ExtendedBlock block;
     int64_t start = 0, end_offset = 0;
     int64_t recv_cursor = 0;   // "cursor" as seen by readNextPacket for the next packet
@@ -335,16 +337,16 @@ struct hdfs3_block_reader {
     ~hdfs3_block_reader() {
         if (ctx) (void)hipStreamSynchronize(ctx->stream);
         for (Batch &b : slot) b.release();
-        if (ctx) hdfs3_crc_ctx_destroy(ctx);
+        if (ctx && own_ctx) hdfs3_crc_ctx_destroy(ctx);
         net::close_fd(fd);
     }
 };
 
-extern "C" {
+namespace hdfs3crc {
 
-int hdfs3_block_reader_open(const char *host, int port, const hdfs3_block_id *blk, int64_t start,
-                            int64_t len, const char *client_name, const hdfs3_reader_opts *opts,
-                            hdfs3_block_reader **out) {
+int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int64_t start, int64_t len,
+                      const char *client_name, const hdfs3_reader_opts *opts, hdfs3_crc_ctx *shared_ctx,
+                      hdfs3_block_reader **out) {
     if (!out || !host || !blk || start < 0 || len < 0) return fail(-EINVAL, "invalid argument");
     *out = nullptr;
     hdfs3_block_reader *r = new (std::nothrow) hdfs3_block_reader();
@@ -359,7 +361,10 @@ int hdfs3_block_reader_open(const char *host, int port, const hdfs3_block_id *bl
     r->block.num_bytes = blk->num_bytes;
     r->start = r->recv_cursor = start;
     r->end_offset = start + len;
-    if (int rc = hdfs3_crc_ctx_create(device, &r->ctx)) {
+    if (shared_ctx) {
+        r->ctx = shared_ctx;
+        r->own_ctx = false;
+    } else if (int rc = hdfs3_crc_ctx_create(device, &r->ctx)) {
         delete r;
         return rc;
     }
@@ -385,6 +390,16 @@ int hdfs3_block_reader_open(const char *host, int port, const hdfs3_block_id *bl
     }
     *out = r;
     return 0;
+}
+
+}  // namespace hdfs3crc
+
+extern "C" {
+
+int hdfs3_block_reader_open(const char *host, int port, const hdfs3_block_id *blk, int64_t start,
+                            int64_t len, const char *client_name, const hdfs3_reader_opts *opts,
+                            hdfs3_block_reader **out) {
+    return open_block_reader(host, port, blk, start, len, client_name, opts, nullptr, out);
 }
 
 int32_t hdfs3_block_reader_read(hdfs3_block_reader *r, void *buf, int32_t len) {

@@ -1,0 +1,309 @@
+// hdfs3_input_stream: InputStreamImpl's read/pread/seek over located blocks with replica
+// failover (src/client/InputStreamImpl.cpp), every block read through the GPU-verifying
+// hdfs3_block_reader. The C entry points keep hdfs.h's -1/errno convention (Hdfs.cpp:826-862).
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../ctx.h"
+#include "block_reader.h"
+#include "hdfs3_client.h"
+#include "hdfs3_crc.h"
+
+using namespace hdfs3crc;
+
+namespace {
+
+constexpr int64_t kMaxSkip = 128 * 1024;  // InputStreamImpl.cpp:1146
+
+struct Node {
+    std::string host;
+    int port;
+    bool operator==(const Node &o) const { return port == o.port && host == o.host; }
+};
+
+struct Block {
+    std::string pool;
+    hdfs3_block_id id;
+    int64_t offset, length;
+    std::vector<Node> replicas;
+};
+
+// hdfs.h convention: errno + -1; the message goes where hdfs3_crc_last_error reads it
+int posix_fail(int err, const std::string &msg) {
+    fail(-err, "%s", msg.c_str());
+    errno = err;
+    return -1;
+}
+
+}  // namespace
+
+struct hdfs3_input_stream {
+    std::vector<Block> blocks;
+    int64_t file_length = 0;
+    hdfs3_reader_opts opts{0, 1, 0, 0};
+    std::string client_name;
+    hdfs3_crc_ctx *ctx = nullptr;
+    int64_t cursor = 0;
+    int64_t end_of_cur_block = 0;
+    int cur = -1;
+    hdfs3_block_reader *reader = nullptr;
+    Node cur_node;
+    std::vector<Node> failed;  // failedNodes
+    uint64_t failovers = 0, opened = 0;
+    std::string last_error;
+
+    ~hdfs3_input_stream() {
+        drop_reader();
+        if (ctx) hdfs3_crc_ctx_destroy(ctx);
+    }
+
+    void drop_reader() {
+        if (reader) hdfs3_block_reader_close(reader);
+        reader = nullptr;
+    }
+
+    int find_block(int64_t pos) const {  // LocatedBlocks::findBlock
+        auto it = std::upper_bound(blocks.begin(), blocks.end(), pos,
+                                   [](int64_t p, const Block &b) { return p < b.offset; });
+        if (it == blocks.begin()) return -1;
+        const int i = int(it - blocks.begin()) - 1;
+        return pos < blocks[i].offset + blocks[i].length ? i : -1;
+    }
+
+    // choseBestNode (InputStreamImpl.cpp:322-335): first replica not yet failed
+    const Node *best_node(const Block &b) const {
+        for (const Node &n : b.replicas)
+            if (std::find(failed.begin(), failed.end(), n) == failed.end()) return &n;
+        return nullptr;
+    }
+
+    // setupBlockReader (:364-450) for [start, start+len) of block b; -errno
+    int setup(const Block &b, int64_t start, int64_t len, hdfs3_block_reader **out, Node *node) {
+        std::string why;
+        for (;;) {
+            const Node *n = best_node(b);
+            if (!n) {
+                last_error = "InputStreamImpl: all nodes have been tried and no valid replica can be read for Block: " +
+                             std::to_string(b.id.block_id) + (why.empty() ? "" : " (last: " + why + ")");
+                return -EIO;
+            }
+            hdfs3_block_id id = b.id;
+            id.pool_id = b.pool.c_str();
+            const int rc = open_block_reader(n->host.c_str(), n->port, &id, start, len, client_name.c_str(), &opts,
+                                             ctx, out);
+            if (rc == 0) {
+                *node = *n;
+                ++opened;
+                return 0;
+            }
+            if (rc == -ENOTSUP || rc == -ENOMEM) {  // not a replica problem: another node cannot help
+                last_error = hdfs3_crc_last_error();
+                return rc;
+            }
+            why = hdfs3_crc_last_error();
+            failed.push_back(*n);
+        }
+    }
+
+    void seek_to_block(int i) {  // seekToBlock: new block, fresh failed list
+        drop_reader();
+        cur = i;
+        end_of_cur_block = blocks[i].offset + blocks[i].length;
+        failed.clear();
+    }
+
+    // readOneBlock (:616-712)
+    int32_t read_one_block(uint8_t *buf, int32_t size) {
+        const Block &b = blocks[cur];
+        for (;;) {
+            if (!reader) {
+                const int64_t off = cursor - b.offset;
+                if (int rc = setup(b, off, b.length - off, &reader, &cur_node)) return rc;
+            }
+            const int32_t todo = int32_t(std::min<int64_t>(size, end_of_cur_block - cursor));
+            const int32_t n = hdfs3_block_reader_read(reader, buf, todo);
+            if (n > 0) {
+                cursor += n;
+                return n;
+            }
+            // ChecksumException or I/O failure: this replica is bad, try another (:682-708)
+            ++failovers;
+            failed.push_back(cur_node);
+            drop_reader();
+        }
+    }
+
+    int32_t read(uint8_t *buf, int32_t size) {
+        if (cursor >= file_length) return 0;  // HdfsEndOfStream -> hdfsRead returns 0
+        if (cursor >= end_of_cur_block || cur < 0) {
+            const int i = find_block(cursor);
+            if (i < 0) return -EIO;
+            seek_to_block(i);
+        }
+        return read_one_block(buf, size);
+    }
+
+    // fetchBlockByteRange (:955-1061): the whole range from one replica, else the next
+    int fetch_range(const Block &b, int64_t start, int64_t len, uint8_t *out) {
+        std::vector<Node> saved;
+        saved.swap(failed);
+        int rc = 0;
+        for (;;) {
+            hdfs3_block_reader *r = nullptr;
+            Node node;
+            if ((rc = setup(b, start, len, &r, &node))) break;
+            int64_t got = 0;
+            while (got < len) {
+                const int32_t n = hdfs3_block_reader_read(r, out + got, int32_t(std::min<int64_t>(len - got, 1 << 30)));
+                if (n <= 0) break;
+                got += n;
+            }
+            hdfs3_block_reader_close(r);
+            if (got == len) break;
+            ++failovers;
+            failed.push_back(node);
+        }
+        failed.swap(saved);
+        return rc;
+    }
+
+    int32_t pread(int64_t pos, uint8_t *buf, int32_t size) {
+        if (pos < 0 || pos >= file_length) return -EINVAL;
+        const int32_t real = int32_t(std::min<int64_t>(size, file_length - pos));
+        int64_t done = 0;
+        while (done < real) {
+            const int i = find_block(pos + done);
+            if (i < 0) return -EIO;
+            const Block &b = blocks[i];
+            const int64_t start = pos + done - b.offset;
+            const int64_t n = std::min<int64_t>(real - done, b.length - start);
+            if (int rc = fetch_range(b, start, n, buf + done)) return rc;
+            done += n;
+        }
+        return real;
+    }
+
+    int seek(int64_t pos) {  // seekInternal (:1133-1170)
+        if (pos == cursor) return 0;
+        if (pos > file_length) return -EOVERFLOW;
+        if (reader && pos > cursor && pos < end_of_cur_block && pos - cursor <= kMaxSkip) {
+            uint8_t scratch[16384];
+            bool ok = true;
+            while (cursor < pos) {
+                const int32_t n = hdfs3_block_reader_read(reader, scratch, int32_t(std::min<int64_t>(sizeof(scratch), pos - cursor)));
+                if (n <= 0) {
+                    ok = false;
+                    break;
+                }
+                cursor += n;
+            }
+            if (ok) return 0;
+        }
+        drop_reader();
+        end_of_cur_block = 0;
+        cursor = pos;
+        return 0;
+    }
+};
+
+extern "C" {
+
+int hdfs3_input_open(const hdfs3_located_block *blocks, int n_blocks, const char *client_name,
+                     const hdfs3_reader_opts *opts, hdfs3_input_stream **out) {
+    if (!out || n_blocks < 0 || (n_blocks && !blocks)) return fail(-EINVAL, "invalid argument");
+    *out = nullptr;
+    hdfs3_input_stream *s = new (std::nothrow) hdfs3_input_stream();
+    if (!s) return fail(-ENOMEM, "input stream allocation");
+    if (opts) s->opts = *opts;
+    s->client_name = client_name ? client_name : "libhdfs3_amd";
+    int64_t expect = n_blocks ? blocks[0].offset : 0;
+    for (int i = 0; i < n_blocks; ++i) {
+        const hdfs3_located_block &lb = blocks[i];
+        if (lb.offset != expect || int64_t(lb.block.num_bytes) < 0 || lb.n_replicas < 0 ||
+            (lb.n_replicas && !lb.replicas)) {
+            delete s;
+            return fail(-EINVAL, "located block %d is not contiguous with its predecessor or malformed", i);
+        }
+        Block b;
+        b.pool = lb.block.pool_id ? lb.block.pool_id : "";
+        b.id = lb.block;
+        b.id.pool_id = nullptr;
+        b.offset = lb.offset;
+        b.length = int64_t(lb.block.num_bytes);
+        for (int k = 0; k < lb.n_replicas; ++k) {
+            if (!lb.replicas[k].host) {
+                delete s;
+                return fail(-EINVAL, "replica %d of block %d has no host", k, i);
+            }
+            b.replicas.push_back(Node{lb.replicas[k].host, lb.replicas[k].port});
+        }
+        expect += b.length;
+        s->blocks.push_back(std::move(b));
+    }
+    if (n_blocks && blocks[0].offset != 0) {
+        delete s;
+        return fail(-EINVAL, "the first block must start at file offset 0");
+    }
+    s->file_length = expect;
+    if (int rc = hdfs3_crc_ctx_create(s->opts.device, &s->ctx)) {
+        delete s;
+        return rc;
+    }
+    *out = s;
+    return 0;
+}
+
+int32_t hdfs3_input_read(hdfs3_input_stream *s, void *buf, int32_t len) {
+    if (!s || !buf || len <= 0) return posix_fail(EINVAL, "hdfsRead: invalid argument");
+    s->last_error.clear();
+    const int32_t rc = s->read(static_cast<uint8_t *>(buf), len);
+    if (rc < 0) return posix_fail(-rc, s->last_error.empty() ? hdfs3_crc_last_error() : s->last_error);
+    return rc;
+}
+
+int32_t hdfs3_input_pread(hdfs3_input_stream *s, int64_t pos, void *buf, int32_t len) {
+    if (!s || !buf || len <= 0 || pos < 0) return posix_fail(EINVAL, "hdfsPread: invalid argument");
+    s->last_error.clear();
+    const int32_t rc = s->pread(pos, static_cast<uint8_t *>(buf), len);
+    if (rc == -EINVAL) return posix_fail(EINVAL, "hdfsPread: position outside the file");
+    if (rc < 0) return posix_fail(-rc, s->last_error.empty() ? hdfs3_crc_last_error() : s->last_error);
+    return rc;
+}
+
+int hdfs3_input_seek(hdfs3_input_stream *s, int64_t pos) {
+    if (!s || pos < 0) return posix_fail(EINVAL, "hdfsSeek: invalid argument");
+    if (int rc = s->seek(pos))
+        return posix_fail(-rc, "InputStreamImpl: seek over EOF, seek target: " + std::to_string(pos));
+    return 0;
+}
+
+int64_t hdfs3_input_tell(hdfs3_input_stream *s) {
+    if (!s) return posix_fail(EINVAL, "hdfsTell: invalid argument");
+    return s->cursor;
+}
+
+int hdfs3_input_available(hdfs3_input_stream *s) {
+    if (!s) return posix_fail(EINVAL, "hdfsAvailable: invalid argument");
+    const int64_t a = s->reader ? hdfs3_block_reader_available(s->reader) : 0;
+    return int(std::min<int64_t>(a, 0x7FFFFFFF));
+}
+
+int64_t hdfs3_input_length(hdfs3_input_stream *s) { return s ? s->file_length : -1; }
+
+int hdfs3_input_stats(hdfs3_input_stream *s, uint64_t *failovers, uint64_t *readers_opened) {
+    if (!s) return fail(-EINVAL, "null stream");
+    if (failovers) *failovers = s->failovers;
+    if (readers_opened) *readers_opened = s->opened;
+    return 0;
+}
+
+int hdfs3_input_close(hdfs3_input_stream *s) {
+    delete s;
+    return 0;
+}
+
+}  // extern "C"

@@ -128,6 +128,17 @@ int launch(hdfs3_crc_ctx *ctx, const ChunkLaunch &a, bool verify) {
     return 0;
 }
 
+// true when [p, p+len) is page-locked host memory the DMA engine can read directly
+// (hdfs3_host_malloc_pinned, hipHostRegister); pageable memory is staged instead
+bool is_pinned_host(const void *p) {
+    hipPointerAttribute_t attr{};
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable pointers report an error; clear it
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost && attr.hostPointer != nullptr;
+}
+
 // Host-buffer pipeline shared by compute and verify: segments of whole chunks
 // alternate between two pinned/device slots, so the CPU copy into pinned memory
 // of segment i+1 overlaps the DMA and kernel of segment i.
@@ -141,6 +152,7 @@ int host_pipeline(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc
         HIP_TRY(hipMemsetAsync(ctx->d_result, 0, sizeof(unsigned long long), ctx->stream));
     }
     const uint8_t *src = static_cast<const uint8_t *>(data);
+    const bool direct = is_pinned_host(data);  // skip the staging copy for pinned callers
     size_t off = 0;
     for (int k = 0; off < len; ++k) {
         Slot &s = ctx->slot[k & 1];
@@ -150,8 +162,8 @@ int host_pipeline(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc
         if (s.done) HIP_TRY(hipEventSynchronize(s.done));
         if (int rc = finish_pending(s)) return rc;
         if (int rc = grow_slot(s, seg, seg_crc)) return rc;
-        std::memcpy(s.h_data, src + off, n);
-        HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, n, hipMemcpyHostToDevice, ctx->stream));
+        if (!direct) std::memcpy(s.h_data, src + off, n);
+        HIP_TRY(hipMemcpyAsync(s.d_data, direct ? src + off : s.h_data, n, hipMemcpyHostToDevice, ctx->stream));
         ChunkLaunch a{};
         a.data = s.d_data;
         a.len = n;

@@ -240,3 +240,96 @@ class BlockReader:
             self.close()
         except Exception:
             pass
+
+
+class HdfsIOError(OSError):
+    """hdfs.h-style failure (-1 + errno) from an hdfs3_input_* call."""
+
+
+class InputStream:
+    """hdfs3_input_stream (include/hdfs3_client.h): hdfsRead/hdfsPread/hdfsSeek/hdfsTell over
+    located blocks with replica failover. `blocks` = [(block_id, num_bytes, [(host, port), ...])]
+    in file order."""
+
+    def __init__(self, blocks, *, device: int = 0, verify: bool = True, batch_packets: int = 64,
+                 timeout_ms: int = 60000, pool_id: bytes = b"BP-loopback", generation_stamp: int = 1):
+        self._lib = _native.lib()
+        arr = (_native.LocatedBlock * len(blocks))()
+        self._keep = []
+        off = 0
+        for i, (bid, nbytes, reps) in enumerate(blocks):
+            dn = (_native.Datanode * max(1, len(reps)))()
+            for k, (host, port) in enumerate(reps):
+                h = host.encode() if isinstance(host, str) else host
+                self._keep.append(h)
+                dn[k].host, dn[k].port = h, port
+            self._keep.append(dn)
+            arr[i].block = _native.BlockId(pool_id, bid, generation_stamp, nbytes)
+            arr[i].offset = off
+            arr[i].replicas = dn
+            arr[i].n_replicas = len(reps)
+            off += nbytes
+        opts = _native.ReaderOpts(device, int(verify), batch_packets, timeout_ms)
+        p = c_void_p()
+        check("hdfs3_input_open", self._lib.hdfs3_input_open(arr, len(blocks), b"libhdfs3_amd", byref(opts), byref(p)))
+        self.s = p.value
+
+    def _posix(self, fn: str, rc: int) -> int:
+        if rc < 0:
+            err = ctypes.get_errno()
+            raise HdfsIOError(err, f"{fn}: {self._lib.hdfs3_crc_last_error().decode(errors='replace')}")
+        return rc
+
+    def read_into(self, out: np.ndarray, offset: int = 0, n: int | None = None) -> int:
+        n = out.nbytes - offset if n is None else n
+        return self._posix("hdfsRead", self._lib.hdfs3_input_read(self.s, out.ctypes.data + offset, n))
+
+    def pread_into(self, pos: int, out: np.ndarray, offset: int = 0, n: int | None = None) -> int:
+        n = out.nbytes - offset if n is None else n
+        return self._posix("hdfsPread", self._lib.hdfs3_input_pread(self.s, pos, out.ctypes.data + offset, n))
+
+    def read_fully(self, length: int, chunk: int = 4 << 20) -> np.ndarray:
+        out = np.empty(length, dtype=np.uint8)
+        pos = 0
+        while pos < length:
+            got = self.read_into(out, pos, min(chunk, length - pos))
+            if got == 0:
+                break
+            pos += got
+        return out[:pos]
+
+    def seek(self, pos: int) -> None:
+        self._posix("hdfsSeek", self._lib.hdfs3_input_seek(self.s, pos))
+
+    def tell(self) -> int:
+        return self._posix("hdfsTell", self._lib.hdfs3_input_tell(self.s))
+
+    def available(self) -> int:
+        return self._posix("hdfsAvailable", self._lib.hdfs3_input_available(self.s))
+
+    @property
+    def length(self) -> int:
+        return int(self._lib.hdfs3_input_length(self.s))
+
+    def stats(self):
+        from ctypes import c_uint64
+        f, o = c_uint64(), c_uint64()
+        check("hdfs3_input_stats", self._lib.hdfs3_input_stats(self.s, byref(f), byref(o)))
+        return {"failovers": f.value, "readers_opened": o.value}
+
+    def close(self):
+        if self.s:
+            self._lib.hdfs3_input_close(self.s)
+            self.s = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -4,35 +4,29 @@ block bytes of [start, start+len); a full-chunk CRC mismatch raises ChecksumExce
 after the packets before it were delivered (RemoteBlockReader.cpp:306-326); a short tail
 mismatch is ignored (:319); CHECKSUM_OK is sent only after every packet verified (:289-304);
 verify=false reads without checking (InputStream verify flag)."""
-import ctypes
 import errno
-import time
 
 import numpy as np
 import pytest
 
-from util import oracle_compute, ptr, splitmix_bytes
+from util import oracle_compute, splitmix_bytes
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
 def dn():
-    from libhdfs3_amd import _native
+    from loopback import LoopbackDatanode
 
-    lb = _native.loopback()
-    port = ctypes.c_int(0)
-    assert lb.hdfs3_loopback_start(ctypes.byref(port)) == 0
-    keep = []
+    node = LoopbackDatanode()
 
     def add(block_id, data, bpc, crc=None, ctype=2):
         crc = oracle_compute(data, bpc) if crc is None else crc
-        keep.append((data, crc))
-        assert lb.hdfs3_loopback_add_block(block_id, ptr(data), data.nbytes, ptr(crc), bpc, ctype) == 0
+        node.add_block(block_id, data, crc, bpc, ctype)
         return crc
 
-    yield lb, port.value, add
-    lb.hdfs3_loopback_stop()
+    yield node, node.port, add
+    node.stop()
 
 
 def _read(port, block_id, start, length, **kw):
@@ -115,11 +109,7 @@ def test_checksum_ok_status_sent_after_verified_read(dn):
     add(6000, data, 512)
     out, _ = _read(port, 6000, 0, data.nbytes)
     assert np.array_equal(out, data)
-    for _ in range(200):
-        if lb.hdfs3_loopback_last_status() == 6:
-            break
-        time.sleep(0.01)
-    assert lb.hdfs3_loopback_last_status() == 6
+    assert lb.last_status(wait_for=6) == 6
 
 
 def test_unknown_block_fails_open(dn):
@@ -129,3 +119,46 @@ def test_unknown_block_fails_open(dn):
     lb, port, add = dn
     with pytest.raises(Hdfs3CrcError):
         BlockReader("127.0.0.1", port, 987654, 0, 100)
+
+
+def test_checksum_null_block_reads_without_verify(dn):
+    lb, port, add = dn
+    data = splitmix_bytes(300_000, 9)
+    lb.add_block(7000, data, None, 512, ctype=0)  # CHECKSUM_NULL: no CRC words on the wire
+    out, st = _read(port, 7000, 0, data.nbytes)
+    assert np.array_equal(out, data) and st["bytes_per_checksum"] == 512
+
+
+def test_crc32_type_is_reported_not_silently_skipped(dn):
+    from libhdfs3_amd.engine import BlockReader
+    from libhdfs3_amd._native import Hdfs3CrcError
+
+    lb, port, add = dn
+    data = splitmix_bytes(4096, 10)
+    lb.add_block(7001, data, np.zeros(32, np.uint8), 512, ctype=1)
+    with pytest.raises(Hdfs3CrcError) as ei:
+        BlockReader("127.0.0.1", port, 7001, 0, data.nbytes)
+    assert ei.value.rc == -errno.ENOTSUP
+
+
+def test_datanode_drop_mid_block_is_an_io_error(dn):
+    from libhdfs3_amd.engine import BlockReader
+    from libhdfs3_amd._native import Hdfs3CrcError
+    from loopback import LoopbackDatanode
+
+    node = LoopbackDatanode()
+    try:
+        data = splitmix_bytes(2 << 20, 11)
+        node.add_block(1, data, oracle_compute(data, 512), 512)
+        node.set_fail_after(1 << 20)
+        with BlockReader("127.0.0.1", node.port, 1, 0, data.nbytes, timeout_ms=5000) as r:
+            out = np.zeros(data.nbytes, np.uint8)
+            pos = 0
+            with pytest.raises(Hdfs3CrcError):
+                while True:
+                    got = r.read_into(out, pos, 1 << 16)
+                    assert got > 0
+                    pos += got
+            assert pos <= 1 << 20 and np.array_equal(out[:pos], data[:pos])
+    finally:
+        node.stop()

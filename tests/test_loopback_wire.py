@@ -7,27 +7,22 @@ import numpy as np
 import pytest
 
 from dtp import Conn, packet_header, parse_packet_header
-from util import oracle_compute, ptr, splitmix_bytes
+from util import oracle_compute, splitmix_bytes
 
 
 @pytest.fixture(scope="module")
 def datanode():
-    from libhdfs3_amd import _native
+    from loopback import LoopbackDatanode
 
-    lb = _native.loopback()
-    import ctypes
-    port = ctypes.c_int(0)
-    assert lb.hdfs3_loopback_start(ctypes.byref(port)) == 0
-    keep = []
+    dn = LoopbackDatanode()
 
     def add(block_id, data, bpc, crc=None, ctype=2):
         crc = oracle_compute(data, bpc) if crc is None else crc
-        keep.append((data, crc))
-        assert lb.hdfs3_loopback_add_block(block_id, ptr(data), data.nbytes, ptr(crc), bpc, ctype) == 0
+        dn.add_block(block_id, data, crc, bpc, ctype)
         return crc
 
-    yield lb, port.value, add
-    lb.hdfs3_loopback_stop()
+    yield dn, dn.port, add
+    dn.stop()
 
 
 def test_packet_header_layout_matches_reference_size():
@@ -89,7 +84,6 @@ def test_unknown_block_is_an_error_response(datanode):
 
 
 def test_status_reaches_datanode(datanode):
-    import time
     lb, port, add = datanode
     data = splitmix_bytes(70_000, 3)
     add(55, data, 512)
@@ -97,8 +91,4 @@ def test_status_reaches_datanode(datanode):
     c.read_block(55, 0, data.nbytes)
     c.send_status(6)
     c.close()
-    for _ in range(100):
-        if lb.hdfs3_loopback_last_status() == 6:
-            break
-        time.sleep(0.01)
-    assert lb.hdfs3_loopback_last_status() == 6  # DT_PROTO_CHECKSUM_OK
+    assert lb.last_status(wait_for=6) == 6  # DT_PROTO_CHECKSUM_OK

@@ -35,14 +35,30 @@ struct Block {
     int type;
 };
 
+// one loopback datanode, identified by its port; several run side by side to act as the
+// replicas of a block (InputStreamImpl failover)
+struct Server {
+    int listen_fd = -1;
+    std::atomic<bool> stop{false};
+    std::mutex mu;
+    std::map<uint64_t, Block> blocks;
+    std::atomic<int> packet_bytes{64 * 1024};
+    std::atomic<int64_t> fail_after{-1};  // drop the connection after this many data bytes
+    std::atomic<uint64_t> served{0};
+    std::atomic<uint64_t> requests{0};
+    std::atomic<int> last_status{-1};
+    std::atomic<int> active{0};
+    std::thread accept;
+};
+
 std::mutex g_mu;
-std::map<uint64_t, Block> g_blocks;
-std::atomic<int> g_listen_fd{-1};
-std::atomic<bool> g_stop{false};
-std::atomic<int> g_packet_bytes{64 * 1024};
-std::atomic<uint64_t> g_served{0};
-std::atomic<int> g_last_status{-1};
-std::thread g_accept;
+std::map<int, Server *> g_servers;
+
+Server *find(int port) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_servers.find(port);
+    return it == g_servers.end() ? nullptr : it->second;
+}
 
 int send_all_iov(int fd, iovec *iov, int n) {
     size_t total = 0;
@@ -71,7 +87,7 @@ int send_all_iov(int fd, iovec *iov, int n) {
     return 0;
 }
 
-void serve(int fd) {
+void serve(Server *sv, int fd) {
     const int to = 60000;
     uint8_t head[3];
     std::string proto;
@@ -81,13 +97,14 @@ void serve(int fd) {
         net::close_fd(fd);
         return;
     }
+    ++sv->requests;
     wire::BlockOpResponse resp;
     Block b{};
     bool found = false;
     {
-        std::lock_guard<std::mutex> lk(g_mu);
-        auto it = g_blocks.find(req.block.block_id);
-        if (it != g_blocks.end()) b = it->second, found = true;
+        std::lock_guard<std::mutex> lk(sv->mu);
+        auto it = sv->blocks.find(req.block.block_id);
+        if (it != sv->blocks.end()) b = it->second, found = true;
     }
     const int version = (head[0] << 8) | head[1];
     if (version != wire::kDataTransferVersion || head[2] != wire::kOpReadBlock || !found ||
@@ -110,13 +127,19 @@ void serve(int fd) {
         net::close_fd(fd);
         return;
     }
-    const uint64_t per = std::max<uint64_t>(b.bpc, uint64_t(g_packet_bytes.load()) / b.bpc * b.bpc);
+    const uint64_t per = std::max<uint64_t>(b.bpc, uint64_t(sv->packet_bytes.load()) / b.bpc * b.bpc);
     const uint32_t csize = b.type == wire::kChecksumNull ? 0 : 4;
+    const int64_t fail_after = sv->fail_after.load();
+    uint64_t sent = 0;
     int64_t seq = 0;
     for (uint64_t pos = first; pos < end; pos += per) {
         uint64_t n = end - pos < per ? end - pos : per;
         n = std::min<uint64_t>(((n + b.bpc - 1) / b.bpc) * b.bpc, b.len - pos);  // whole chunks
         const uint64_t chunks = (n + b.bpc - 1) / b.bpc;
+        if (fail_after >= 0 && sent + n > uint64_t(fail_after)) {  // injected datanode failure
+            net::close_fd(fd);
+            return;
+        }
         wire::PacketHeader h;
         h.packet_len = int32_t(4 + n + chunks * csize);
         h.offset_in_block = int64_t(pos);
@@ -132,7 +155,8 @@ void serve(int fd) {
             net::close_fd(fd);
             return;
         }
-        g_served += n;
+        sv->served += n;
+        sent += n;
         if (pos + n >= end) break;
     }
     wire::PacketHeader last;
@@ -148,21 +172,23 @@ void serve(int fd) {
         int status = -1;
         if (net::read_delimited(fd, st, 1024, 10000) == 0 &&
             wire::decode_client_read_status(st.data(), st.size(), status))
-            g_last_status = status;
+            sv->last_status = status;
     }
     net::close_fd(fd);
 }
 
-void accept_loop() {
-    for (;;) {
-        const int lfd = g_listen_fd.load();
-        if (lfd < 0 || g_stop) return;
-        const int fd = accept(lfd, nullptr, nullptr);
+void accept_loop(Server *sv) {
+    while (!sv->stop) {
+        const int fd = accept(sv->listen_fd, nullptr, nullptr);
         if (fd < 0) {
-            if (g_stop) return;
+            if (sv->stop) return;
             continue;
         }
-        std::thread(serve, fd).detach();
+        ++sv->active;
+        std::thread([sv, fd] {
+            serve(sv, fd);
+            --sv->active;
+        }).detach();
     }
 }
 
@@ -170,44 +196,87 @@ void accept_loop() {
 
 extern "C" {
 
+/* start a datanode on 127.0.0.1 (ephemeral port); the port identifies it afterwards */
 int hdfs3_loopback_start(int *port) {
-    if (g_listen_fd >= 0) return -EBUSY;
     int p = 0;
     const int fd = net::listen_tcp(0, &p);
     if (fd < 0) return fd;
-    g_stop = false;
-    g_listen_fd = fd;
-    g_accept = std::thread(accept_loop);
+    Server *sv = new Server();
+    sv->listen_fd = fd;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_servers[p] = sv;
+    }
+    sv->accept = std::thread(accept_loop, sv);
     if (port) *port = p;
     return 0;
 }
 
-int hdfs3_loopback_add_block(uint64_t block_id, const void *data, uint64_t len, const void *crc_be,
+/* serve block_id from (data, crc_be); the buffers are referenced, not copied */
+int hdfs3_loopback_add_block(int port, uint64_t block_id, const void *data, uint64_t len, const void *crc_be,
                              uint32_t bpc, int checksum_type) {
-    if (!bpc) return -EINVAL;
-    std::lock_guard<std::mutex> lk(g_mu);
-    g_blocks[block_id] = Block{static_cast<const uint8_t *>(data), len, static_cast<const uint8_t *>(crc_be), bpc,
-                               checksum_type};
+    Server *sv = find(port);
+    if (!sv || !bpc) return -EINVAL;
+    std::lock_guard<std::mutex> lk(sv->mu);
+    sv->blocks[block_id] = Block{static_cast<const uint8_t *>(data), len, static_cast<const uint8_t *>(crc_be), bpc,
+                                 checksum_type};
     return 0;
 }
 
-void hdfs3_loopback_clear_blocks(void) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    g_blocks.clear();
+int hdfs3_loopback_clear_blocks(int port) {
+    Server *sv = find(port);
+    if (!sv) return -EINVAL;
+    std::lock_guard<std::mutex> lk(sv->mu);
+    sv->blocks.clear();
+    return 0;
 }
 
-void hdfs3_loopback_set_packet_bytes(int n) { g_packet_bytes = n > 0 ? n : 64 * 1024; }
-uint64_t hdfs3_loopback_served_bytes(void) { return g_served.load(); }
-int hdfs3_loopback_last_status(void) { return g_last_status.load(); }
+int hdfs3_loopback_set_packet_bytes(int port, int n) {
+    Server *sv = find(port);
+    if (!sv) return -EINVAL;
+    sv->packet_bytes = n > 0 ? n : 64 * 1024;
+    return 0;
+}
 
-int hdfs3_loopback_stop(void) {
-    const int fd = g_listen_fd.exchange(-1);
-    g_stop = true;
-    if (fd >= 0) {
-        shutdown(fd, SHUT_RDWR);
-        net::close_fd(fd);
+/* drop every later connection after `bytes` data bytes (-1: never) */
+int hdfs3_loopback_set_fail_after(int port, int64_t bytes) {
+    Server *sv = find(port);
+    if (!sv) return -EINVAL;
+    sv->fail_after = bytes;
+    return 0;
+}
+
+uint64_t hdfs3_loopback_served_bytes(int port) {
+    Server *sv = find(port);
+    return sv ? sv->served.load() : 0;
+}
+
+uint64_t hdfs3_loopback_requests(int port) {
+    Server *sv = find(port);
+    return sv ? sv->requests.load() : 0;
+}
+
+int hdfs3_loopback_last_status(int port) {
+    Server *sv = find(port);
+    return sv ? sv->last_status.load() : -1;
+}
+
+int hdfs3_loopback_stop(int port) {
+    Server *sv = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_servers.find(port);
+        if (it == g_servers.end()) return -EINVAL;
+        sv = it->second;
+        g_servers.erase(it);
     }
-    if (g_accept.joinable()) g_accept.join();
+    sv->stop = true;
+    shutdown(sv->listen_fd, SHUT_RDWR);
+    net::close_fd(sv->listen_fd);
+    if (sv->accept.joinable()) sv->accept.join();
+    // connection threads reference the server; wait for them before freeing it
+    for (int i = 0; i < 6000 && sv->active.load() > 0; ++i) usleep(10000);
+    if (sv->active.load() == 0) delete sv;  // else leak rather than free under a live thread
     return 0;
 }
 
