@@ -110,6 +110,55 @@ int64_t hdfs3_input_length(hdfs3_input_stream *s);
 int hdfs3_input_stats(hdfs3_input_stream *s, uint64_t *failovers, uint64_t *readers_opened);
 int hdfs3_input_close(hdfs3_input_stream *s);
 
+/* ------------------------------------------------------------------------------------
+ * Output stream: the hdfsWrite / hdfsFlush / hdfsSync / hdfsTell / hdfsCloseFile surface
+ * (Hdfs.cpp:864-922) over OutputStreamImpl's append/flush/close (OutputStreamImpl.cpp:
+ * 298-441, 512-575). Every chunk's CRC32C is computed on the GPU in batches of packets
+ * (compute-on-write) and every packet handed to the sink is byte-identical to
+ * Packet::getBuffer (Packet.cpp:124-153): [31 B PacketHeader][chunks x BE32 CRC][data],
+ * same seqno/offsetInBlock/lastPacketInBlock sequence, the flushed partial chunk re-sent
+ * by the next packet, the empty last packet closing every block.
+ *
+ * The sink is where PipelineImpl::send (Pipeline.cpp:621-678) plugs in: packets arrive
+ * in seqno order, batch_packets at a time (and at every flush/sync/close, which return
+ * only after the sink received everything written so far). A non-zero sink return fails
+ * the stream (sticky, like OutputStreamImpl::setError).
+ * Error convention: hdfs.h's (-1 with errno) for write/flush/sync/tell/close.
+ * ---------------------------------------------------------------------------------- */
+typedef struct hdfs3_output_stream hdfs3_output_stream;
+
+typedef struct hdfs3_packet_info {
+    int64_t seqno;
+    int64_t offset_in_block;
+    int64_t block_index;         /* 0 for the first block of the stream                */
+    int32_t data_len;
+    int32_t num_chunks;
+    int32_t last_packet_in_block;
+} hdfs3_packet_info;
+
+/* returns 0, or -errno to fail the stream; `packet` is valid only during the call */
+typedef int (*hdfs3_packet_sink)(void *user, const void *packet, size_t len, const hdfs3_packet_info *info);
+
+typedef struct hdfs3_writer_opts {
+    int device;
+    uint32_t bytes_per_checksum;  /* dfs.bytes-per-checksum (512)                      */
+    int32_t packet_size;          /* dfs.client-write-packet-size (65536)               */
+    int64_t block_size;           /* dfs.default.blocksize; a multiple of the chunk size */
+    int batch_packets;            /* packets per GPU batch (64)                         */
+} hdfs3_writer_opts;
+
+/* 0 or -errno; -EINVAL for a packet size below the chunk size or a block size that is
+ * not a multiple of it (OutputStreamImpl.cpp:258-273) */
+int hdfs3_output_open(const hdfs3_writer_opts *opts, hdfs3_packet_sink sink, void *user,
+                      hdfs3_output_stream **out);
+int32_t hdfs3_output_write(hdfs3_output_stream *s, const void *buf, int32_t len);  /* hdfsWrite: len or -1 */
+int hdfs3_output_flush(hdfs3_output_stream *s);    /* hdfsFlush / hdfsHFlush: flushInternal(false) */
+int hdfs3_output_sync(hdfs3_output_stream *s);     /* hdfsSync: flushInternal(true)               */
+int64_t hdfs3_output_tell(hdfs3_output_stream *s);
+int hdfs3_output_stats(hdfs3_output_stream *s, uint64_t *packets, uint64_t *gpu_batches);
+/* hdfsCloseFile: the remaining packets and the block's last packet reach the sink; frees s */
+int hdfs3_output_close(hdfs3_output_stream *s);
+
 #ifdef __cplusplus
 }
 #endif

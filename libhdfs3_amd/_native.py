@@ -92,6 +92,24 @@ class LocatedBlock(ctypes.Structure):
                 ("n_replicas", c_int)]
 
 
+class PacketInfo(ctypes.Structure):
+    """hdfs3_packet_info (include/hdfs3_client.h)."""
+
+    _fields_ = [("seqno", c_int64), ("offset_in_block", c_int64), ("block_index", c_int64),
+                ("data_len", ctypes.c_int32), ("num_chunks", ctypes.c_int32),
+                ("last_packet_in_block", ctypes.c_int32)]
+
+
+PACKET_SINK = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t, POINTER(PacketInfo))
+
+
+class WriterOpts(ctypes.Structure):
+    """hdfs3_writer_opts (include/hdfs3_client.h)."""
+
+    _fields_ = [("device", c_int), ("bytes_per_checksum", c_uint32), ("packet_size", ctypes.c_int32),
+                ("block_size", c_int64), ("batch_packets", c_int)]
+
+
 # every symbol include/hdfs3_client.h declares
 CLIENT_API = {
     "hdfs3_block_reader_open": (c_int, [ctypes.c_char_p, c_int, POINTER(BlockId), c_int64, c_int64,
@@ -110,6 +128,13 @@ CLIENT_API = {
     "hdfs3_input_length": (c_int64, [c_void_p]),
     "hdfs3_input_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "hdfs3_input_close": (c_int, [c_void_p]),
+    "hdfs3_output_open": (c_int, [POINTER(WriterOpts), PACKET_SINK, c_void_p, POINTER(c_void_p)]),
+    "hdfs3_output_write": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),
+    "hdfs3_output_flush": (c_int, [c_void_p]),
+    "hdfs3_output_sync": (c_int, [c_void_p]),
+    "hdfs3_output_tell": (c_int64, [c_void_p]),
+    "hdfs3_output_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "hdfs3_output_close": (c_int, [c_void_p]),
 }
 
 # measurement hooks (bench.py only; not in the public header)
@@ -118,6 +143,7 @@ BENCH_API = {
     "hdfs3x_lane_read": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p]),
     "hdfs3x_grid_cap": (c_int, [c_void_p]),
     "hdfs3x_set_variant": (None, [c_int]),
+    "hdfs3x_block_reader_timing": (c_int, [c_void_p, POINTER(c_uint64)]),
 }
 
 

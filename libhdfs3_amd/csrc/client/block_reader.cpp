@@ -1,21 +1,31 @@
 // hdfs3_block_reader: RemoteBlockReader (src/client/RemoteBlockReader.cpp) with the
 // per-packet CPU verify replaced by batched GPU verification (include/hdfs3_client.h).
 //
-// Receive/verify pipeline: packets are read off the socket into one of two pinned
-// arenas (payload placed so each packet's data region is 16-byte aligned), the full
-// arena is copied to HBM and verified by the packet kernel asynchronously, and the next
-// arena is filled while the GPU works. Delivery to the caller only ever comes from a
-// batch whose verification has completed.
+// Pipeline (three stages on a ring of kSlots pinned arenas):
+//   receiver thread  socket -> arena (readNextPacket, up to batch_packets packets; each
+//                    packet's data region 16-byte aligned) -> async H2D + packet kernel +
+//                    result D2H + event on the ctx stream -> `ready` queue
+//   GPU              verifies batch i while the receiver fills batch i+1
+//   caller (read)    waits for the front batch's event, copies its verified bytes out,
+//                    returns the arena to the receiver
+// so socket receive, verification and delivery overlap; the reference does all three in
+// sequence on the caller's thread (RemoteBlockReader::read, :332-357). Delivery only ever
+// comes from a batch whose verification completed.
 #include "hdfs3_client.h"
 
 #include <hip/hip_runtime.h>
+#include <sys/socket.h>
 
 #include <algorithm>
 #include <cerrno>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../ctx.h"
@@ -31,6 +41,9 @@ namespace {
 constexpr int kDefaultBatchPackets = 64;
 constexpr int kDefaultTimeoutMs = 60000;  // input.read.timeout default (SessionConfig.cpp)
 constexpr size_t kMaxResponse = 10u << 20;  // RemoteBlockReader.cpp:116
+constexpr int kSlots = 3;                  // receiving / verifying / delivering
+constexpr size_t kArenaCacheMax = 6;       // arenas a ctx keeps for its next reader
+constexpr size_t kPacketGuess = 64 * 1024 + 16 * 1024;  // 64 KiB payload + CRCs + alignment
 
 struct PacketRef {
     uint64_t data_off, crc_off;  // inside the arena
@@ -40,34 +53,32 @@ struct PacketRef {
 };
 
 struct Batch {
-    uint8_t *h = nullptr, *d = nullptr;  // pinned / device arena
-    size_t cap = 0, used = 0;
-    DevPacket *h_desc = nullptr, *d_desc = nullptr;
-    size_t desc_cap = 0;
-    unsigned long long *d_res = nullptr, *h_res = nullptr;
-    hipEvent_t done = nullptr;
+    PacketArena a;
+    size_t used = 0;
     std::vector<PacketRef> pk;
-    bool launched = false, verified = false;
+    bool verified = false;
     int64_t bad_pkt = -1;
     size_t dpkt = 0, doff = 0;  // delivery cursor
 
     void reset() {
         used = 0;
         pk.clear();
-        launched = verified = false;
+        verified = false;
         bad_pkt = -1;
         dpkt = doff = 0;
     }
-    void release() {
-        if (h) (void)hipHostFree(h);
-        if (d) (void)hipFree(d);
-        if (h_desc) (void)hipHostFree(h_desc);
-        if (d_desc) (void)hipFree(d_desc);
-        if (h_res) (void)hipHostFree(h_res);
-        if (d_res) (void)hipFree(d_res);
-        if (done) (void)hipEventDestroy(done);
-        *this = Batch();
-    }
+};
+
+uint64_t now_ns() {
+    return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
+struct Timer {  // adds the scope's duration to a counter
+    std::atomic<uint64_t> &acc;
+    uint64_t t0 = now_ns();
+    explicit Timer(std::atomic<uint64_t> &a) : acc(a) {}
+    ~Timer() { acc.fetch_add(now_ns() - t0, std::memory_order_relaxed); }
 };
 
 int hip_err(hipError_t e, const char *what) {
@@ -80,29 +91,29 @@ int hip_err(hipError_t e, const char *what) {
         if (e_ != hipSuccess) return hip_err(e_, #expr);  \
     } while (0)
 
-int grow(Batch &b, size_t cap, size_t descs) {
-    if (cap > b.cap) {
-        if (b.h) (void)hipHostFree(b.h);
-        if (b.d) (void)hipFree(b.d);
-        b.h = b.d = nullptr;
-        b.cap = 0;
-        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.h), cap, hipHostMallocDefault));
-        HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.d), cap));
-        b.cap = cap;
+int grow(PacketArena &a, size_t cap, size_t descs) {
+    if (cap > a.cap) {
+        if (a.h) (void)hipHostFree(a.h);
+        if (a.d) (void)hipFree(a.d);
+        a.h = a.d = nullptr;
+        a.cap = 0;
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h), cap, hipHostMallocDefault));
+        HIP_OK(hipMalloc(reinterpret_cast<void **>(&a.d), cap));
+        a.cap = cap;
     }
-    if (descs > b.desc_cap) {
-        if (b.h_desc) (void)hipHostFree(b.h_desc);
-        if (b.d_desc) (void)hipFree(b.d_desc);
-        b.h_desc = b.d_desc = nullptr;
-        b.desc_cap = 0;
-        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.h_desc), descs * sizeof(DevPacket), hipHostMallocDefault));
-        HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.d_desc), descs * sizeof(DevPacket)));
-        b.desc_cap = descs;
+    if (descs > a.desc_cap) {
+        if (a.h_desc) (void)hipHostFree(a.h_desc);
+        if (a.d_desc) (void)hipFree(a.d_desc);
+        a.h_desc = a.d_desc = nullptr;
+        a.desc_cap = 0;
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h_desc), descs * sizeof(DevPacket), hipHostMallocDefault));
+        HIP_OK(hipMalloc(reinterpret_cast<void **>(&a.d_desc), descs * sizeof(DevPacket)));
+        a.desc_cap = descs;
     }
-    if (!b.d_res) {
-        HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.d_res), sizeof(unsigned long long)));
-        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.h_res), sizeof(unsigned long long), hipHostMallocDefault));
-        HIP_OK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+    if (!a.d_res) {
+        HIP_OK(hipMalloc(reinterpret_cast<void **>(&a.d_res), sizeof(unsigned long long)));
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long), hipHostMallocDefault));
+        HIP_OK(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
     }
     return 0;
 }
@@ -118,21 +129,36 @@ struct hdfs3_block_reader {
     bool own_ctx = true;       // false when borrowed from an input stream
     wire::ExtendedBlock block;
     int64_t start = 0, end_offset = 0;
-    int64_t recv_cursor = 0;   // "cursor" as seen by readNextPacket for the next packet
-    int64_t delivered = 0;     // bytes handed to the caller
-    int64_t last_seqno = -1;
     uint32_t chunk_size = 0;
     uint32_t checksum_size = 0;
+
+    // receiver-thread state (touched only by the receiver once it runs)
+    int64_t recv_cursor = 0;   // "cursor" as seen by readNextPacket for the next packet
+    int64_t last_seqno = -1;
     bool range_done = false;   // every packet of the range (and the trailer) received
+    bool have_pending_hdr = false;
+    wire::PacketHeader pending_hdr;
+
+    // shared between receiver and caller, under mu
+    std::mutex mu;
+    std::condition_variable cv;
+    Batch slot[kSlots];
+    std::deque<int> ready;     // launched batches in order, front = delivering
+    std::deque<int> free_slots;
+    bool recv_done = false;    // the receiver has finished (range complete or failed)
+    int recv_error = 0;
+    std::string recv_msg;
+    bool stop = false;
+    std::thread rx;
+
+    // caller state
+    int64_t delivered = 0;
     bool sent_status = false;
     int error = 0;             // sticky failure (-errno)
     std::string error_msg;
-    bool have_pending_hdr = false;
-    wire::PacketHeader pending_hdr;
-    Batch slot[2];
-    std::deque<int> queue;     // launched batches in order, front = delivering
-    int next_slot = 0;
-    uint64_t packets = 0, batches = 0;
+
+    std::atomic<uint64_t> packets{0}, batches{0};
+    std::atomic<uint64_t> t_ns[5] = {};  // receive, alloc, launch, wait, deliver (hdfs3x_block_reader_timing)
 
     int sticky(int code, const std::string &msg) {
         error = code;
@@ -140,7 +166,7 @@ struct hdfs3_block_reader {
         return fail(code, "%s", msg.c_str());
     }
 
-    // RemoteBlockReader::checkResponse (:112-203)
+    // RemoteBlockReader::checkResponse (:112-203); runs on the opening thread
     int check_response() {
         std::string resp;
         if (int rc = net::read_delimited(fd, resp, kMaxResponse, timeout_ms))
@@ -168,6 +194,13 @@ struct hdfs3_block_reader {
         return 0;
     }
 
+    // ---- receiver thread --------------------------------------------------------------
+    // Receiver-side failures carry their message back through recv_msg (fail() is thread-local).
+    int rx_fail(int code, const std::string &msg) {
+        recv_msg = msg;
+        return code;
+    }
+
     int read_header(wire::PacketHeader &h) {
         if (have_pending_hdr) {
             h = pending_hdr;
@@ -176,19 +209,19 @@ struct hdfs3_block_reader {
         }
         uint8_t buf[wire::kPacketHeaderSize];
         if (int rc = net::read_fully(fd, buf, sizeof(buf), timeout_ms))
-            return sticky(rc, "RemoteBlockReader: failed to read block header");
-        if (!h.decode(buf, sizeof(buf))) return sticky(-EPROTO, "Invalid PacketHeader");
+            return rx_fail(rc, "RemoteBlockReader: failed to read block header");
+        if (!h.decode(buf, sizeof(buf))) return rx_fail(-EPROTO, "Invalid PacketHeader");
         return 0;
     }
 
     // readNextPacket (:226-277) for up to batch_packets packets into `b`
     int receive(Batch &b) {
+        Timer tm(t_ns[0]);
         b.reset();
         while (int(b.pk.size()) < batch_packets && !range_done) {
             wire::PacketHeader h;
             if (int rc = read_header(h)) return rc;
-            if (!h.sanity_check(last_seqno))
-                return sticky(-EIO, "RemoteBlockReader: Packet failed on sanity check");
+            if (!h.sanity_check(last_seqno)) return rx_fail(-EIO, "RemoteBlockReader: Packet failed on sanity check");
             if (h.data_len <= 0) {  // the empty last packet ends the block
                 last_seqno = h.seqno;
                 range_done = true;
@@ -197,22 +230,22 @@ struct hdfs3_block_reader {
             const uint64_t chunks = (uint64_t(h.data_len) + chunk_size - 1) / chunk_size;
             const uint64_t crc_len = chunks * checksum_size;
             if (int64_t(h.packet_len) != 4 + int64_t(h.data_len) + int64_t(crc_len))
-                return sticky(-EIO, "Invalid Packet, packetLen does not match dataLen and checksums");
+                return rx_fail(-EIO, "Invalid Packet, packetLen does not match dataLen and checksums");
             const uint64_t size = crc_len + uint64_t(h.data_len);
             uint64_t off = ((b.used + crc_len + 15) & ~uint64_t(15)) - crc_len;
-            if (off + size > b.cap) {
+            if (off + size > b.a.cap) {
                 if (!b.pk.empty()) {  // close this batch; the header opens the next
                     pending_hdr = h;
                     have_pending_hdr = true;
                     break;
                 }
-                if (int rc = grow(b, size + 64, size_t(batch_packets))) return sticky(rc, "arena growth failed");
+                if (int rc = grow(b.a, size + 64, size_t(batch_packets))) return rx_fail(rc, "arena growth failed");
                 off = ((crc_len + 15) & ~uint64_t(15)) - crc_len;
             }
-            if (int rc = net::read_fully(fd, b.h + off, size, timeout_ms))
-                return sticky(rc, "RemoteBlockReader: failed to read packet payload");
+            if (int rc = net::read_fully(fd, b.a.h + off, size, timeout_ms))
+                return rx_fail(rc, "RemoteBlockReader: failed to read packet payload");
             last_seqno = h.seqno;
-            ++packets;
+            packets.fetch_add(1, std::memory_order_relaxed);
             int64_t ahead = recv_cursor - h.offset_in_block;
             ahead = ahead > 0 ? ahead : 0;
             const int64_t useful = std::max<int64_t>(0, std::min<int64_t>(h.data_len - ahead, end_offset - recv_cursor));
@@ -232,52 +265,96 @@ struct hdfs3_block_reader {
     }
 
     int launch(Batch &b) {
-        b.launched = true;
-        ++batches;
-        if (!verify || b.pk.empty()) {
+        Timer tm(t_ns[2]);
+        batches.fetch_add(1, std::memory_order_relaxed);
+        if (!verify) {
             b.verified = true;
             return 0;
         }
         for (size_t i = 0; i < b.pk.size(); ++i)
-            b.h_desc[i] = DevPacket{b.pk[i].data_off, b.pk[i].crc_off, b.pk[i].data_len, 0};
-        HIP_OK(hipMemcpyAsync(b.d, b.h, b.used, hipMemcpyHostToDevice, ctx->stream));
-        HIP_OK(hipMemcpyAsync(b.d_desc, b.h_desc, b.pk.size() * sizeof(DevPacket), hipMemcpyHostToDevice,
+            b.a.h_desc[i] = DevPacket{b.pk[i].data_off, b.pk[i].crc_off, b.pk[i].data_len, 0};
+        HIP_OK(hipMemcpyAsync(b.a.d, b.a.h, b.used, hipMemcpyHostToDevice, ctx->stream));
+        HIP_OK(hipMemcpyAsync(b.a.d_desc, b.a.h_desc, b.pk.size() * sizeof(DevPacket), hipMemcpyHostToDevice,
                               ctx->stream));
-        HIP_OK(hipMemsetAsync(b.d_res, 0, sizeof(unsigned long long), ctx->stream));
-        HIP_OK(launch_packets(b.d, b.d_desc, b.pk.size(), chunk_size, true, /*check_short_tail=*/0, b.d_res,
+        HIP_OK(hipMemsetAsync(b.a.d_res, 0, sizeof(unsigned long long), ctx->stream));
+        HIP_OK(launch_packets(b.a.d, b.a.d_desc, b.pk.size(), chunk_size, true, /*check_short_tail=*/0, b.a.d_res,
                               ctx->d_tables, ctx->grid_cap, ctx->stream));
         ++ctx->launches;
-        HIP_OK(hipMemcpyAsync(b.h_res, b.d_res, sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
-        HIP_OK(hipEventRecord(b.done, ctx->stream));
+        HIP_OK(hipMemcpyAsync(b.a.h_res, b.a.d_res, sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_OK(hipEventRecord(b.a.done, ctx->stream));
         return 0;
     }
 
+    // an arena for `b`: already owned, else one the ctx cached from an earlier reader, else new
+    int acquire(Batch &b) {
+        Timer tm(t_ns[1]);
+        if (!b.a.h) {
+            std::lock_guard<std::mutex> lk(ctx->arena_mu);
+            if (!ctx->arena_cache.empty()) {
+                b.a = ctx->arena_cache.back();
+                ctx->arena_cache.pop_back();
+            }
+        }
+        if (int rc = grow(b.a, std::max(b.a.cap, size_t(batch_packets) * kPacketGuess), size_t(batch_packets)))
+            return rx_fail(rc, "arena allocation failed");
+        return 0;
+    }
+
+    void receiver() {
+        (void)hipSetDevice(ctx->device);
+        for (;;) {
+            int s;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || !free_slots.empty(); });
+                if (stop) break;
+                s = free_slots.front();
+                free_slots.pop_front();
+            }
+            Batch &b = slot[s];
+            int rc = acquire(b);
+            if (!rc) rc = receive(b);
+            if (!rc && !b.pk.empty()) {
+                rc = launch(b);
+                if (rc) recv_msg = hdfs3_crc_last_error();
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!rc && !b.pk.empty())
+                    ready.push_back(s);
+                else
+                    free_slots.push_back(s);
+                if (rc) recv_error = rc;
+                if (rc || range_done) recv_done = true;
+            }
+            cv.notify_all();
+            if (rc || range_done) break;
+        }
+    }
+
+    void start_receiver() {
+        for (int i = 0; i < kSlots; ++i) free_slots.push_back(i);
+        rx = std::thread([this] { receiver(); });
+    }
+
+    // ---- caller side ----------------------------------------------------------------------
     int wait(Batch &b) {
         if (b.verified) return 0;
-        HIP_OK(hipEventSynchronize(b.done));
-        const unsigned long long r = *b.h_res;
+        Timer tm(t_ns[3]);
+        HIP_OK(hipEventSynchronize(b.a.done));
+        const unsigned long long r = *b.a.h_res;
         if (r) b.bad_pkt = int64_t((~r) >> 32);
         b.verified = true;
         return 0;
     }
 
-    // fill + launch one more batch if the range still has packets
-    int pump() {
-        if (range_done || queue.size() >= 2) return 0;
-        Batch &b = slot[next_slot];
-        if (int rc = grow(b, std::max<size_t>(b.cap, size_t(batch_packets) * (65536 + 16 * 1024)), size_t(batch_packets)))
-            return sticky(rc, "arena allocation failed");
-        if (int rc = receive(b)) return rc;
-        if (b.pk.empty() && range_done) return 0;
-        if (int rc = launch(b)) return sticky(rc, hdfs3_crc_last_error());
-        queue.push_back(next_slot);
-        next_slot ^= 1;
-        return 0;
-    }
-
-    // sendStatus (:289-304), once every packet of the range verified
+    // sendStatus (:289-304), once every packet of the range verified and was handed out
     void maybe_send_status() {
-        if (sent_status || !range_done || !queue.empty() || error) return;
+        if (sent_status || error) return;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!recv_done || recv_error || !ready.empty()) return;
+        }
         const std::string msg = wire::encode_client_read_status(verify ? wire::kChecksumOk : wire::kSuccess);
         if (net::write_delimited(fd, msg, timeout_ms) == 0) sent_status = true;
     }
@@ -287,45 +364,68 @@ struct hdfs3_block_reader {
         if (len <= 0 || !out) return fail(-EINVAL, "invalid read buffer");
         int32_t total = 0;
         while (total < len) {
-            if (queue.empty()) {
-                if (int rc = pump()) return total ? total : rc;
-                if (queue.empty()) break;  // range exhausted
+            int s;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !ready.empty() || recv_done; });
+                if (ready.empty()) {
+                    if (recv_error) {  // good batches were all delivered first
+                        const int code = recv_error;
+                        const std::string msg = recv_msg;
+                        lk.unlock();
+                        if (total) {
+                            error = code;
+                            error_msg = msg;
+                            return total;
+                        }
+                        return sticky(code, msg);
+                    }
+                    break;  // range exhausted
+                }
+                s = ready.front();
             }
-            // keep the next batch receiving while this one verifies on the GPU
-            if (int rc = pump()) return total ? total : rc;
-            Batch &b = slot[queue.front()];
+            Batch &b = slot[s];
             if (int rc = wait(b)) return total ? total : sticky(rc, hdfs3_crc_last_error());
             const size_t limit = b.bad_pkt >= 0 ? size_t(b.bad_pkt) : b.pk.size();
-            while (total < len && b.dpkt < limit) {
-                const PacketRef &p = b.pk[b.dpkt];
-                const size_t avail = p.deliver - b.doff;
-                const size_t n = std::min<size_t>(avail, size_t(len - total));
-                std::memcpy(out + total, b.h + p.data_off + p.skip + b.doff, n);
-                total += int32_t(n);
-                b.doff += n;
-                delivered += int64_t(n);
-                if (b.doff == p.deliver) {
-                    ++b.dpkt;
-                    b.doff = 0;
+            {
+                Timer tm(t_ns[4]);
+                while (total < len && b.dpkt < limit) {
+                    const PacketRef &p = b.pk[b.dpkt];
+                    const size_t avail = p.deliver - b.doff;
+                    const size_t n = std::min<size_t>(avail, size_t(len - total));
+                    std::memcpy(out + total, b.a.h + p.data_off + p.skip + b.doff, n);
+                    total += int32_t(n);
+                    b.doff += n;
+                    delivered += int64_t(n);
+                    if (b.doff == p.deliver) {
+                        ++b.dpkt;
+                        b.doff = 0;
+                    }
                 }
             }
             if (b.dpkt == limit) {
                 if (b.bad_pkt >= 0) {
                     sticky(-EIO, "ChecksumException: RemoteBlockReader: checksum not match for Block: " +
-                                     std::to_string(block.block_id) + " (packet " +
-                                     std::to_string(b.bad_pkt) + " of a GPU batch)");
+                                     std::to_string(block.block_id) + " (packet " + std::to_string(b.bad_pkt) +
+                                     " of a GPU batch)");
                     return total ? total : error;
                 }
-                queue.pop_front();
-                maybe_send_status();
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    ready.pop_front();
+                    free_slots.push_back(s);
+                }
+                cv.notify_all();
             }
         }
+        maybe_send_status();
         return total;
     }
 
-    int64_t available() const {
+    int64_t available() {
+        std::lock_guard<std::mutex> lk(mu);
         int64_t a = 0;
-        for (int s : queue) {
+        for (int s : ready) {
             const Batch &b = slot[s];
             if (!b.verified) continue;
             const size_t limit = b.bad_pkt >= 0 ? size_t(b.bad_pkt) : b.pk.size();
@@ -335,8 +435,29 @@ struct hdfs3_block_reader {
     }
 
     ~hdfs3_block_reader() {
+        if (rx.joinable()) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                stop = true;
+            }
+            cv.notify_all();
+            if (fd >= 0) shutdown(fd, SHUT_RDWR);  // unblocks a receiver waiting on the socket
+            rx.join();
+        }
         if (ctx) (void)hipStreamSynchronize(ctx->stream);
-        for (Batch &b : slot) b.release();
+        for (Batch &b : slot) {
+            if (!b.a.h) continue;
+            bool cached = false;
+            if (ctx && !own_ctx) {
+                std::lock_guard<std::mutex> lk(ctx->arena_mu);
+                if (ctx->arena_cache.size() < kArenaCacheMax) {
+                    ctx->arena_cache.push_back(b.a);
+                    cached = true;
+                }
+            }
+            if (!cached) b.a.release();
+            b.a = PacketArena();
+        }
         if (ctx && own_ctx) hdfs3_crc_ctx_destroy(ctx);
         net::close_fd(fd);
     }
@@ -388,6 +509,7 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
         delete r;
         return rc;
     }
+    r->start_receiver();  // read-ahead starts now, as RemoteBlockReader's first read would
     *out = r;
     return 0;
 }
@@ -412,8 +534,15 @@ int64_t hdfs3_block_reader_available(hdfs3_block_reader *r) { return r ? r->avai
 int hdfs3_block_reader_stats(hdfs3_block_reader *r, uint32_t *bpc, uint64_t *packets, uint64_t *gpu_batches) {
     if (!r) return fail(-EINVAL, "null reader");
     if (bpc) *bpc = r->chunk_size;
-    if (packets) *packets = r->packets;
-    if (gpu_batches) *gpu_batches = r->batches;
+    if (packets) *packets = r->packets.load();
+    if (gpu_batches) *gpu_batches = r->batches.load();
+    return 0;
+}
+
+// measurement hook (not in the public header): nanoseconds spent per phase so far
+int hdfs3x_block_reader_timing(hdfs3_block_reader *r, uint64_t *out5) {
+    if (!r || !out5) return fail(-EINVAL, "invalid argument");
+    for (int i = 0; i < 5; ++i) out5[i] = r->t_ns[i].load();
     return 0;
 }
 

@@ -4,8 +4,11 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
+#include <mutex>
+#include <vector>
 
 #include "crc32c_kernels.h"
 
@@ -27,6 +30,29 @@ struct Slot {
     size_t pending_bytes = 0;
 };
 
+// One packet batch's buffers for the block reader: pinned wire arena + its HBM mirror,
+// packet descriptors, the verify result word and the completion event. Cached in the ctx
+// so the block readers an input stream opens one after another reuse them.
+struct PacketArena {
+    uint8_t *h = nullptr, *d = nullptr;
+    size_t cap = 0;
+    DevPacket *h_desc = nullptr, *d_desc = nullptr;
+    size_t desc_cap = 0;
+    unsigned long long *d_res = nullptr, *h_res = nullptr;
+    hipEvent_t done = nullptr;
+
+    void release() {
+        if (h) (void)hipHostFree(h);
+        if (d) (void)hipFree(d);
+        if (h_desc) (void)hipHostFree(h_desc);
+        if (d_desc) (void)hipFree(d_desc);
+        if (h_res) (void)hipHostFree(h_res);
+        if (d_res) (void)hipFree(d_res);
+        if (done) (void)hipEventDestroy(done);
+        *this = PacketArena();
+    }
+};
+
 }  // namespace hdfs3crc
 
 struct hdfs3_crc_ctx {
@@ -42,6 +68,8 @@ struct hdfs3_crc_ctx {
     hdfs3crc::DevPacket *h_pk = nullptr;               // pinned
     size_t pk_cap = 0;
     hdfs3crc::Slot slot[2];
-    uint64_t launches = 0;
+    std::atomic<uint64_t> launches{0};
+    std::mutex arena_mu;                          // guards arena_cache
+    std::vector<hdfs3crc::PacketArena> arena_cache;
 };
 

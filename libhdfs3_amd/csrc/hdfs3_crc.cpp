@@ -306,6 +306,8 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx) {
         if (s.d_crc) (void)hipFree(s.d_crc);
         if (s.done) (void)hipEventDestroy(s.done);
     }
+    for (PacketArena &a : ctx->arena_cache) a.release();
+    ctx->arena_cache.clear();
     if (ctx->d_pk) (void)hipFree(ctx->d_pk);
     if (ctx->h_pk) (void)hipHostFree(ctx->h_pk);
     if (ctx->d_tables) (void)hipFree(ctx->d_tables);
@@ -333,7 +335,7 @@ int hdfs3_crc_ctx_synchronize(hdfs3_crc_ctx *ctx) {
     return 0;
 }
 
-uint64_t hdfs3_crc_ctx_kernel_launches(hdfs3_crc_ctx *ctx) { return ctx ? ctx->launches : 0; }
+uint64_t hdfs3_crc_ctx_kernel_launches(hdfs3_crc_ctx *ctx) { return ctx ? ctx->launches.load() : 0; }
 
 int64_t hdfs3_crc_decode_result(uint64_t r) { return r ? int64_t(~r) : -1; }
 

@@ -333,3 +333,74 @@ class InputStream:
             self.close()
         except Exception:
             pass
+
+
+class OutputStream:
+    """hdfs3_output_stream (include/hdfs3_client.h): hdfsWrite/hdfsFlush/hdfsSync/hdfsCloseFile
+    with GPU compute-on-write. `sink(packet: bytes, info: dict) -> int` receives every wire
+    packet in seqno order (PipelineImpl::send); by default packets are collected in .packets."""
+
+    def __init__(self, *, device: int = 0, bytes_per_checksum: int = 512, packet_size: int = 65536,
+                 block_size: int = 64 << 20, batch_packets: int = 64, sink=None):
+        self._lib = _native.lib()
+        self.packets: list[tuple[bytes, dict]] = []
+        user_sink = sink
+
+        def _sink(_user, pkt, n, info):
+            i = info.contents
+            d = {"seqno": i.seqno, "offset_in_block": i.offset_in_block, "block_index": i.block_index,
+                 "data_len": i.data_len, "num_chunks": i.num_chunks, "last": bool(i.last_packet_in_block)}
+            b = ctypes.string_at(pkt, n)
+            if user_sink is not None:
+                return int(user_sink(b, d))
+            self.packets.append((b, d))
+            return 0
+
+        self._cb = _native.PACKET_SINK(_sink)  # kept alive for the stream's lifetime
+        opts = _native.WriterOpts(device, bytes_per_checksum, packet_size, block_size, batch_packets)
+        p = c_void_p()
+        check("hdfs3_output_open", self._lib.hdfs3_output_open(byref(opts), self._cb, None, byref(p)))
+        self.s = p.value
+
+    def _posix(self, fn: str, rc: int) -> int:
+        if rc < 0:
+            raise HdfsIOError(ctypes.get_errno(), f"{fn}: {self._lib.hdfs3_crc_last_error().decode(errors='replace')}")
+        return rc
+
+    def write(self, data) -> int:
+        buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
+        return self._posix("hdfsWrite", self._lib.hdfs3_output_write(self.s, buf.ctypes.data, buf.nbytes))
+
+    def flush(self) -> None:
+        self._posix("hdfsFlush", self._lib.hdfs3_output_flush(self.s))
+
+    def sync(self) -> None:
+        self._posix("hdfsSync", self._lib.hdfs3_output_sync(self.s))
+
+    def tell(self) -> int:
+        return self._posix("hdfsTell", self._lib.hdfs3_output_tell(self.s))
+
+    def stats(self):
+        from ctypes import c_uint64
+        pk, b = c_uint64(), c_uint64()
+        check("hdfs3_output_stats", self._lib.hdfs3_output_stats(self.s, byref(pk), byref(b)))
+        return {"packets": pk.value, "gpu_batches": b.value}
+
+    def close(self) -> None:
+        if self.s:
+            s, self.s = self.s, None
+            self._posix("hdfsCloseFile", self._lib.hdfs3_output_close(s))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        if self.s:
+            self.close()
+
+    def __del__(self):
+        try:
+            if self.s:
+                self._lib.hdfs3_output_close(self.s)
+        except Exception:
+            pass

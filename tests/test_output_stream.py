@@ -1,0 +1,154 @@
+"""GPU tests of the write-path drop-in (hdfs3_output_stream): every packet handed to the
+sink must be byte-identical to what the reference's OutputStreamImpl + Packet produce for
+the same hdfsWrite/hdfsFlush/hdfsSync/hdfsCloseFile sequence (tests/writer_model.py, CRC
+words from the oracle) — headers, seqnos, offsets, BE32 CRC words of every chunk including
+short tails, the re-sent partial chunk after a flush and the empty last packet per block."""
+import errno
+import random
+
+import numpy as np
+import pytest
+
+from util import oracle_crc, splitmix_bytes
+from writer_model import OutputStreamModel
+
+pytestmark = pytest.mark.gpu
+
+
+def crc(b: bytes) -> int:
+    return oracle_crc(np.frombuffer(b, np.uint8)) if b else 0
+
+
+def run_both(ops, data, **cfg):
+    from libhdfs3_amd.engine import OutputStream
+
+    model = OutputStreamModel(crc, bpc=cfg.get("bytes_per_checksum", 512), packet_size=cfg.get("packet_size", 65536),
+                              block_size=cfg.get("block_size", 64 << 20))
+    gpu = OutputStream(**cfg)
+    pos = 0
+    for op, n in ops:
+        if op == "w":
+            chunk = data[pos:pos + n]
+            pos += n
+            model.write(chunk.tobytes())
+            assert gpu.write(chunk) == n
+            assert gpu.tell() == model.cursor
+        elif op == "f":
+            model.flush()
+            gpu.flush()
+            assert [p for p, _ in gpu.packets] == [p for p, _ in model.sent]  # flush drains everything
+        elif op == "s":
+            model.sync()
+            gpu.sync()
+    model.close()
+    gpu.close()
+    return model.sent, gpu.packets
+
+
+def random_ops(rng, total, flush_p=0.1):
+    ops, left = [], total
+    while left > 0:
+        r = rng.random()
+        if r < flush_p:
+            ops.append(("f", 0))
+        elif r < flush_p * 1.3:
+            ops.append(("s", 0))
+        else:
+            n = min(left, rng.choice([1, 3, 100, 511, 512, 513, 4096, 65536, 70000, 1 << 20, rng.randint(1, 300000)]))
+            ops.append(("w", n))
+            left -= n
+    return ops
+
+
+@pytest.mark.parametrize("bpc,packet_size,block_size,batch", [
+    (512, 65536, 64 << 20, 64),      # reference defaults
+    (512, 65536, 1 << 20, 3),        # block boundaries every 16 packets, small batches
+    (4096, 65536, 2 << 20, 64),
+    (2048, 4096, 256 << 10, 1),      # one chunk-ish per packet, one packet per GPU batch
+    (100, 1000, 100 * 37, 5),        # odd chunk size, ragged everything
+])
+def test_packets_identical_to_reference_model(bpc, packet_size, block_size, batch):
+    rng = random.Random(bpc * 7 + batch)
+    data = splitmix_bytes(5 << 20, bpc + batch)
+    ops = random_ops(rng, data.nbytes)
+    want, got = run_both(ops, data, bytes_per_checksum=bpc, packet_size=packet_size, block_size=block_size,
+                         batch_packets=batch)
+    assert len(got) == len(want)
+    for i, ((gp, gi), (wp, wi)) in enumerate(zip(got, want)):
+        assert gi == wi, (i, gi, wi)
+        assert gp == wp, i
+
+
+@pytest.mark.parametrize("ops", [
+    [("w", 700), ("f", 0), ("w", 1300)],
+    [("w", 700), ("f", 0), ("f", 0), ("s", 0)],
+    [("w", 512 * 127)],
+    [("w", 512 * 127 + 1), ("f", 0)],
+    [("s", 0), ("w", 5)],
+    [("w", 10), ("s", 0), ("s", 0)],
+    [],
+])
+def test_flush_sync_close_edge_cases(ops):
+    data = splitmix_bytes(1 << 20, 3)
+    want, got = run_both(ops, data, block_size=512 * 254, batch_packets=2)
+    assert got == want
+
+
+def test_roundtrip_through_verify_and_block_boundaries():
+    """Packets split at block ends, the data reassembles, every packet verifies on the GPU."""
+    from libhdfs3_amd.engine import CrcContext, OutputStream
+
+    bsz = 1 << 20
+    data = splitmix_bytes(3 * bsz + 12345, 4)
+    with OutputStream(block_size=bsz) as s:
+        for off in range(0, data.nbytes, 1 << 20):
+            s.write(data[off:off + (1 << 20)])
+    pk = s.packets
+    blocks = {}
+    ctx = CrcContext(0)
+    for p, info in pk:
+        n = info["num_chunks"]
+        body = np.frombuffer(p, np.uint8)
+        crcs, d = body[31:31 + 4 * n], body[31 + 4 * n:]
+        assert ctx.verify(d, 512, crcs, check_short_tail=True) == -1
+        blocks.setdefault(info["block_index"], bytearray())
+        if info["data_len"]:
+            assert info["offset_in_block"] == len(blocks[info["block_index"]])
+            blocks[info["block_index"]] += d.tobytes()
+    assert sorted(blocks) == [0, 1, 2, 3]
+    assert b"".join(bytes(blocks[i]) for i in range(4)) == data.tobytes()
+    lasts = [info for _, info in pk if info["last"]]
+    assert [i["block_index"] for i in lasts] == [0, 1, 2, 3]
+    ctx.close()
+
+
+def test_sink_failure_fails_the_stream():
+    from libhdfs3_amd.engine import HdfsIOError, OutputStream
+
+    calls = []
+
+    def sink(pkt, info):
+        calls.append(info["seqno"])
+        return -errno.ENOSPC if info["seqno"] == 2 else 0
+
+    s = OutputStream(sink=sink, batch_packets=1)
+    data = splitmix_bytes(1 << 20, 5)
+    with pytest.raises(HdfsIOError) as ei:
+        for off in range(0, data.nbytes, 65536):
+            s.write(data[off:off + 65536])
+    assert ei.value.errno == errno.ENOSPC
+    with pytest.raises(HdfsIOError):
+        s.write(data[:10])
+    assert calls[:3] == [0, 1, 2]
+    with pytest.raises(HdfsIOError):
+        s.close()
+
+
+def test_invalid_configuration_rejected():
+    from libhdfs3_amd.engine import OutputStream
+    from libhdfs3_amd._native import Hdfs3CrcError
+
+    with pytest.raises(Hdfs3CrcError):
+        OutputStream(block_size=1000)  # not a multiple of 512
+    with pytest.raises(Hdfs3CrcError):
+        OutputStream(packet_size=100)  # below the chunk size

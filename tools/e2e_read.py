@@ -1,10 +1,11 @@
 """Config 5 (BASELINE.json): end-to-end, PCIe-inclusive rates of the read path.
 
   host_verify   hdfs3_crc32c_verify on a 1 GiB host buffer (pinned ring -> H2D -> verify)
-  loopback      1 GiB file = 8 x 128 MiB blocks served by the loopback datanode over TCP
-                127.0.0.1, read through hdfs3_block_reader (socket -> pinned arena -> H2D ->
-                packet-kernel verify -> caller buffer), verify on vs off, 1 reader reading the
-                blocks in turn (InputStreamImpl order) and 8 concurrent readers (one per block)
+  hdfsRead      1 GiB file = 8 x 128 MiB blocks served by the loopback datanode over TCP
+                127.0.0.1, read through hdfs3_input_read (InputStreamImpl block walk ->
+                hdfs3_block_reader: socket -> pinned arena -> H2D -> packet-kernel verify ->
+                caller buffer), verify on vs off
+  parallel      8 concurrent streams, one hdfsPread of one whole block each
 
 The datanode thread and the reader share the host's cores, so the loopback numbers bound
 the client from below; the verify-off line is the same transport without the GPU work.
@@ -23,6 +24,7 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))  # loopback helper
 
 GIB = 1 << 30
 
@@ -37,21 +39,47 @@ def host_verify(ctx, data, crc, bpc, reps):
     return data.nbytes / dt / GIB
 
 
-def read_block(port, bid, nbytes, out, verify, batch, errors):
-    from libhdfs3_amd.engine import BlockReader
+def pread_block(blocks, port, i, bsz, out, verify, batch, errors):
+    from libhdfs3_amd.engine import InputStream
 
     try:
-        with BlockReader("127.0.0.1", port, bid, 0, nbytes, verify=verify, batch_packets=batch) as r:
-            pos = 0
-            while pos < nbytes:
-                got = r.read_into(out, pos, min(4 << 20, nbytes - pos))
-                if got == 0:
-                    break
-                pos += got
-            if pos != nbytes:
-                errors.append(f"block {bid}: short read {pos}")
+        with InputStream([(bid, n, [("127.0.0.1", port)]) for bid, n in blocks], verify=verify,
+                         batch_packets=batch) as s:
+            got = s.pread_into(i * bsz, out)
+            if got != bsz:
+                errors.append(f"block {i}: short pread {got}")
     except Exception as e:  # noqa: BLE001 - reported
-        errors.append(f"block {bid}: {e}")
+        errors.append(f"block {i}: {e}")
+
+
+def diag(dn, blocks, out, data, args):
+    """Where a block read spends its time: receive / alloc / launch / wait / deliver (ns)."""
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import BlockReader
+
+    lib = _native.lib()
+    for verify in (True, False, True, False):
+        acc = np.zeros(5, np.uint64)
+        t0 = time.perf_counter()
+        off = 0
+        for bid, n in blocks:
+            with BlockReader("127.0.0.1", dn.port, bid, 0, n, verify=verify, batch_packets=args.batch) as r:
+                pos = 0
+                while pos < n:
+                    got = r.read_into(out, off + pos, min(args.read_mib << 20, n - pos))
+                    assert got > 0
+                    pos += got
+                t = (ctypes.c_uint64 * 5)()
+                _native.check("timing", lib.hdfs3x_block_reader_timing(r.r, t))
+                acc += np.array(list(t), np.uint64)
+            off += n
+        dt = time.perf_counter() - t0
+        assert np.array_equal(out[:off], data[:off])
+        print(json.dumps({"bench": "e2e_diag", "verify": verify, "gib_s": round(off / dt / GIB, 2),
+                          "wall_ms": round(dt * 1e3, 1),
+                          **{k: round(float(v) / 1e6, 1) for k, v in
+                             zip(["recv_ms", "alloc_ms", "launch_ms", "wait_ms", "deliver_ms"], acc)}}),
+              flush=True)
 
 
 def main():
@@ -62,6 +90,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--packet-kib", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--read-mib", type=int, default=4, help="hdfsRead request size")
+    ap.add_argument("--diag", action="store_true", help="per-phase timing of the block reader only")
     args = ap.parse_args()
 
     from libhdfs3_amd import _native
@@ -89,30 +119,41 @@ def main():
     del pinned
     lib.hdfs3_host_free_pinned(hp)
 
-    lb = _native.loopback()
-    port = ctypes.c_int(0)
-    assert lb.hdfs3_loopback_start(ctypes.byref(port)) == 0
-    lb.hdfs3_loopback_set_packet_bytes(args.packet_kib << 10)
+    from loopback import LoopbackDatanode
+    from libhdfs3_amd.engine import InputStream
+
+    dn = LoopbackDatanode(packet_bytes=args.packet_kib << 10)
     blocks = []
     for i in range(args.blocks):
         d = data[i * bsz:(i + 1) * bsz]
         c = crc[4 * (i * bsz // args.bpc): 4 * ((i + 1) * bsz // args.bpc)]
-        assert lb.hdfs3_loopback_add_block(10 + i, d.ctypes.data, d.nbytes, c.ctypes.data, args.bpc, 2) == 0
-        blocks.append((d, c))
+        dn.add_block(10 + i, d, c, args.bpc)
+        blocks.append((10 + i, bsz))
     out = np.empty(total, dtype=np.uint8)
+    if args.diag:
+        try:
+            diag(dn, blocks, out, data, args)
+        finally:
+            dn.stop()
+        return
     try:
         for verify in (True, False):
-            for readers in (1, args.blocks):
+            for mode in ("hdfsRead", "parallel_pread"):
                 best = 0.0
                 for _ in range(args.reps):
                     errors: list[str] = []
                     t0 = time.perf_counter()
-                    if readers == 1:
-                        for i in range(args.blocks):
-                            read_block(port.value, 10 + i, bsz, out[i * bsz:(i + 1) * bsz], verify, args.batch, errors)
+                    if mode == "hdfsRead":
+                        with InputStream([(b, n, [("127.0.0.1", dn.port)]) for b, n in blocks], verify=verify,
+                                         batch_packets=args.batch) as s:
+                            pos = 0
+                            while pos < total:
+                                got = s.read_into(out, pos, min(args.read_mib << 20, total - pos))
+                                assert got > 0
+                                pos += got
                     else:
-                        th = [threading.Thread(target=read_block,
-                                               args=(port.value, 10 + i, bsz, out[i * bsz:(i + 1) * bsz], verify,
+                        th = [threading.Thread(target=pread_block,
+                                               args=(blocks, dn.port, i, bsz, out[i * bsz:(i + 1) * bsz], verify,
                                                      args.batch, errors)) for i in range(args.blocks)]
                         for t in th:
                             t.start()
@@ -122,11 +163,12 @@ def main():
                     assert not errors, errors
                     best = max(best, total / dt / GIB)
                 assert np.array_equal(out, data)
-                print(json.dumps({**line, "mode": "loopback_read", "verify": verify, "readers": readers,
-                                  "batch_packets": args.batch, "packet_kib": args.packet_kib,
+                out[:] = 0
+                print(json.dumps({**line, "mode": mode, "verify": verify, "streams": 1 if mode == "hdfsRead"
+                                  else args.blocks, "batch_packets": args.batch, "packet_kib": args.packet_kib,
                                   "gib_s": round(best, 2)}), flush=True)
     finally:
-        lb.hdfs3_loopback_stop()
+        dn.stop()
     ctx.close()
 
 
