@@ -13,7 +13,8 @@ LIB      := $(LIBDIR)/libhdfs3_crc.so
 LOOPBACK := $(LIBDIR)/libhdfs3_loopback.so
 OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc32c.o \
             $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/client_block_reader.o \
-            $(OBJDIR)/client_input_stream.o $(OBJDIR)/client_output_stream.o
+            $(OBJDIR)/client_input_stream.o $(OBJDIR)/client_output_stream.o \
+            $(OBJDIR)/client_local_reader.o
 
 all: $(LIB) $(LOOPBACK) oracle
 
@@ -46,6 +47,10 @@ $(OBJDIR)/client_input_stream.o: $(CSRC)/client/input_stream.cpp $(CSRC)/client/
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(OBJDIR)/client_output_stream.o: $(CSRC)/client/output_stream.cpp include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h $(CSRC)/client/wire.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(OBJDIR)/client_local_reader.o: $(CSRC)/client/local_reader.cpp include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h $(CSRC)/client/wire.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 

@@ -111,6 +111,34 @@ int hdfs3_input_stats(hdfs3_input_stream *s, uint64_t *failovers, uint64_t *read
 int hdfs3_input_close(hdfs3_input_stream *s);
 
 /* ------------------------------------------------------------------------------------
+ * Local (short-circuit) block reader: LocalBlockReader (LocalBlockReader.cpp:46-263) over
+ * a block file and its .meta file (BE16 version 1 | u8 type | BE32 bytesPerChecksum |
+ * BE32 CRC per chunk). Every chunk is verified on the GPU, the short tail included
+ * (:138-163); windows of window_buffers x buffer_size bytes are read ahead by a loader
+ * thread. On a mismatch nothing of the buffer_size buffer holding the first bad chunk is
+ * returned — the reference verifies a whole buffer before returning any of it — and
+ * read returns -EIO ("ChecksumException"). Same -errno convention as the block reader.
+ * ---------------------------------------------------------------------------------- */
+typedef struct hdfs3_local_reader hdfs3_local_reader;
+
+typedef struct hdfs3_local_opts {
+    int device;
+    int verify;               /* 0: no verification                                     */
+    int32_t buffer_size;      /* input.localread.default.buffersize (1 MiB), chunk-rounded */
+    int window_buffers;       /* buffers per GPU window (16)                            */
+} hdfs3_local_opts;
+
+/* num_bytes <= 0 takes the block file's size; offset skips like LocalBlockReader::skip.
+ * -EIO on a bad version/type, -ENOTSUP for CHECKSUM_CRC32 meta. */
+int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_t num_bytes, int64_t offset,
+                            const hdfs3_local_opts *opts, hdfs3_local_reader **out);
+int32_t hdfs3_local_reader_read(hdfs3_local_reader *r, void *buf, int32_t len);
+int64_t hdfs3_local_reader_available(hdfs3_local_reader *r);
+int hdfs3_local_reader_stats(hdfs3_local_reader *r, uint32_t *bytes_per_checksum, int *checksum_type,
+                             uint64_t *gpu_batches);
+int hdfs3_local_reader_close(hdfs3_local_reader *r);
+
+/* ------------------------------------------------------------------------------------
  * Output stream: the hdfsWrite / hdfsFlush / hdfsSync / hdfsTell / hdfsCloseFile surface
  * (Hdfs.cpp:864-922) over OutputStreamImpl's append/flush/close (OutputStreamImpl.cpp:
  * 298-441, 512-575). Every chunk's CRC32C is computed on the GPU in batches of packets

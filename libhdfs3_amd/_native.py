@@ -92,6 +92,12 @@ class LocatedBlock(ctypes.Structure):
                 ("n_replicas", c_int)]
 
 
+class LocalOpts(ctypes.Structure):
+    """hdfs3_local_opts (include/hdfs3_client.h)."""
+
+    _fields_ = [("device", c_int), ("verify", c_int), ("buffer_size", ctypes.c_int32), ("window_buffers", c_int)]
+
+
 class PacketInfo(ctypes.Structure):
     """hdfs3_packet_info (include/hdfs3_client.h)."""
 
@@ -128,6 +134,12 @@ CLIENT_API = {
     "hdfs3_input_length": (c_int64, [c_void_p]),
     "hdfs3_input_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "hdfs3_input_close": (c_int, [c_void_p]),
+    "hdfs3_local_reader_open": (c_int, [ctypes.c_char_p, ctypes.c_char_p, c_int64, c_int64, POINTER(LocalOpts),
+                                        POINTER(c_void_p)]),
+    "hdfs3_local_reader_read": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),
+    "hdfs3_local_reader_available": (c_int64, [c_void_p]),
+    "hdfs3_local_reader_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_int), POINTER(c_uint64)]),
+    "hdfs3_local_reader_close": (c_int, [c_void_p]),
     "hdfs3_output_open": (c_int, [POINTER(WriterOpts), PACKET_SINK, c_void_p, POINTER(c_void_p)]),
     "hdfs3_output_write": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),
     "hdfs3_output_flush": (c_int, [c_void_p]),

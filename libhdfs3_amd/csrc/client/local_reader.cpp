@@ -1,0 +1,377 @@
+// hdfs3_local_reader: LocalBlockReader (src/client/LocalBlockReader.cpp) — the short-
+// circuit read of a block file and its .meta file — with readAndVerify's per-chunk CPU
+// loop (:138-163) replaced by GPU verification of large windows.
+//
+// .meta layout (:40-43, :64-121): BE16 version (1) | u8 checksum type | BE32 bytesPerChecksum
+// | one BE32 CRC per chunk. Local semantics check every chunk, the short tail included.
+//
+// Pipeline: a loader thread preads a window (window_buffers x buffer_size bytes of block
+// data, chunk aligned) and its CRC words into a pinned arena, then queues H2D + verify
+// (check_short_tail=1) + result D2H + event on the ctx stream; the caller's read() waits
+// for a window's event and copies verified bytes out, while the loader fills the next.
+// Delivery granularity on a mismatch is the reference's: readAndVerify verifies one
+// buffer_size buffer before any of it is returned, so bytes of the buffer holding the
+// first bad chunk — and everything after — are withheld and -EIO is returned.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+
+#include "../ctx.h"
+#include "hdfs3_client.h"
+#include "hdfs3_crc.h"
+#include "wire.h"
+
+using namespace hdfs3crc;
+
+namespace {
+
+constexpr int kMetaHeader = 7;             // HEADER_SIZE: version 2 + type 1 + bpc 4
+constexpr int kSlots = 3;
+constexpr int32_t kDefaultBuffer = 1 << 20;  // input.localread.default.buffersize
+constexpr int kDefaultWindowBuffers = 16;
+
+int hip_err(hipError_t e, const char *what) {
+    return fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIP_OK(expr)                                      \
+    do {                                                  \
+        hipError_t e_ = (expr);                           \
+        if (e_ != hipSuccess) return hip_err(e_, #expr);  \
+    } while (0)
+
+int pread_fully(int fd, void *buf, size_t n, int64_t off) {
+    uint8_t *p = static_cast<uint8_t *>(buf);
+    while (n) {
+        const ssize_t r = ::pread(fd, p, n, off);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return -errno;
+        }
+        if (r == 0) return -EIO;  // file shorter than the block / meta says
+        p += r;
+        n -= size_t(r);
+        off += r;
+    }
+    return 0;
+}
+
+struct Window {
+    PacketArena a;            // h/d: [data (cap_data)][crc words]
+    int64_t start = 0;        // block offset of the window's first byte (chunk aligned)
+    uint32_t len = 0;         // data bytes
+    int64_t bad_chunk = -1;   // first mismatching chunk (block-relative), after wait
+    bool verified = false;
+};
+
+}  // namespace
+
+struct hdfs3_local_reader {
+    int data_fd = -1, meta_fd = -1;
+    hdfs3_crc_ctx *ctx = nullptr;
+    bool verify = true;
+    int checksum_type = 2;
+    uint32_t chunk_size = 0;
+    int32_t buffer_size = kDefaultBuffer;    // localBufferSize (chunk-rounded when verifying)
+    uint32_t window = 0;                     // bytes per GPU window (multiple of buffer_size)
+    size_t cap_data = 0;
+    int64_t length = 0;                      // block length
+    int64_t first = 0;                       // first byte the loader reads (chunk aligned)
+    int64_t cursor = 0;                      // next byte handed to the caller
+
+    std::mutex mu;
+    std::condition_variable cv;
+    Window slot[kSlots];
+    std::deque<int> ready, free_slots;
+    bool load_done = false, stop = false;
+    int load_error = 0;
+    std::string load_msg;
+    std::thread loader;
+    int error = 0;
+    std::string error_msg;
+    std::atomic<uint64_t> batches{0};
+
+    int sticky(int code, const std::string &msg) {
+        error = code;
+        error_msg = msg;
+        return fail(code, "%s", msg.c_str());
+    }
+
+    // LocalBlockReader ctor (:46-130): meta header, engine selection, buffer size
+    int open_meta(bool want_verify) {
+        uint8_t h[kMetaHeader];
+        if (int rc = pread_fully(meta_fd, h, sizeof(h), 0)) return sticky(rc, "LocalBlockReader: cannot read the meta header");
+        const int version = (h[0] << 8) | h[1];
+        if (version != 1)
+            return sticky(-EIO, "LocalBlockReader get an unmatched block, expected block version 1, real version is " +
+                                    std::to_string(version));
+        checksum_type = h[2];
+        verify = want_verify;
+        switch (checksum_type) {
+        case wire::kChecksumNull: verify = false; break;
+        case wire::kChecksumCrc32c:
+            chunk_size = (uint32_t(h[3]) << 24) | (uint32_t(h[4]) << 16) | (uint32_t(h[5]) << 8) | h[6];
+            break;
+        case wire::kChecksumCrc32:
+            // the reference verifies CRC32 meta with its CRC32C engine (:82-96); see DESIGN.md §7
+            return sticky(-ENOTSUP, "CHECKSUM_CRC32 (zlib) .meta is not implemented on the GPU path");
+        default:
+            return sticky(-EIO, "LocalBlockReader cannot recognize checksum type: " + std::to_string(checksum_type));
+        }
+        if (verify && (chunk_size == 0 || chunk_size > (64u << 20)))
+            return sticky(-EIO, "LocalBlockReader get an invalid checksum parameter, bytes per check: " +
+                                    std::to_string(chunk_size));
+        return 0;
+    }
+
+    // ---- loader thread ------------------------------------------------------------------
+    int load(Window &w, int64_t start) {
+        w.start = start;
+        w.len = uint32_t(std::min<int64_t>(window, length - start));
+        w.bad_chunk = -1;
+        w.verified = false;
+        if (int rc = pread_fully(data_fd, w.a.h, w.len, start)) {
+            load_msg = "LocalBlockReader: failed to read the block file";
+            return rc;
+        }
+        batches.fetch_add(1, std::memory_order_relaxed);
+        if (!verify) {
+            w.verified = true;
+            return 0;
+        }
+        const uint64_t chunk0 = uint64_t(start) / chunk_size;
+        const uint64_t chunks = (uint64_t(w.len) + chunk_size - 1) / chunk_size;
+        if (int rc = pread_fully(meta_fd, w.a.h + cap_data, 4 * chunks, kMetaHeader + 4 * int64_t(chunk0))) {
+            load_msg = "LocalBlockReader: failed to read the meta file";
+            return rc;
+        }
+        HIP_OK(hipMemcpyAsync(w.a.d, w.a.h, w.len, hipMemcpyHostToDevice, ctx->stream));
+        HIP_OK(hipMemcpyAsync(w.a.d + cap_data, w.a.h + cap_data, 4 * chunks, hipMemcpyHostToDevice, ctx->stream));
+        HIP_OK(hipMemsetAsync(w.a.d_res, 0, sizeof(unsigned long long), ctx->stream));
+        if (int rc = hdfs3_crc32c_verify_dev_async(ctx, w.a.d, w.len, chunk_size, w.a.d + cap_data,
+                                                   /*check_short_tail=*/1, reinterpret_cast<uint64_t *>(w.a.d_res))) {
+            load_msg = hdfs3_crc_last_error();
+            return rc;
+        }
+        HIP_OK(hipMemcpyAsync(w.a.h_res, w.a.d_res, sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_OK(hipEventRecord(w.a.done, ctx->stream));
+        return 0;
+    }
+
+    void run_loader() {
+        (void)hipSetDevice(ctx->device);
+        int64_t next = first;
+        while (next < length) {
+            int s;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || !free_slots.empty(); });
+                if (stop) return;
+                s = free_slots.front();
+                free_slots.pop_front();
+            }
+            const int rc = load(slot[s], next);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (rc) {
+                    load_error = rc;
+                    if (load_msg.empty()) load_msg = hdfs3_crc_last_error();
+                    free_slots.push_back(s);
+                } else {
+                    ready.push_back(s);
+                }
+                if (rc || next + slot[s].len >= length) load_done = true;
+            }
+            cv.notify_all();
+            if (rc) return;
+            next += slot[s].len;
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        load_done = true;
+        cv.notify_all();
+    }
+
+    // ---- caller side ----------------------------------------------------------------------
+    int wait(Window &w) {
+        if (w.verified) return 0;
+        HIP_OK(hipEventSynchronize(w.a.done));
+        const unsigned long long r = *w.a.h_res;
+        if (r) w.bad_chunk = int64_t(uint64_t(w.start) / chunk_size) + hdfs3_crc_decode_result(r);
+        w.verified = true;
+        return 0;
+    }
+
+    int32_t read(uint8_t *out, int32_t len) {
+        if (error) return fail(error, "%s", error_msg.c_str());
+        if (!out || len <= 0) return fail(-EINVAL, "invalid read buffer");
+        int32_t total = 0;
+        while (total < len && cursor < length) {
+            int s;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !ready.empty() || load_done; });
+                if (ready.empty()) {
+                    if (load_error) {
+                        const int code = load_error;
+                        const std::string msg = load_msg;
+                        lk.unlock();
+                        if (total) {
+                            error = code;
+                            error_msg = msg;
+                            return total;
+                        }
+                        return sticky(code, msg);
+                    }
+                    break;
+                }
+                s = ready.front();
+            }
+            Window &w = slot[s];
+            if (int rc = wait(w)) return total ? total : sticky(rc, hdfs3_crc_last_error());
+            // deliverable end: everything, or up to the local buffer holding the bad chunk
+            int64_t end = w.start + w.len;
+            if (w.bad_chunk >= 0) {
+                const int64_t bad_off = w.bad_chunk * int64_t(chunk_size);
+                end = first + (bad_off - first) / buffer_size * int64_t(buffer_size);
+            }
+            const int64_t begin = std::max<int64_t>(cursor, w.start);
+            if (begin < end) {
+                const int64_t n = std::min<int64_t>(end - begin, len - total);
+                std::memcpy(out + total, w.a.h + (begin - w.start), size_t(n));
+                total += int32_t(n);
+                cursor = begin + n;
+            }
+            if (w.bad_chunk >= 0 && cursor >= end) {
+                sticky(-EIO, "ChecksumException: LocalBlockReader checksum not match for block (chunk " +
+                                 std::to_string(w.bad_chunk) + ")");
+                return total ? total : error;
+            }
+            if (cursor >= w.start + w.len) {
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    ready.pop_front();
+                    free_slots.push_back(s);
+                }
+                cv.notify_all();
+            }
+        }
+        return total;
+    }
+
+    int64_t available() {
+        std::lock_guard<std::mutex> lk(mu);
+        int64_t a = 0;
+        for (int s : ready)
+            if (slot[s].verified && slot[s].bad_chunk < 0)
+                a += slot[s].start + slot[s].len - std::max<int64_t>(cursor, slot[s].start);
+        return a;
+    }
+
+    ~hdfs3_local_reader() {
+        if (loader.joinable()) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                stop = true;
+            }
+            cv.notify_all();
+            loader.join();
+        }
+        if (ctx) {
+            (void)hipStreamSynchronize(ctx->stream);
+            for (Window &w : slot) w.a.release();
+            hdfs3_crc_ctx_destroy(ctx);
+        }
+        if (data_fd >= 0) ::close(data_fd);
+        if (meta_fd >= 0) ::close(meta_fd);
+    }
+};
+
+extern "C" {
+
+int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_t num_bytes, int64_t offset,
+                            const hdfs3_local_opts *opts, hdfs3_local_reader **out) {
+    if (!out || !data_path || !meta_path || offset < 0) return fail(-EINVAL, "invalid argument");
+    *out = nullptr;
+    hdfs3_local_reader *r = new (std::nothrow) hdfs3_local_reader();
+    if (!r) return fail(-ENOMEM, "reader allocation");
+    auto bail = [&](int rc) {
+        delete r;
+        return rc;
+    };
+    const int device = opts ? opts->device : 0;
+    if (opts && opts->buffer_size > 0) r->buffer_size = opts->buffer_size;
+    const int wbuf = opts && opts->window_buffers > 0 ? opts->window_buffers : kDefaultWindowBuffers;
+    r->data_fd = ::open(data_path, O_RDONLY | O_CLOEXEC);
+    if (r->data_fd < 0) return bail(fail(-errno, "LocalBlockReader: cannot open block file %s", data_path));
+    r->meta_fd = ::open(meta_path, O_RDONLY | O_CLOEXEC);
+    if (r->meta_fd < 0) return bail(fail(-errno, "LocalBlockReader: cannot open meta file %s", meta_path));
+    struct stat st;
+    if (fstat(r->data_fd, &st) != 0) return bail(fail(-errno, "fstat failed"));
+    r->length = num_bytes > 0 ? num_bytes : int64_t(st.st_size);
+    if (num_bytes > int64_t(st.st_size)) return bail(fail(-EIO, "block file shorter than the block length"));
+    if (offset > r->length) return bail(fail(-EINVAL, "offset beyond the block"));
+    if (int rc = r->open_meta(opts ? opts->verify != 0 : true)) return bail(rc);
+    if (r->verify) {  // chunk-rounded local buffer (:112-116); reads start on a chunk (skip, :232-263)
+        r->buffer_size = int32_t((int64_t(r->buffer_size) + r->chunk_size - 1) / r->chunk_size * r->chunk_size);
+        r->first = offset / r->chunk_size * r->chunk_size;
+    } else {
+        r->first = offset;
+    }
+    r->cursor = offset;
+    r->window = uint32_t(std::min<int64_t>(int64_t(r->buffer_size) * wbuf, 1ll << 30) / r->buffer_size * r->buffer_size);
+    r->cap_data = (size_t(r->window) + 255) & ~size_t(255);
+    if (int rc = hdfs3_crc_ctx_create(device, &r->ctx)) return bail(rc);
+    const size_t crc_bytes = r->verify ? 4 * ((size_t(r->window) + r->chunk_size - 1) / r->chunk_size) : 0;
+    for (Window &w : r->slot) {
+        PacketArena &a = w.a;
+        if (hipHostMalloc(reinterpret_cast<void **>(&a.h), r->cap_data + crc_bytes, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.d), r->cap_data + crc_bytes) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.d_res), sizeof(unsigned long long)) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&a.done, hipEventDisableTiming) != hipSuccess)
+            return bail(fail(-ENOMEM, "LocalBlockReader: window allocation failed"));
+        a.cap = r->cap_data + crc_bytes;
+    }
+    for (int i = 0; i < kSlots; ++i) r->free_slots.push_back(i);
+    if (r->first < r->length) {
+        r->loader = std::thread([r] { r->run_loader(); });
+    } else {
+        r->load_done = true;
+    }
+    *out = r;
+    return 0;
+}
+
+int32_t hdfs3_local_reader_read(hdfs3_local_reader *r, void *buf, int32_t len) {
+    if (!r) return fail(-EINVAL, "null reader");
+    return r->read(static_cast<uint8_t *>(buf), len);
+}
+
+int64_t hdfs3_local_reader_available(hdfs3_local_reader *r) { return r ? r->available() : 0; }
+
+int hdfs3_local_reader_stats(hdfs3_local_reader *r, uint32_t *bpc, int *checksum_type, uint64_t *gpu_batches) {
+    if (!r) return fail(-EINVAL, "null reader");
+    if (bpc) *bpc = r->chunk_size;
+    if (checksum_type) *checksum_type = r->checksum_type;
+    if (gpu_batches) *gpu_batches = r->batches.load();
+    return 0;
+}
+
+int hdfs3_local_reader_close(hdfs3_local_reader *r) {
+    delete r;
+    return 0;
+}
+
+}  // extern "C"

@@ -404,3 +404,56 @@ class OutputStream:
                 self._lib.hdfs3_output_close(self.s)
         except Exception:
             pass
+
+
+class LocalBlockReader:
+    """hdfs3_local_reader (include/hdfs3_client.h): short-circuit read of a block file and
+    its .meta file with GPU verification of every chunk."""
+
+    def __init__(self, data_path: str, meta_path: str, *, num_bytes: int = 0, offset: int = 0, device: int = 0,
+                 verify: bool = True, buffer_size: int = 1 << 20, window_buffers: int = 16):
+        self._lib = _native.lib()
+        opts = _native.LocalOpts(device, int(verify), buffer_size, window_buffers)
+        p = c_void_p()
+        check("hdfs3_local_reader_open",
+              self._lib.hdfs3_local_reader_open(str(data_path).encode(), str(meta_path).encode(), num_bytes, offset,
+                                                byref(opts), byref(p)))
+        self.r = p.value
+
+    def read_into(self, out: np.ndarray, offset: int = 0, n: int | None = None) -> int:
+        n = out.nbytes - offset if n is None else n
+        got = self._lib.hdfs3_local_reader_read(self.r, out.ctypes.data + offset, min(n, 0x7FFFFFFF))
+        return check("hdfs3_local_reader_read", got)
+
+    def read_all(self, length: int, chunk: int = 4 << 20) -> np.ndarray:
+        out = np.empty(length, dtype=np.uint8)
+        pos = 0
+        while pos < length:
+            got = self.read_into(out, pos, min(chunk, length - pos))
+            if got == 0:
+                break
+            pos += got
+        return out[:pos]
+
+    def stats(self):
+        from ctypes import c_uint32, c_uint64
+        bpc, t, b = c_uint32(), c_int(), c_uint64()
+        check("hdfs3_local_reader_stats", self._lib.hdfs3_local_reader_stats(self.r, byref(bpc), byref(t), byref(b)))
+        return {"bytes_per_checksum": bpc.value, "checksum_type": t.value, "gpu_batches": b.value}
+
+    def close(self):
+        if self.r:
+            self._lib.hdfs3_local_reader_close(self.r)
+            self.r = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
