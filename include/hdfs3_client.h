@@ -129,7 +129,8 @@ typedef struct hdfs3_local_opts {
 } hdfs3_local_opts;
 
 /* num_bytes <= 0 takes the block file's size; offset skips like LocalBlockReader::skip.
- * -EIO on a bad version/type, -ENOTSUP for CHECKSUM_CRC32 meta. */
+ * -EIO on a bad version or unknown type. CHECKSUM_CRC32 meta is verified with the zlib
+ * polynomial (the reference uses its CRC32C engine there, LocalBlockReader.cpp:82-96). */
 int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_t num_bytes, int64_t offset,
                             const hdfs3_local_opts *opts, hdfs3_local_reader **out);
 int32_t hdfs3_local_reader_read(hdfs3_local_reader *r, void *buf, int32_t len);

@@ -39,7 +39,10 @@ extern "C" {
 
 #define HDFS3_CRC_ABI_VERSION 1
 
-/* CHECKSUM_TYPE_CRC32C (src/common/Checksum.h:35) — the only type implemented. */
+/* ChecksumTypeProto (hdfs.proto; Checksum.h:34-35). CRC32C is the default of every
+ * ctx; CRC32 (zlib polynomial, boost::crc_32_type in the reference, Crc32.h:41-75) is
+ * selected per ctx with hdfs3_crc_ctx_set_checksum_type. */
+#define HDFS3_CHECKSUM_TYPE_CRC32 1
 #define HDFS3_CHECKSUM_TYPE_CRC32C 2
 
 typedef struct hdfs3_crc_ctx hdfs3_crc_ctx;
@@ -69,6 +72,11 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx);
 int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream);
 void *hdfs3_crc_ctx_get_stream(hdfs3_crc_ctx *ctx);
 int hdfs3_crc_ctx_synchronize(hdfs3_crc_ctx *ctx);
+/* Polynomial used by every later compute/verify call on this ctx (the hdfs3_crc32c_*
+ * names are kept for the default): HDFS3_CHECKSUM_TYPE_CRC32C or _CRC32; -EINVAL else.
+ * The same kernels run either way; only the table image differs. */
+int hdfs3_crc_ctx_set_checksum_type(hdfs3_crc_ctx *ctx, int type);
+int hdfs3_crc_ctx_get_checksum_type(hdfs3_crc_ctx *ctx);
 /* Number of checksum kernels this ctx has launched (lets callers/tests prove the
  * GPU path ran). */
 uint64_t hdfs3_crc_ctx_kernel_launches(hdfs3_crc_ctx *ctx);

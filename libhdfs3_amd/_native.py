@@ -64,6 +64,8 @@ PUBLIC_API = {
     "hdfs3_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
     "hdfs3_memset_dev": (c_int, [c_void_p, c_void_p, c_int, c_size_t]),
     "hdfs3_device_count": (c_int, [POINTER(c_int)]),
+    "hdfs3_crc_ctx_set_checksum_type": (c_int, [c_void_p, c_int]),
+    "hdfs3_crc_ctx_get_checksum_type": (c_int, [c_void_p]),
 }
 
 class BlockId(ctypes.Structure):

@@ -131,6 +131,7 @@ struct hdfs3_block_reader {
     int64_t start = 0, end_offset = 0;
     uint32_t chunk_size = 0;
     uint32_t checksum_size = 0;
+    const uint32_t *tables = nullptr;  // slice tables of the negotiated polynomial
 
     // receiver-thread state (touched only by the receiver once it runs)
     int64_t recv_cursor = 0;   // "cursor" as seen by readNextPacket for the next packet
@@ -181,9 +182,9 @@ struct hdfs3_block_reader {
         chunk_size = r.bytes_per_checksum;
         switch (r.checksum_type) {
         case wire::kChecksumNull: verify = false; checksum_size = 0; break;
-        case wire::kChecksumCrc32c: checksum_size = 4; break;
-        case wire::kChecksumCrc32:
-            return sticky(-ENOTSUP, "CHECKSUM_CRC32 (zlib) is not implemented on the GPU path (DESIGN.md §7)");
+        case wire::kChecksumCrc32c: checksum_size = 4; tables = ctx->d_tables_by[0]; break;
+        // the engine switch of :158-189 (Crc32 for CHECKSUM_CRC32): the zlib-polynomial image
+        case wire::kChecksumCrc32: checksum_size = 4; tables = ctx->d_tables_by[1]; break;
         default: return sticky(-EPROTO, "RemoteBlockReader cannot recognize checksum type");
         }
         if (chunk_size == 0 || (checksum_size && (chunk_size & 3u)))
@@ -278,7 +279,7 @@ struct hdfs3_block_reader {
                               ctx->stream));
         HIP_OK(hipMemsetAsync(b.a.d_res, 0, sizeof(unsigned long long), ctx->stream));
         HIP_OK(launch_packets(b.a.d, b.a.d_desc, b.pk.size(), chunk_size, true, /*check_short_tail=*/0, b.a.d_res,
-                              ctx->d_tables, ctx->grid_cap, ctx->stream));
+                              tables, ctx->grid_cap, ctx->stream));
         ++ctx->launches;
         HIP_OK(hipMemcpyAsync(b.a.h_res, b.a.d_res, sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
         HIP_OK(hipEventRecord(b.a.done, ctx->stream));

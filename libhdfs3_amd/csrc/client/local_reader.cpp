@@ -122,11 +122,12 @@ struct hdfs3_local_reader {
         switch (checksum_type) {
         case wire::kChecksumNull: verify = false; break;
         case wire::kChecksumCrc32c:
+        case wire::kChecksumCrc32:
+            // Divergence, on purpose: the reference checks CRC32 meta with its CRC32C engine
+            // (:82-96), so such a block can never pass a short-circuit read there; this
+            // verifies it with the polynomial the meta declares.
             chunk_size = (uint32_t(h[3]) << 24) | (uint32_t(h[4]) << 16) | (uint32_t(h[5]) << 8) | h[6];
             break;
-        case wire::kChecksumCrc32:
-            // the reference verifies CRC32 meta with its CRC32C engine (:82-96); see DESIGN.md §7
-            return sticky(-ENOTSUP, "CHECKSUM_CRC32 (zlib) .meta is not implemented on the GPU path");
         default:
             return sticky(-EIO, "LocalBlockReader cannot recognize checksum type: " + std::to_string(checksum_type));
         }
@@ -333,6 +334,8 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
     r->window = uint32_t(std::min<int64_t>(int64_t(r->buffer_size) * wbuf, 1ll << 30) / r->buffer_size * r->buffer_size);
     r->cap_data = (size_t(r->window) + 255) & ~size_t(255);
     if (int rc = hdfs3_crc_ctx_create(device, &r->ctx)) return bail(rc);
+    if (r->checksum_type == wire::kChecksumCrc32)
+        if (int rc = hdfs3_crc_ctx_set_checksum_type(r->ctx, HDFS3_CHECKSUM_TYPE_CRC32)) return bail(rc);
     const size_t crc_bytes = r->verify ? 4 * ((size_t(r->window) + r->chunk_size - 1) / r->chunk_size) : 0;
     for (Window &w : r->slot) {
         PacketArena &a = w.a;

@@ -11,15 +11,18 @@
 
 namespace hdfs3crc {
 
-constexpr uint32_t kPolyReflected = 0x82F63B78u;
+constexpr uint32_t kPolyReflected = 0x82F63B78u;  // CRC32C (Castagnoli), CHECKSUM_CRC32C
+// CRC-32 (IEEE 802.3 / zlib / boost::crc_32_type, Crc32.h:41-75), CHECKSUM_CRC32: same
+// reflected form, init and final xor, so only the tables differ
+constexpr uint32_t kPolyCrc32 = 0xEDB88320u;
 constexpr int kSlices = 4;
 constexpr int kTableEntries = 256;
 constexpr int kTableWords = kSlices * kTableEntries;  // 1024 words = 4 KiB image
 
-inline void build_slice_tables(uint32_t out[kSlices][kTableEntries]) {
+inline void build_slice_tables(uint32_t out[kSlices][kTableEntries], uint32_t poly = kPolyReflected) {
     for (uint32_t i = 0; i < 256; ++i) {
         uint32_t c = i;
-        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? kPolyReflected : 0u);
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? poly : 0u);
         out[0][i] = c;
     }
     for (int k = 1; k < kSlices; ++k)

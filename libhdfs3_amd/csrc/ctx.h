@@ -60,8 +60,12 @@ struct hdfs3_crc_ctx {
     int grid_cap = 256;            // one 1024-thread workgroup per CU (128 KiB LDS image)
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    uint32_t *d_tables = nullptr;  // 4 x 256 slice-table image
-    uint32_t *d_fold = nullptr;    // lane-fold GF(2) matrices (crc32c_tables.h)
+    uint32_t *d_tables = nullptr;  // active 4 x 256 slice-table image (checksum_type)
+    uint32_t *d_fold = nullptr;    // active lane-fold GF(2) matrices (crc32c_tables.h)
+    // per polynomial: [0] CRC32C (CHECKSUM_CRC32C = 2), [1] CRC-32/zlib (CHECKSUM_CRC32 = 1)
+    uint32_t *d_tables_by[2] = {nullptr, nullptr};
+    uint32_t *d_fold_by[2] = {nullptr, nullptr};
+    int checksum_type = 2;
     unsigned long long *d_result = nullptr;
     unsigned long long *h_result = nullptr;  // pinned
     hdfs3crc::DevPacket *d_pk = nullptr;

@@ -272,25 +272,37 @@ int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out) {
     if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(-EIO, "hipStreamCreate failed"));
     ctx->stream = ctx->own_stream;
-    uint32_t t[kSlices][kTableEntries];
-    build_slice_tables(t);
-    if (hipMalloc(reinterpret_cast<void **>(&ctx->d_tables), sizeof(t)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&ctx->d_result), sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(reinterpret_cast<void **>(&ctx->d_result), sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&ctx->h_result), sizeof(unsigned long long),
                       hipHostMallocDefault) != hipSuccess)
         return bail(fail(-ENOMEM, "device allocation for ctx failed"));
-    if (hipMemcpy(ctx->d_tables, t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess)
-        return bail(fail(-EIO, "table upload failed"));
-    // fold image: kFoldWords matrix columns, then 4 nibble-table sets (G = 8,16,32,64)
-    static uint32_t fold[kFoldWords + 4 * kFoldNibbleWords];
-    static std::once_flag fold_once;
-    std::call_once(fold_once, [&] {
-        build_fold_matrices(t[0], fold);
-        for (int set = 0; set < 4; ++set) build_fold_nibbles(fold, set, fold + kFoldWords + set * kFoldNibbleWords);
+    // per polynomial: slice tables, then the fold image (kFoldWords matrix columns and 4
+    // nibble-table sets for G = 8,16,32,64), built once per process
+    struct Image {
+        uint32_t t[kSlices][kTableEntries];
+        uint32_t fold[kFoldWords + 4 * kFoldNibbleWords];
+    };
+    static Image img[2];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const uint32_t polys[2] = {kPolyReflected, kPolyCrc32};
+        for (int p = 0; p < 2; ++p) {
+            build_slice_tables(img[p].t, polys[p]);
+            build_fold_matrices(img[p].t[0], img[p].fold);
+            for (int set = 0; set < 4; ++set)
+                build_fold_nibbles(img[p].fold, set, img[p].fold + kFoldWords + set * kFoldNibbleWords);
+        }
     });
-    if (hipMalloc(reinterpret_cast<void **>(&ctx->d_fold), sizeof(fold)) != hipSuccess ||
-        hipMemcpy(ctx->d_fold, fold, sizeof(fold), hipMemcpyHostToDevice) != hipSuccess)
-        return bail(fail(-ENOMEM, "fold-matrix upload failed"));
+    for (int p = 0; p < 2; ++p) {
+        if (hipMalloc(reinterpret_cast<void **>(&ctx->d_tables_by[p]), sizeof(img[p].t)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&ctx->d_fold_by[p]), sizeof(img[p].fold)) != hipSuccess)
+            return bail(fail(-ENOMEM, "device allocation for ctx failed"));
+        if (hipMemcpy(ctx->d_tables_by[p], img[p].t, sizeof(img[p].t), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(ctx->d_fold_by[p], img[p].fold, sizeof(img[p].fold), hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(-EIO, "table upload failed"));
+    }
+    ctx->d_tables = ctx->d_tables_by[0];
+    ctx->d_fold = ctx->d_fold_by[0];
     *out = ctx;
     return 0;
 }
@@ -310,8 +322,10 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx) {
     ctx->arena_cache.clear();
     if (ctx->d_pk) (void)hipFree(ctx->d_pk);
     if (ctx->h_pk) (void)hipHostFree(ctx->h_pk);
-    if (ctx->d_tables) (void)hipFree(ctx->d_tables);
-    if (ctx->d_fold) (void)hipFree(ctx->d_fold);
+    for (int p = 0; p < 2; ++p) {
+        if (ctx->d_tables_by[p]) (void)hipFree(ctx->d_tables_by[p]);
+        if (ctx->d_fold_by[p]) (void)hipFree(ctx->d_fold_by[p]);
+    }
     if (ctx->d_result) (void)hipFree(ctx->d_result);
     if (ctx->h_result) (void)hipHostFree(ctx->h_result);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
@@ -327,6 +341,19 @@ int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream) {
 }
 
 void *hdfs3_crc_ctx_get_stream(hdfs3_crc_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
+
+int hdfs3_crc_ctx_set_checksum_type(hdfs3_crc_ctx *ctx, int type) {
+    if (!ctx) return fail(-EINVAL, "null ctx");
+    if (type != HDFS3_CHECKSUM_TYPE_CRC32C && type != HDFS3_CHECKSUM_TYPE_CRC32)
+        return fail(-EINVAL, "checksum type %d has no CRC polynomial", type);
+    const int i = type == HDFS3_CHECKSUM_TYPE_CRC32C ? 0 : 1;
+    ctx->d_tables = ctx->d_tables_by[i];
+    ctx->d_fold = ctx->d_fold_by[i];
+    ctx->checksum_type = type;
+    return 0;
+}
+
+int hdfs3_crc_ctx_get_checksum_type(hdfs3_crc_ctx *ctx) { return ctx ? ctx->checksum_type : -EINVAL; }
 
 int hdfs3_crc_ctx_synchronize(hdfs3_crc_ctx *ctx) {
     if (!ctx) return fail(-EINVAL, "null ctx");

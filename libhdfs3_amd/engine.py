@@ -87,6 +87,14 @@ class CrcContext:
     def set_stream(self, hip_stream: int | None) -> None:
         check("hdfs3_crc_ctx_set_stream", self._lib.hdfs3_crc_ctx_set_stream(self.ctx, hip_stream))
 
+    def set_checksum_type(self, ctype: int) -> None:
+        """2 = CHECKSUM_CRC32C (default), 1 = CHECKSUM_CRC32 (zlib polynomial)."""
+        check("hdfs3_crc_ctx_set_checksum_type", self._lib.hdfs3_crc_ctx_set_checksum_type(self.ctx, ctype))
+
+    @property
+    def checksum_type(self) -> int:
+        return int(self._lib.hdfs3_crc_ctx_get_checksum_type(self.ctx))
+
     def synchronize(self) -> None:
         check("hdfs3_crc_ctx_synchronize", self._lib.hdfs3_crc_ctx_synchronize(self.ctx))
 

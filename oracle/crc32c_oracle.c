@@ -268,3 +268,26 @@ void oracle_fill_splitmix(void *dst, size_t len, uint64_t seed) {
         memcpy(o + i * 8, &z, n);
     }
 }
+
+/* ---- CHECKSUM_CRC32 (boost::crc_32_type behind Crc32.h:41-75) --------------------------
+ * Bit-serial restatement of the published algorithm (reflected, poly 0xEDB88320): slow on
+ * purpose — an independent formulation from the GPU's slice tables. */
+uint32_t oracle_crc32_update(uint32_t state, const void *p, size_t len) {
+    const unsigned char *b = (const unsigned char *)p;
+    for (size_t i = 0; i < len; ++i) {
+        state ^= b[i];
+        for (int k = 0; k < 8; ++k) state = (state >> 1) ^ (0xEDB88320u & (0u - (state & 1u)));
+    }
+    return state;
+}
+
+void oracle_compute_chunks_crc32(const void *data, size_t len, uint32_t bpc, void *crc_be_out) {
+    const unsigned char *d = (const unsigned char *)data;
+    unsigned char *o = (unsigned char *)crc_be_out;
+    size_t chunks = (len + bpc - 1) / bpc;
+    for (size_t i = 0; i < chunks; ++i) {
+        size_t off = i * bpc;
+        size_t sz = len - off < bpc ? len - off : bpc;
+        wr_be32(o + 4 * i, ~oracle_crc32_update(0xFFFFFFFFu, d + off, sz));
+    }
+}

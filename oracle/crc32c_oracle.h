@@ -62,6 +62,16 @@ double oracle_bench_verify(int engine, const void *data, size_t len, uint32_t bp
 /* Deterministic test-data generator shared with tests/util.py (splitmix64). */
 void oracle_fill_splitmix(void *dst, size_t len, uint64_t seed);
 
+/* CHECKSUM_CRC32 — Crc32 (src/common/Crc32.h:41-75) wraps boost::crc_32_type, a
+ * third-party dependency absent from /root/reference (version unpinned; README: "tested
+ * on 1.53+"). Its published parameters: width 32, poly 0x04C11DB7 (reflected
+ * 0xEDB88320), init 0xFFFFFFFF, reflect in/out, final xor 0xFFFFFFFF — the zlib CRC-32.
+ * Parity unpinned by reference tests (none cover type 1); pinned instead by the standard
+ * check value crc32("123456789") = 0xCBF43926 and Python's zlib.crc32 in tests/.
+ * Raw-state update with the same reset/getValue convention as the CRC32C engines. */
+uint32_t oracle_crc32_update(uint32_t state, const void *p, size_t len);
+void oracle_compute_chunks_crc32(const void *data, size_t len, uint32_t bpc, void *crc_be_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -129,16 +129,28 @@ def test_checksum_null_block_reads_without_verify(dn):
     assert np.array_equal(out, data) and st["bytes_per_checksum"] == 512
 
 
-def test_crc32_type_is_reported_not_silently_skipped(dn):
+def test_crc32_type_block_is_verified_with_the_zlib_polynomial(dn):
     from libhdfs3_amd.engine import BlockReader
     from libhdfs3_amd._native import Hdfs3CrcError
+    from util import oracle_compute_crc32
 
     lb, port, add = dn
-    data = splitmix_bytes(4096, 10)
-    lb.add_block(7001, data, np.zeros(32, np.uint8), 512, ctype=1)
-    with pytest.raises(Hdfs3CrcError) as ei:
-        BlockReader("127.0.0.1", port, 7001, 0, data.nbytes)
-    assert ei.value.rc == -errno.ENOTSUP
+    data = splitmix_bytes(2_000_000 + 5, 10)
+    crc = oracle_compute_crc32(data, 512)
+    lb.add_block(7001, data, crc, 512, ctype=1)  # CHECKSUM_CRC32
+    out, st = _read(port, 7001, 0, data.nbytes)
+    assert np.array_equal(out, data)
+    bad = data.copy()
+    bad[1_000_000] ^= 2
+    lb.add_block(7002, bad, crc, 512, ctype=1)
+    with BlockReader("127.0.0.1", port, 7002, 0, data.nbytes) as r:
+        with pytest.raises(Hdfs3CrcError):
+            r.read_all(data.nbytes)
+    # CRC32C words under a CRC32 response must fail (the polynomial follows the response)
+    lb.add_block(7003, data, oracle_compute(data, 512), 512, ctype=1)
+    with BlockReader("127.0.0.1", port, 7003, 0, data.nbytes) as r:
+        with pytest.raises(Hdfs3CrcError):
+            r.read_all(data.nbytes)
 
 
 def test_datanode_drop_mid_block_is_an_io_error(dn):

@@ -100,7 +100,7 @@ def test_null_type_and_verify_off_read_without_checking(tmp_path):
     assert np.array_equal(out, bad)
 
 
-def test_bad_version_and_crc32_type(tmp_path):
+def test_bad_version_is_an_error(tmp_path):
     from libhdfs3_amd._native import Hdfs3CrcError
 
     data = splitmix_bytes(4096, 12)
@@ -108,7 +108,20 @@ def test_bad_version_and_crc32_type(tmp_path):
     with pytest.raises(Hdfs3CrcError) as ei:
         read(d, m)
     assert ei.value.rc == -errno.EIO and "version" in str(ei.value)
-    d, m = write_block(tmp_path, "blk_crc32", data, ctype=1)
-    with pytest.raises(Hdfs3CrcError) as ei:
+
+
+def test_crc32_meta_verified_with_its_own_polynomial(tmp_path):
+    """Divergence from the reference on purpose: LocalBlockReader.cpp:82-96 checks CRC32
+    meta with a CRC32C engine (so such blocks always fail there); here they verify."""
+    from libhdfs3_amd._native import Hdfs3CrcError
+    from util import oracle_compute_crc32
+
+    data = splitmix_bytes(1_000_003, 13)
+    d, m = write_block(tmp_path, "blk_crc32", data, ctype=1, crc=oracle_compute_crc32(data, 512))
+    out, st = read(d, m)
+    assert np.array_equal(out, data) and st["checksum_type"] == 1
+    bad = data.copy()
+    bad[-1] ^= 1  # short tail: checked locally
+    d, m = write_block(tmp_path, "blk_crc32_bad", bad, ctype=1, crc=oracle_compute_crc32(data, 512))
+    with pytest.raises(Hdfs3CrcError):
         read(d, m)
-    assert ei.value.rc == -errno.ENOTSUP

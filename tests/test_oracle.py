@@ -145,3 +145,22 @@ def test_oracle_vs_compiled_reference_random():
         want = ref.ref_hw_crc32c(ptr(buf) + a, n)
         for e in ENGINES:
             assert oracle().oracle_crc32c(e, ptr(buf) + a, n) == want
+
+
+def test_crc32_oracle_matches_zlib_and_check_value():
+    """CHECKSUM_CRC32 (boost::crc_32_type behind Crc32.h:41-75): parity pinned by the
+    standard check value and Python's zlib.crc32 (no reference test covers type 1)."""
+    import zlib
+
+    from util import oracle_compute_crc32, oracle_crc32
+
+    assert oracle_crc32(b"123456789") == 0xCBF43926
+    assert oracle_crc32(b"") == 0
+    buf = splitmix_bytes(5000, 77)
+    for n in list(range(0, 70)) + [511, 512, 513, 4095, 4096, 4097, 5000]:
+        for off in (0, 3):
+            piece = buf[off:off + n]
+            assert oracle_crc32(piece) == zlib.crc32(piece.tobytes())
+    words = oracle_compute_crc32(buf, 512)
+    want = b"".join(zlib.crc32(buf[i:i + 512].tobytes()).to_bytes(4, "big") for i in range(0, buf.nbytes, 512))
+    assert words.tobytes() == want

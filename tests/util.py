@@ -48,6 +48,10 @@ def oracle() -> ctypes.CDLL:
         lib.oracle_bench_verify.restype = c_double
         lib.oracle_bench_verify.argtypes = [c_int, c_void_p, c_size_t, c_uint32, c_void_p, c_int, c_int,
                                             ctypes.POINTER(c_int64)]
+        lib.oracle_crc32_update.restype = c_uint32
+        lib.oracle_crc32_update.argtypes = [c_uint32, c_void_p, c_size_t]
+        lib.oracle_compute_chunks_crc32.restype = None
+        lib.oracle_compute_chunks_crc32.argtypes = [c_void_p, c_size_t, c_uint32, c_void_p]
         lib.oracle_fill_splitmix.restype = None
         lib.oracle_fill_splitmix.argtypes = [c_void_p, c_size_t, c_uint64]
         _ORACLE = lib
@@ -100,6 +104,19 @@ def oracle_compute(data: np.ndarray, bpc: int, engine: int = PCL) -> np.ndarray:
     out = np.zeros(4 * n, dtype=np.uint8)
     oracle().oracle_compute_chunks(engine, ptr(data) if data.nbytes else None, data.nbytes, bpc, ptr(out))
     return out
+
+
+def oracle_compute_crc32(data: np.ndarray, bpc: int) -> np.ndarray:
+    """CHECKSUM_CRC32 words (zlib polynomial) per chunk, big-endian."""
+    n = (data.nbytes + bpc - 1) // bpc
+    out = np.zeros(4 * n, dtype=np.uint8)
+    oracle().oracle_compute_chunks_crc32(ptr(data) if data.nbytes else None, data.nbytes, bpc, ptr(out))
+    return out
+
+
+def oracle_crc32(data: bytes | np.ndarray) -> int:
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    return (~int(oracle().oracle_crc32_update(0xFFFFFFFF, ptr(a) if a.nbytes else None, a.nbytes))) & 0xFFFFFFFF
 
 
 def oracle_verify(data: np.ndarray, bpc: int, crc_be: np.ndarray, check_short_tail: bool,
