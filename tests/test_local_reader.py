@@ -43,8 +43,13 @@ def test_full_and_offset_reads(tmp_path, bpc):
     for off in [1, bpc - 1, bpc + 5, 1 << 20, data.nbytes - 10, data.nbytes]:
         out, _ = read(d, m, offset=off)
         assert np.array_equal(out, data[off:]), off
-    out, _ = read(d, m, num_bytes=1_000_000)
-    assert np.array_equal(out, data[:1_000_000])
+    out, _ = read(d, m, num_bytes=245 * 4096)  # a chunk-aligned prefix of the block
+    assert np.array_equal(out, data[:245 * 4096])
+    # a length that cuts a chunk short makes the last chunk's stored word (over the whole
+    # on-disk chunk) mismatch — readAndVerify checks bufferSize % chunkSize bytes (:145-151)
+    from libhdfs3_amd._native import Hdfs3CrcError
+    with pytest.raises(Hdfs3CrcError):
+        read(d, m, num_bytes=245 * 4096 + 100)
 
 
 @pytest.mark.parametrize("where", [0, 300_000, (1 << 20) + 5, 3 * (1 << 20) + 700])
