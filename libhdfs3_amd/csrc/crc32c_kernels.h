@@ -21,6 +21,7 @@ struct ChunkLaunch {
     unsigned long long *result;  // verify: atomicMax(~first_bad) target (device)
     uint64_t chunk_base;      // added to chunk indices reported in *result
     int check_short_tail;     // 1: tail chunk checked (LocalBlockReader semantics)
+    uint64_t *trace = nullptr;  // diagnostic variant 13 only: 4 s_memrealtime stamps per wave
 };
 
 // Packet-descriptor as seen by the device (mirrors hdfs3_pkt_desc).
@@ -41,6 +42,7 @@ hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_
 
 // Measurement knob: selects kernel variants for in-process A/B (0 = production).
 void set_variant(int v);
+void set_trace(uint64_t *d_trace);  // buffer for variant 13 (4 x u64 per wave)
 
 // Measurement-only kernels (bench/profiling): HBM read ceiling and the CRC
 // kernel's access pattern without the table arithmetic.

@@ -558,7 +558,7 @@ __device__ __forceinline__ uint32_t combine(const Look &l, uint32_t next) {
     return xor3(xor3(l.v[0], l.v[1], l.v[2]), l.v[3], next);
 }
 
-template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true>
+template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a,
                                                                     const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
@@ -585,6 +585,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         return k < K ? a.data + (wave + k * nwaves) * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
     };
 
+    // TRACE (variant 13): lane 0 of each wave stamps entry, post-fill, post-first-step
+    // and end of the main loop with the device-wide 100 MHz counter
+    uint64_t *tr = TRACE ? a.trace + 4 * wave : nullptr;
+    auto stamp = [&](int i) {
+        if constexpr (TRACE) {
+            const uint64_t t = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) tr[i] = t;
+        }
+    };
+    stamp(0);
     // table + nibble-image words, then the first round(s), then the LDS fill
     uint32_t tv[kFillPerThread];
     fetch_tables(tv, g_tab);
@@ -602,6 +612,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         dst[1] = n1;
     }
     lds_barrier();
+    stamp(1);
     const Lut t(lds);
     const NibFold nf(lds);
     const uint32_t init = j == 0 ? 0xFFFFFFFFu : 0u;
@@ -670,12 +681,32 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             finish(k, y0, w0);
             finish(k + 1, y1, w1);
         };
+        // PRIO: the SIMD arbiter favours older waves, so with equal work the 4 waves of a
+        // SIMD finish staggered and the last ones run alone, too few to keep the CU's
+        // share of HBM busy (tools/wave_trace.py). Priority by work remaining (quartiles,
+        // s_setprio 3..0) lets lagging waves catch up so the CU drains together.
+        auto prio = [&](uint64_t k) {
+            if constexpr (PRIO) {
+                const uint64_t left = K - k;  // rounds still to consume, incl. this step
+                const uint32_t p = uint32_t(left * 4 > 3 * K ? 3 : left * 4 > 2 * K ? 2 : left * 4 > K ? 1 : 0);
+                switch (p) {  // s_setprio takes an immediate
+                case 3: __builtin_amdgcn_s_setprio(3); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+                }
+            }
+        };
         for (uint64_t k = 0; k < K; k += 4) {
+            prio(k);
             step(b[0], b[1], b[2], b[3], k);
+            if (k == 0) stamp(2);
             if (k + 2 >= K) break;
+            prio(k + 2);
             step(b[2], b[3], b[0], b[1], k + 2);
         }
     }
+    stamp(3);
 
     // slow region: chunks after the last whole round, plus the short tail chunk
     const uint64_t nfull = a.len / BPC;
@@ -845,6 +876,7 @@ hipError_t launch_t(const ChunkLaunch &a, const uint32_t *tab, int grid, hipStre
 }
 
 int g_variant = 0;  // measurement knob (hdfs3x_set_variant); 0 = production choice
+uint64_t *g_trace = nullptr;
 
 template <int BPC, bool V, int DEPTH, bool FOLD4>
 hipError_t launch_r3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
@@ -858,7 +890,7 @@ hipError_t launch_r3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *
     return hipGetLastError();
 }
 
-template <int BPC, bool V, int PAIR, bool NT = false, bool BUF = true>
+template <int BPC, bool V, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false>
 hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                        hipStream_t s) {
     if constexpr (BPC > kRoundBytes) {
@@ -870,8 +902,8 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         const uint64_t units = a.len / kRoundBytes;
         const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
         const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
-        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF>), dim3(grid), dim3(kBlockThreads), 0,
-                           s, a, tab, nib);
+        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO>), dim3(grid),
+                           dim3(kBlockThreads), 0, s, a, tab, nib);
         return hipGetLastError();
     }
 }
@@ -911,6 +943,19 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
         hipLaunchKernelGGL(fixed_cost_kernel<12>, dim3(grid_cap), dim3(kBlockThreads), 0, s, tab,
                            fold + kFoldWords, nullptr);
         return hipGetLastError();
+    case 13: {  // diagnostic: production kernel + per-wave timestamps (tools/wave_trace.py)
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true>(e, tab, fold, grid_cap, s);
+    }
+    case 14: return launch_wave<BPC, V, 2, true, true, false, true>(a, tab, fold, grid_cap, s);  // + s_setprio
+    case 15: {  // 14 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, true>(e, tab, fold, grid_cap, s);
+    }
     default: return launch_wave<BPC, V, 2, true>(a, tab, fold, grid_cap, s);
     }
 }
@@ -968,6 +1013,7 @@ hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_
 }
 
 void set_variant(int v) { g_variant = v; }
+void set_trace(uint64_t *d_trace) { g_trace = d_trace; }
 
 hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,
                               hipStream_t stream) {

@@ -553,5 +553,6 @@ int hdfs3x_grid_cap(hdfs3_crc_ctx *ctx) { return ctx ? ctx->grid_cap : 0; }
 
 // Process-wide kernel-variant knob for in-process A/B measurements (tools/ab.py).
 void hdfs3x_set_variant(int v) { set_variant(v); }
+void hdfs3x_set_trace(void *d_trace) { set_trace(static_cast<uint64_t *>(d_trace)); }
 
 }  // extern "C"
