@@ -146,31 +146,36 @@ def run_steps(work, ctx, mode, n, result, events=None):
 
 
 def batched_rate(torch, work, ctx, mode, reps=20):
-    """Secondary measurement (never `value`): the same blocks verified `blocks` at a time in
-    one launch. The arena keeps the blocks and their CRC arrays contiguous and every block
-    is a whole number of chunks, so one call over the arena verifies each block exactly as
-    the per-block calls do (chunk k of block b is reported as b*N + k). Amortises the
-    per-launch head and dispatch gap the single-block launches pay."""
+    """Secondary measurement (never `value`): the same `blocks` blocks per call through the
+    multi-block batch API (hdfs3_crc32c_{verify,compute}_blocks_dev*, one launch of the
+    segmented wave kernel; each block keeps its own data, CRC array and (block, chunk)
+    result key). Amortises the per-launch head and dispatch gap."""
+    blocks = [(work.data_ptr(b), work.crc_ptr(b), work.block_bytes) for b in range(work.blocks)]
     nbytes = work.block_bytes * work.blocks
     res = torch.zeros(reps, dtype=torch.int64, device=work.data.device)
+
+    def one(i):
+        if mode == "verify":
+            ctx.verify_blocks_dev_async(blocks, work.bpc, res.data_ptr() + 8 * i)
+        else:
+            ctx.compute_blocks_dev(blocks, work.bpc)
+
     for i in range(3):
-        ctx.verify_dev_async(work.data_ptr(0), nbytes, work.bpc, work.crc_ptr(0), res.data_ptr())
+        one(0)
     torch.cuda.synchronize()
     res.zero_()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for i in range(reps):
-        if mode == "verify":
-            ctx.verify_dev_async(work.data_ptr(0), nbytes, work.bpc, work.crc_ptr(0), res.data_ptr() + 8 * i)
-        else:
-            ctx.compute_dev(work.data_ptr(0), nbytes, work.bpc, work.crc_ptr(0))
+        one(i)
     e1.record()
     torch.cuda.synchronize()
     if mode == "verify" and bool((res != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the batched pass")
     t = e0.elapsed_time(e1) * 1e-3 / reps
     alg = work.blocks * work.nchunks * (work.bpc + 4)
-    return {"blocks_per_launch": work.blocks, "value": round(nbytes / t / 2**30, 2), "unit": "GiB/s",
+    return {"api": "hdfs3_crc32c_verify_blocks_dev_async" if mode == "verify" else "hdfs3_crc32c_compute_blocks_dev",
+            "blocks_per_launch": work.blocks, "value": round(nbytes / t / 2**30, 2), "unit": "GiB/s",
             "avg_launch_us": round(t * 1e6, 2), "achieved_GBps": round(alg / t / 1e9, 1),
             "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}
 

@@ -110,6 +110,27 @@ int hdfs3_crc32c_verify_dev_async(hdfs3_crc_ctx *ctx, const void *d_data, size_t
                                   uint64_t *d_result);
 int64_t hdfs3_crc_decode_result(uint64_t result_word);
 
+/* ---- batch of independent device-resident blocks -------------------------------
+ * n blocks (each its own data, CRC array and length; chunk counts < 2^32) verified or
+ * computed in ONE launch of the segmented wave kernel — the batch form of the calls
+ * above, for callers holding several resident blocks (a block scanner, a multi-block
+ * read). Each block is checked exactly as hdfs3_crc32c_verify_dev would check it alone;
+ * the launch amortises the per-launch head and dispatch gap.
+ * Mismatch key = (block << 32) | chunk: the sync form returns the lexicographically
+ * first bad (block, chunk) or -1/-1; the async form leaves ~key (0 when clean) in the
+ * caller-zeroed *d_result (hdfs3_crc_decode_result returns the key). */
+typedef struct hdfs3_dev_block {
+    const void *data;  /* device pointer                                        */
+    void *crc_be;      /* device: stored BE32 words (verify) / written (compute) */
+    uint64_t len;      /* bytes                                                 */
+} hdfs3_dev_block;
+
+int hdfs3_crc32c_verify_blocks_dev(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, uint32_t bpc,
+                                   int check_short_tail, int64_t *bad_block, int64_t *bad_chunk);
+int hdfs3_crc32c_verify_blocks_dev_async(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n,
+                                         uint32_t bpc, int check_short_tail, uint64_t *d_result);
+int hdfs3_crc32c_compute_blocks_dev(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, uint32_t bpc);
+
 /* ---- packet-stream API -----------------------------------------------------
  * n packets of one block in one arena (wire layout of a5/a6 in SURVEY.md §8a).
  * Verifies every chunk of every packet; on mismatch reports the first bad packet

@@ -28,6 +28,12 @@ class PktDesc(ctypes.Structure):
                 ("reserved", c_uint32)]
 
 
+class DevBlock(ctypes.Structure):
+    """hdfs3_dev_block (include/hdfs3_crc.h)."""
+
+    _fields_ = [("data", c_void_p), ("crc_be", c_void_p), ("len", c_uint64)]
+
+
 # name -> (restype, argtypes); every symbol include/hdfs3_crc.h declares.
 PUBLIC_API = {
     "hdfs3_crc_abi_version": (c_int, []),
@@ -65,6 +71,11 @@ PUBLIC_API = {
     "hdfs3_memset_dev": (c_int, [c_void_p, c_void_p, c_int, c_size_t]),
     "hdfs3_device_count": (c_int, [POINTER(c_int)]),
     "hdfs3_crc_ctx_set_checksum_type": (c_int, [c_void_p, c_int]),
+    "hdfs3_crc32c_verify_blocks_dev": (c_int, [c_void_p, POINTER(DevBlock), c_size_t, c_uint32, c_int,
+                                               POINTER(c_int64), POINTER(c_int64)]),
+    "hdfs3_crc32c_verify_blocks_dev_async": (c_int, [c_void_p, POINTER(DevBlock), c_size_t, c_uint32, c_int,
+                                                     c_void_p]),
+    "hdfs3_crc32c_compute_blocks_dev": (c_int, [c_void_p, POINTER(DevBlock), c_size_t, c_uint32]),
     "hdfs3_crc_ctx_get_checksum_type": (c_int, [c_void_p]),
 }
 

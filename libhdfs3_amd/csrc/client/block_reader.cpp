@@ -42,6 +42,7 @@ constexpr int kDefaultBatchPackets = 64;
 constexpr int kDefaultTimeoutMs = 60000;  // input.read.timeout default (SessionConfig.cpp)
 constexpr size_t kMaxResponse = 10u << 20;  // RemoteBlockReader.cpp:116
 constexpr int kSlots = 3;                  // receiving / verifying / delivering
+constexpr int32_t kMaxPacketData = 16 << 20;  // PacketReceiver.MAX_PACKET_SIZE (Hadoop)
 constexpr size_t kArenaCacheMax = 6;       // arenas a ctx keeps for its next reader
 constexpr size_t kPacketGuess = 64 * 1024 + 16 * 1024;  // 64 KiB payload + CRCs + alignment
 
@@ -106,8 +107,8 @@ int grow(PacketArena &a, size_t cap, size_t descs) {
         if (a.d_desc) (void)hipFree(a.d_desc);
         a.h_desc = a.d_desc = nullptr;
         a.desc_cap = 0;
-        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h_desc), descs * sizeof(DevPacket), hipHostMallocDefault));
-        HIP_OK(hipMalloc(reinterpret_cast<void **>(&a.d_desc), descs * sizeof(DevPacket)));
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h_desc), descs * sizeof(DevSegment), hipHostMallocDefault));
+        HIP_OK(hipMalloc(reinterpret_cast<void **>(&a.d_desc), descs * sizeof(DevSegment)));
         a.desc_cap = descs;
     }
     if (!a.d_res) {
@@ -228,6 +229,11 @@ struct hdfs3_block_reader {
                 range_done = true;
                 break;
             }
+            // stricter than the reference on malformed input (it asserts, :237-243): a bounded
+            // packet (Hadoop's PacketReceiver MAX_PACKET_SIZE) that continues the byte stream
+            if (h.data_len > kMaxPacketData) return rx_fail(-EIO, "Invalid Packet, dataLen exceeds 16 MiB");
+            if (h.offset_in_block > recv_cursor || recv_cursor - h.offset_in_block >= h.data_len)
+                return rx_fail(-EIO, "Invalid Packet, offsetInBlock does not continue the block");
             const uint64_t chunks = (uint64_t(h.data_len) + chunk_size - 1) / chunk_size;
             const uint64_t crc_len = chunks * checksum_size;
             if (int64_t(h.packet_len) != 4 + int64_t(h.data_len) + int64_t(crc_len))
@@ -272,14 +278,13 @@ struct hdfs3_block_reader {
             b.verified = true;
             return 0;
         }
-        for (size_t i = 0; i < b.pk.size(); ++i)
-            b.a.h_desc[i] = DevPacket{b.pk[i].data_off, b.pk[i].crc_off, b.pk[i].data_len, 0};
+        std::vector<DevPacket> hp(b.pk.size());
+        for (size_t i = 0; i < b.pk.size(); ++i) hp[i] = DevPacket{b.pk[i].data_off, b.pk[i].crc_off, b.pk[i].data_len, 0};
         HIP_OK(hipMemcpyAsync(b.a.d, b.a.h, b.used, hipMemcpyHostToDevice, ctx->stream));
-        HIP_OK(hipMemcpyAsync(b.a.d_desc, b.a.h_desc, b.pk.size() * sizeof(DevPacket), hipMemcpyHostToDevice,
-                              ctx->stream));
         HIP_OK(hipMemsetAsync(b.a.d_res, 0, sizeof(unsigned long long), ctx->stream));
-        HIP_OK(launch_packets(b.a.d, b.a.d_desc, b.pk.size(), chunk_size, true, /*check_short_tail=*/0, b.a.d_res,
-                              tables, ctx->grid_cap, ctx->stream));
+        HIP_OK(launch_packet_batch(b.a.d, hp.data(), hp.size(), chunk_size, true, /*check_short_tail=*/0, b.a.d_res,
+                                   b.a.h_desc, b.a.d_desc, tables, ctx->d_fold_by[tables == ctx->d_tables_by[1]],
+                                   ctx->grid_cap, ctx->stream));
         ++ctx->launches;
         HIP_OK(hipMemcpyAsync(b.a.h_res, b.a.d_res, sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
         HIP_OK(hipEventRecord(b.a.done, ctx->stream));

@@ -32,6 +32,7 @@ using namespace hdfs3crc;
 namespace {
 
 constexpr int kDefaultBatchPackets = 64;
+constexpr int kMaxBatchPackets = 1024;
 constexpr int kHeader = wire::kPacketHeaderSize;  // 31
 
 uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
@@ -123,9 +124,9 @@ struct hdfs3_output_stream {
             HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.a.h), arena_bytes, hipHostMallocDefault));
             HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.a.d), arena_bytes));
             b.a.cap = arena_bytes;
-            HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.a.h_desc), batch_packets * sizeof(DevPacket),
+            HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.a.h_desc), batch_packets * sizeof(DevSegment),
                                  hipHostMallocDefault));
-            HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.a.d_desc), batch_packets * sizeof(DevPacket)));
+            HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.a.d_desc), batch_packets * sizeof(DevSegment)));
             b.a.desc_cap = size_t(batch_packets);
             HIP_OK(hipEventCreateWithFlags(&b.a.done, hipEventDisableTiming));
             b.pk.reserve(size_t(batch_packets));
@@ -140,9 +141,10 @@ struct hdfs3_output_stream {
         ++batches;
         size_t n = 0;
         uint64_t chunks = 0, lo = UINT64_MAX, hi = 0;
+        DevPacket hp[kMaxBatchPackets];
         for (const Pkt &p : b.pk) {
             if (!p.data_len) continue;
-            b.a.h_desc[n++] = DevPacket{p.data_off, crc_region + 4 * chunks, p.data_len, 0};
+            hp[n++] = DevPacket{p.data_off, crc_region + 4 * chunks, p.data_len, 0};
             chunks += (p.data_len + bpc - 1) / bpc;
             lo = std::min(lo, p.data_off);
             hi = std::max(hi, p.data_off + p.data_len);
@@ -150,9 +152,8 @@ struct hdfs3_output_stream {
         b.chunks = chunks;
         if (n) {
             HIP_OK(hipMemcpyAsync(b.a.d + lo, b.a.h + lo, hi - lo, hipMemcpyHostToDevice, ctx->stream));
-            HIP_OK(hipMemcpyAsync(b.a.d_desc, b.a.h_desc, n * sizeof(DevPacket), hipMemcpyHostToDevice, ctx->stream));
-            HIP_OK(launch_packets(b.a.d, b.a.d_desc, n, bpc, false, 0, nullptr, ctx->d_tables, ctx->grid_cap,
-                                  ctx->stream));
+            HIP_OK(launch_packet_batch(b.a.d, hp, n, bpc, false, 0, nullptr, b.a.h_desc, b.a.d_desc, ctx->d_tables,
+                                       ctx->d_fold, ctx->grid_cap, ctx->stream));
             ++ctx->launches;
             HIP_OK(hipMemcpyAsync(b.a.h + crc_region, b.a.d + crc_region, 4 * chunks, hipMemcpyDeviceToHost,
                                   ctx->stream));
@@ -322,7 +323,7 @@ int hdfs3_output_open(const hdfs3_writer_opts *opts, hdfs3_packet_sink sink, voi
         if (opts->bytes_per_checksum) s->bpc = opts->bytes_per_checksum;
         if (opts->packet_size > 0) s->packet_size = opts->packet_size;
         if (opts->block_size > 0) s->block_size = opts->block_size;
-        if (opts->batch_packets > 0) s->batch_packets = opts->batch_packets;
+        if (opts->batch_packets > 0) s->batch_packets = std::min(opts->batch_packets, kMaxBatchPackets);
     }
     // OutputStreamImpl::open checks (OutputStreamImpl.cpp:258-273)
     if (s->bpc == 0 || s->packet_size < int32_t(s->bpc) || s->block_size % s->bpc != 0) {

@@ -32,6 +32,38 @@ struct DevPacket {
     uint32_t reserved;
 };
 
+// One independent byte range of a segmented launch (a block of a batch, or one packet's
+// data region): device pointers, its whole 4 KiB rounds start at global unit unit_begin,
+// chunk c of it is reported as key_base + c (packets: packet << 32).
+struct DevSegment {
+    const uint8_t *data;
+    uint8_t *crc;            // verify: stored BE32 words; compute: written here
+    uint64_t len;
+    uint64_t unit_begin;
+    uint64_t key_base;
+};
+
+// Fills h_seg for n segments (data/crc/len/key_base already set) and returns the total
+// whole-round count; *uniform = units per segment when every segment but the last has
+// the same count (direct unit -> segment mapping), else 0 (binary search).
+uint64_t plan_segments(DevSegment *h_seg, size_t n, uint64_t *uniform);
+// True when the segmented wave kernel can take these segments: bpc in {512..4096},
+// every data pointer 16-byte aligned and every CRC pointer 4-byte aligned.
+bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc);
+// Launches over d_seg (a device copy of a planned h_seg array).
+hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,
+                           uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
+                           const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream);
+
+// Packet batch (packets API, block reader, output stream): descriptors in host memory;
+// h_stage/d_stage are pinned/device staging for n DevSegments. Uses the segmented wave
+// kernel when segments_fast() holds, else the chunk-per-lane packet kernel. Keys are
+// (packet << 32 | chunk).
+hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
+                               int check_short_tail, unsigned long long *result, DevSegment *h_stage,
+                               DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
+                               hipStream_t stream);
+
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream);
 

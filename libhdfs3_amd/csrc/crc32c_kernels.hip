@@ -22,6 +22,8 @@
 // v_perm_b32 builds a lookup address from the CRC state and a per-lane base
 // (bytes 0 and 2), and v_bitop3_b32 folds three lookups per instruction: a
 // 32-bit word costs 4 v_perm + 2 v_bitop3 + 4 ds_read_b32.
+#include <hip/hip_ext.h>
+
 #include "crc32c_kernels.h"
 #include "crc32c_tables.h"
 
@@ -727,6 +729,171 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     }
 }
 
+// ---- segmented wave kernel: independent segments (blocks of a batch, packets) ----
+//
+// The wave kernel's rounds, over the union of every segment's whole 4 KiB rounds: global
+// unit u (round-robin over waves as before) belongs to the segment with the largest
+// unit_begin <= u — u / uniform when the host found equal-sized segments, else a scalar
+// binary search over the descriptor array (wave-uniform, so SALU + scalar loads). Each
+// round's segment view is resolved when the round is prefetched and travels with its
+// buffer. Leftover chunks and short tails of every segment go to a per-segment slow pass.
+struct SegLaunch {
+    const DevSegment *seg;
+    uint32_t nseg;
+    uint64_t units;
+    uint64_t uniform;
+    unsigned long long *result;
+    int check_short_tail;
+};
+
+struct RoundView {
+    const uint8_t *p;    // round data (or the table image past the wave's last round)
+    uint8_t *crc;        // segment's CRC array
+    uint64_t chunk0;     // segment chunk index of the round's first chunk
+    uint64_t key0;       // key_base + chunk0
+};
+
+template <int BPC, bool VERIFY>
+__global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, const uint32_t *__restrict__ g_tab,
+                                                                   const uint32_t *__restrict__ g_nib) {
+    static_assert(BPC <= kRoundBytes && BPC % 64 == 0, "one-round units");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytesWave / 4];
+    constexpr int G = BPC / 64;
+    constexpr int kChunksPerUnit = kRoundBytes / BPC;
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t j = lane % G;
+    const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
+    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
+    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t K = wave < L.units ? (L.units - wave + nwaves - 1) / nwaves : 0;
+
+    auto seg_of = [&](uint64_t u) -> uint32_t {
+        if (L.uniform) {
+            const uint64_t s = u / L.uniform;
+            return uint32_t(s < L.nseg ? s : L.nseg - 1);
+        }
+        uint32_t lo = 0, hi = L.nseg - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (L.seg[mid].unit_begin <= u) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    auto view = [&](uint64_t k) -> RoundView {
+        RoundView v;
+        if (k < K) {
+            const uint64_t u = wave + k * nwaves;
+            const DevSegment *sd = L.seg + seg_of(u);
+            const uint64_t r = u - sd->unit_begin;
+            v.p = sd->data + r * kRoundBytes;
+            v.crc = sd->crc;
+            v.chunk0 = r * kChunksPerUnit;
+            v.key0 = sd->key_base + v.chunk0;
+        } else {  // unconditional prefetch target past the end (see crc32c_wave_kernel)
+            v.p = reinterpret_cast<const uint8_t *>(g_tab);
+            v.crc = nullptr;
+            v.chunk0 = 0;
+            v.key0 = 0;
+        }
+        return v;
+    };
+
+    uint32_t tv[kFillPerThread];
+    fetch_tables(tv, g_tab);
+    const u32x4 n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
+    const u32x4 n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+    RoundView rv[4] = {view(0), view(1), RoundView{}, RoundView{}};
+    __builtin_amdgcn_sched_barrier(0);
+    Round b[4];
+    load_round_buf<true>(b[0], rv[0].p, lane_off);
+    load_round_buf<true>(b[1], rv[1].p, lane_off);
+    __builtin_amdgcn_sched_barrier(0);
+    store_tables(lds, tv);
+    {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * threadIdx.x;
+        dst[0] = n0;
+        dst[1] = n1;
+    }
+    lds_barrier();
+    const Lut t(lds);
+    const NibFold nf(lds);
+    const uint32_t init = j == 0 ? 0xFFFFFFFFu : 0u;
+
+    auto want_of = [&](uint64_t k, const RoundView &v) -> uint32_t {
+        if constexpr (VERIFY) {
+            if (k >= K) return 0;
+            return *reinterpret_cast<const uint32_t *>(v.crc + 4 * (v.chunk0 + lane / G));
+        }
+        return 0;
+    };
+    auto finish = [&](uint64_t k, const RoundView &v, uint32_t y, uint32_t want) {
+        if (k >= K || j != 0) return;
+        const uint32_t c = ~y;
+        if constexpr (VERIFY) {
+            if (__builtin_bswap32(want) != c) atomicMax(L.result, ~(unsigned long long)(v.key0 + lane / G));
+        } else {
+            *reinterpret_cast<uint32_t *>(v.crc + 4 * (v.chunk0 + lane / G)) = __builtin_bswap32(c);
+        }
+    };
+    auto word = [](const Round &r, int i) -> uint32_t { return r.w[i >> 2][i & 3]; };
+
+    // step: consume rounds k, k+1 (c0, c1 with views v0, v1), prefetch k+2, k+3 into p0, p1
+    auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, const RoundView &v0, const RoundView &v1,
+                    RoundView &pv0, RoundView &pv1, uint64_t k) {
+        const uint32_t w0 = want_of(k, v0), w1 = want_of(k + 1, v1);
+        pv0 = view(k + 2);
+        pv1 = view(k + 3);
+        load_round_buf<true>(p0, pv0.p, lane_off);
+        load_round_buf<true>(p1, pv1.p, lane_off);
+        __builtin_amdgcn_sched_barrier(0);
+        regroup(c0);
+        regroup(c1);
+        uint32_t x0 = init ^ word(c0, 0), x1 = init ^ word(c1, 0);
+        Look l0 = lookups(t, x0), l1;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            l1 = lookups(t, x1);
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = combine(l0, i < 15 ? word(c0, i < 15 ? i + 1 : 15) : 0u);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i < 15) l0 = lookups(t, x0);
+            __builtin_amdgcn_sched_barrier(0);
+            x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        finish(k, v0, group_xor<G>(nf.apply(x0)), w0);
+        finish(k + 1, v1, group_xor<G>(nf.apply(x1)), w1);
+    };
+    for (uint64_t k = 0; k < K; k += 4) {
+        step(b[0], b[1], b[2], b[3], rv[0], rv[1], rv[2], rv[3], k);
+        if (k + 2 >= K) break;
+        step(b[2], b[3], b[0], b[1], rv[2], rv[3], rv[0], rv[1], k + 2);
+    }
+
+    // slow pass: per segment, the chunks after its last whole round and its short tail
+    const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
+    const uint64_t nthreads = uint64_t(gridDim.x) * kBlockThreads;
+    for (uint64_t si = gtid; si < L.nseg; si += nthreads) {
+        const DevSegment sd = L.seg[si];
+        const uint64_t nfull = sd.len / BPC;
+        const uint64_t first = (sd.len / kRoundBytes) * kChunksPerUnit;
+        const uint64_t last = nfull + (sd.len % BPC ? 1 : 0);
+        for (uint64_t c = first; c < last; ++c) {
+            const uint32_t sz = c < nfull ? uint32_t(BPC) : uint32_t(sd.len % BPC);
+            const uint32_t v = ~crc_run_any(t, 0xFFFFFFFFu, sd.data + c * BPC, sz);
+            if constexpr (VERIFY) {
+                if ((sz == uint32_t(BPC) || L.check_short_tail) && load_be32(sd.crc + 4 * c, true) != v)
+                    atomicMax(L.result, ~(unsigned long long)(sd.key_base + c));
+            } else {
+                store_be32(sd.crc + 4 * c, v, true);
+            }
+        }
+    }
+}
+
 // Packet kernel: one wave per packet (grid-stride over packets), lanes over that
 // packet's chunks. Result key = (packet << 32 | chunk), atomicMax of its complement
 // keeps the lexicographically first bad (packet, chunk).
@@ -890,7 +1057,8 @@ hipError_t launch_r3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *
     return hipGetLastError();
 }
 
-template <int BPC, bool V, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false>
+template <int BPC, bool V, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
+          bool ANY_ORDER = false>
 hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                        hipStream_t s) {
     if constexpr (BPC > kRoundBytes) {
@@ -902,8 +1070,12 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         const uint64_t units = a.len / kRoundBytes;
         const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
         const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
-        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO>), dim3(grid),
-                           dim3(kBlockThreads), 0, s, a, tab, nib);
+        if constexpr (ANY_ORDER)  // experiment (variant 16): AQL packet without the barrier bit
+            hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO>), dim3(grid),
+                                  dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+        else
+            hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO>), dim3(grid),
+                               dim3(kBlockThreads), 0, s, a, tab, nib);
         return hipGetLastError();
     }
 }
@@ -950,6 +1122,7 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
         return launch_wave<BPC, V, 2, true, true, true>(e, tab, fold, grid_cap, s);
     }
     case 14: return launch_wave<BPC, V, 2, true, true, false, true>(a, tab, fold, grid_cap, s);  // + s_setprio
+    case 16: return launch_wave<BPC, V, 2, true, true, false, false, true>(a, tab, fold, grid_cap, s);
     case 15: {  // 14 with timestamps
         if (!g_trace) return hipErrorInvalidValue;
         ChunkLaunch e = a;
@@ -1010,6 +1183,83 @@ hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_
                            stream, d_arena, const_cast<uint8_t *>(d_arena), d_pk, n, bpc, 0,
                            result, d_tables);
     return hipGetLastError();
+}
+
+uint64_t plan_segments(DevSegment *h_seg, size_t n, uint64_t *uniform) {
+    uint64_t units = 0, u0 = n ? h_seg[0].len / kRoundBytes : 0;
+    bool same = true;
+    for (size_t i = 0; i < n; ++i) {
+        h_seg[i].unit_begin = units;
+        const uint64_t u = h_seg[i].len / kRoundBytes;
+        if (i + 1 < n && u != u0) same = false;
+        units += u;
+    }
+    *uniform = same && u0 > 0 ? u0 : 0;
+    return units;
+}
+
+bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc) {
+    if (bpc != 512 && bpc != 1024 && bpc != 2048 && bpc != 4096) return false;
+    for (size_t i = 0; i < n; ++i)
+        if ((reinterpret_cast<uintptr_t>(h_seg[i].data) & 15u) || (reinterpret_cast<uintptr_t>(h_seg[i].crc) & 3u))
+            return false;
+    return true;
+}
+
+template <int BPC>
+hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *fold, int grid,
+                        hipStream_t s) {
+    constexpr int set = BPC == 512 ? 0 : BPC == 1024 ? 1 : BPC == 2048 ? 2 : 3;
+    const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
+    if (verify)
+        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, true>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
+    else
+        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
+    return hipGetLastError();
+}
+
+hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,
+                           uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
+                           const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream) {
+    if (nseg == 0) return hipSuccess;
+    const SegLaunch L{d_seg, nseg, units, uniform, result, check_short_tail};
+    const uint64_t need = (units + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock);
+    const uint64_t slow_need = (nseg + kBlockThreads - 1) / kBlockThreads;
+    uint64_t g = need > slow_need ? need : slow_need;
+    g = g < uint64_t(grid_cap) ? g : uint64_t(grid_cap);
+    const int grid = int(g > 0 ? g : 1);
+    switch (bpc) {
+    case 512: return launch_seg_t<512>(L, verify, d_tables, d_fold, grid, stream);
+    case 1024: return launch_seg_t<1024>(L, verify, d_tables, d_fold, grid, stream);
+    case 2048: return launch_seg_t<2048>(L, verify, d_tables, d_fold, grid, stream);
+    case 4096: return launch_seg_t<4096>(L, verify, d_tables, d_fold, grid, stream);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
+                               int check_short_tail, unsigned long long *result, DevSegment *h_stage,
+                               DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
+                               hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    for (size_t i = 0; i < n; ++i)
+        h_stage[i] = DevSegment{d_arena + h_pk[i].data_off, const_cast<uint8_t *>(d_arena) + h_pk[i].crc_off,
+                                h_pk[i].data_len, 0, uint64_t(i) << 32};
+    if (g_variant != 17 && segments_fast(h_stage, n, bpc)) {
+        uint64_t uniform = 0;
+        const uint64_t units = plan_segments(h_stage, n, &uniform);
+        hipError_t e = hipMemcpyAsync(d_stage, h_stage, n * sizeof(DevSegment), hipMemcpyHostToDevice, stream);
+        if (e != hipSuccess) return e;
+        return launch_segments(d_stage, uint32_t(n), units, uniform, bpc, verify, check_short_tail, result,
+                               d_tables, d_fold, grid_cap, stream);
+    }
+    // variant 17 (A/B) or unaligned / other chunk sizes: one wave per packet
+    DevPacket *hp = reinterpret_cast<DevPacket *>(h_stage);
+    for (size_t i = 0; i < n; ++i) hp[i] = h_pk[i];
+    hipError_t e = hipMemcpyAsync(d_stage, hp, n * sizeof(DevPacket), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    return launch_packets(d_arena, reinterpret_cast<const DevPacket *>(d_stage), n, bpc, verify, check_short_tail,
+                          result, d_tables, grid_cap, stream);
 }
 
 void set_variant(int v) { g_variant = v; }

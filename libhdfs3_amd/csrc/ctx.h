@@ -36,7 +36,7 @@ struct Slot {
 struct PacketArena {
     uint8_t *h = nullptr, *d = nullptr;
     size_t cap = 0;
-    DevPacket *h_desc = nullptr, *d_desc = nullptr;
+    DevSegment *h_desc = nullptr, *d_desc = nullptr;  // descriptor staging (DevSegment-sized)
     size_t desc_cap = 0;
     unsigned long long *d_res = nullptr, *h_res = nullptr;
     hipEvent_t done = nullptr;
@@ -68,9 +68,16 @@ struct hdfs3_crc_ctx {
     int checksum_type = 2;
     unsigned long long *d_result = nullptr;
     unsigned long long *h_result = nullptr;  // pinned
-    hdfs3crc::DevPacket *d_pk = nullptr;
-    hdfs3crc::DevPacket *h_pk = nullptr;               // pinned
+    hdfs3crc::DevSegment *d_pk = nullptr;              // packets-API descriptor staging
+    hdfs3crc::DevSegment *h_pk = nullptr;              // pinned
     size_t pk_cap = 0;
+    // blocks API: a ring of descriptor stagings, each reusable once its event fired
+    struct SegStage {
+        hdfs3crc::DevSegment *h = nullptr, *d = nullptr;
+        size_t cap = 0;
+        hipEvent_t done = nullptr;
+    } seg_ring[4];
+    unsigned seg_next = 0;
     hdfs3crc::Slot slot[2];
     std::atomic<uint64_t> launches{0};
     std::mutex arena_mu;                          // guards arena_cache

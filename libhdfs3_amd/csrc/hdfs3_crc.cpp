@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 #include <mutex>
 #include <new>
 
@@ -106,8 +107,8 @@ int grow_pk(hdfs3_crc_ctx *ctx, size_t n) {
     ctx->d_pk = nullptr;
     ctx->h_pk = nullptr;
     ctx->pk_cap = 0;
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&ctx->d_pk), n * sizeof(DevPacket)));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_pk), n * sizeof(DevPacket), hipHostMallocDefault));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&ctx->d_pk), n * sizeof(DevSegment)));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_pk), n * sizeof(DevSegment), hipHostMallocDefault));
     ctx->pk_cap = n;
     return 0;
 }
@@ -212,13 +213,11 @@ int packets_common(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len,
     if (int rc = grow_pk(ctx, n)) return rc;
     // the previous call's descriptors may still be in flight from h_pk
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    for (size_t i = 0; i < n; ++i)
-        ctx->h_pk[i] = DevPacket{pk[i].data_off, pk[i].crc_off, pk[i].data_len, 0};
-    HIP_TRY(hipMemcpyAsync(ctx->d_pk, ctx->h_pk, n * sizeof(DevPacket), hipMemcpyHostToDevice,
-                           ctx->stream));
+    std::vector<DevPacket> hp(n);
+    for (size_t i = 0; i < n; ++i) hp[i] = DevPacket{pk[i].data_off, pk[i].crc_off, pk[i].data_len, 0};
     if (verify) HIP_TRY(hipMemsetAsync(ctx->d_result, 0, sizeof(unsigned long long), ctx->stream));
-    HIP_TRY(launch_packets(d_arena, ctx->d_pk, n, bpc, verify, check_short_tail, ctx->d_result,
-                           ctx->d_tables, ctx->grid_cap, ctx->stream));
+    HIP_TRY(launch_packet_batch(d_arena, hp.data(), n, bpc, verify, check_short_tail, ctx->d_result, ctx->h_pk,
+                                ctx->d_pk, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
     ++ctx->launches;
     if (verify) {
         HIP_TRY(hipMemcpyAsync(ctx->h_result, ctx->d_result, sizeof(unsigned long long),
@@ -234,9 +233,105 @@ int packets_common(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len,
     return 0;
 }
 
+// a descriptor staging slot of the blocks API, reusable once its previous launch ran
+int stage_segments(hdfs3_crc_ctx *ctx, size_t n, hdfs3_crc_ctx::SegStage **out) {
+    hdfs3_crc_ctx::SegStage &st = ctx->seg_ring[ctx->seg_next++ & 3u];
+    if (st.done) HIP_TRY(hipEventSynchronize(st.done));
+    if (n > st.cap) {
+        if (st.h) (void)hipHostFree(st.h);
+        if (st.d) (void)hipFree(st.d);
+        st.h = st.d = nullptr;
+        st.cap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&st.h), n * sizeof(DevSegment), hipHostMallocDefault));
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&st.d), n * sizeof(DevSegment)));
+        st.cap = n;
+    }
+    if (!st.done) HIP_TRY(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
+    *out = &st;
+    return 0;
+}
+
+int blocks_common(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, uint32_t bpc, bool verify,
+                  int check_short_tail, unsigned long long *d_result) {
+    if (n > (size_t(1) << 31)) return fail(-EINVAL, "too many blocks in one batch");
+    for (size_t i = 0; i < n; ++i) {
+        if (blocks[i].len && (!blocks[i].data || !blocks[i].crc_be)) return fail(-EINVAL, "block %zu: null buffer", i);
+        if ((blocks[i].len + bpc - 1) / bpc >= (uint64_t(1) << 32))
+            return fail(-EINVAL, "block %zu: 2^32 chunks or more", i);
+    }
+    hdfs3_crc_ctx::SegStage *st = nullptr;
+    if (int rc = stage_segments(ctx, n, &st)) return rc;
+    for (size_t i = 0; i < n; ++i)
+        st->h[i] = DevSegment{static_cast<const uint8_t *>(blocks[i].data), static_cast<uint8_t *>(blocks[i].crc_be),
+                              blocks[i].len, 0, uint64_t(i) << 32};
+    if (segments_fast(st->h, n, bpc)) {
+        uint64_t uniform = 0;
+        const uint64_t units = plan_segments(st->h, n, &uniform);
+        HIP_TRY(hipMemcpyAsync(st->d, st->h, n * sizeof(DevSegment), hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(launch_segments(st->d, uint32_t(n), units, uniform, bpc, verify, check_short_tail, d_result,
+                                ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
+        ++ctx->launches;
+    } else {  // other chunk sizes or unaligned buffers: one launch per block, same keys
+        for (size_t i = 0; i < n; ++i) {
+            if (!blocks[i].len) continue;
+            ChunkLaunch a{};
+            a.data = st->h[i].data;
+            a.len = blocks[i].len;
+            a.bpc = bpc;
+            a.crc_be = st->h[i].crc;
+            a.out_be = st->h[i].crc;
+            a.result = d_result;
+            a.chunk_base = uint64_t(i) << 32;
+            a.check_short_tail = check_short_tail;
+            if (int rc = launch(ctx, a, verify)) return rc;
+        }
+    }
+    HIP_TRY(hipEventRecord(st->done, ctx->stream));
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+int hdfs3_crc32c_verify_blocks_dev_async(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n,
+                                         uint32_t bpc, int check_short_tail, uint64_t *d_result) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (n == 0) return 0;
+    if (!blocks || !d_result) return fail(-EINVAL, "null argument");
+    DeviceGuard g(ctx->device);
+    return blocks_common(ctx, blocks, n, bpc, true, check_short_tail, reinterpret_cast<unsigned long long *>(d_result));
+}
+
+int hdfs3_crc32c_verify_blocks_dev(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, uint32_t bpc,
+                                   int check_short_tail, int64_t *bad_block, int64_t *bad_chunk) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (bad_block) *bad_block = -1;
+    if (bad_chunk) *bad_chunk = -1;
+    if (n == 0) return 0;
+    if (!blocks) return fail(-EINVAL, "null argument");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipMemsetAsync(ctx->d_result, 0, sizeof(unsigned long long), ctx->stream));
+    if (int rc = blocks_common(ctx, blocks, n, bpc, true, check_short_tail, ctx->d_result)) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->h_result, ctx->d_result, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const unsigned long long r = *ctx->h_result;
+    if (r) {
+        const uint64_t key = ~r;
+        if (bad_block) *bad_block = int64_t(key >> 32);
+        if (bad_chunk) *bad_chunk = int64_t(key & 0xFFFFFFFFu);
+    }
+    return 0;
+}
+
+int hdfs3_crc32c_compute_blocks_dev(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, uint32_t bpc) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (n == 0) return 0;
+    if (!blocks) return fail(-EINVAL, "null argument");
+    DeviceGuard g(ctx->device);
+    return blocks_common(ctx, blocks, n, bpc, false, 0, nullptr);
+}
 
 int hdfs3_crc_abi_version(void) { return HDFS3_CRC_ABI_VERSION; }
 
@@ -320,6 +415,11 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx) {
     }
     for (PacketArena &a : ctx->arena_cache) a.release();
     ctx->arena_cache.clear();
+    for (auto &st : ctx->seg_ring) {
+        if (st.h) (void)hipHostFree(st.h);
+        if (st.d) (void)hipFree(st.d);
+        if (st.done) (void)hipEventDestroy(st.done);
+    }
     if (ctx->d_pk) (void)hipFree(ctx->d_pk);
     if (ctx->h_pk) (void)hipHostFree(ctx->h_pk);
     for (int p = 0; p < 2; ++p) {

@@ -98,13 +98,17 @@ class CrcContext:
     def synchronize(self) -> None:
         check("hdfs3_crc_ctx_synchronize", self._lib.hdfs3_crc_ctx_synchronize(self.ctx))
 
-    def upload(self, host: np.ndarray, dev: DeviceBuffer | None = None, offset: int = 0) -> DeviceBuffer:
+    def upload(self, host: np.ndarray, dev: DeviceBuffer | int | None = None, offset: int = 0):
+        """Copy host bytes to a DeviceBuffer (bounds-checked) or a raw device address."""
         host = np.ascontiguousarray(host)
         if dev is None:
             dev = DeviceBuffer(host.nbytes)
-        assert offset + host.nbytes <= dev.nbytes
-        check("hdfs3_memcpy_h2d",
-              self._lib.hdfs3_memcpy_h2d(self.ctx, dev.ptr + offset, _ptr(host), host.nbytes))
+        if isinstance(dev, DeviceBuffer):
+            assert offset + host.nbytes <= dev.nbytes
+            base = dev.ptr
+        else:
+            base = int(dev)
+        check("hdfs3_memcpy_h2d", self._lib.hdfs3_memcpy_h2d(self.ctx, base + offset, _ptr(host), host.nbytes))
         return dev
 
     def download(self, dev: DeviceBuffer | int, nbytes: int, offset: int = 0) -> np.ndarray:
@@ -155,6 +159,31 @@ class CrcContext:
 
     def decode_result(self, word: int) -> int:
         return int(self._lib.hdfs3_crc_decode_result(word))
+
+    # -- batch of device-resident blocks ------------------------------------------------
+    @staticmethod
+    def _blocks(blocks) -> ctypes.Array:
+        arr = (_native.DevBlock * max(1, len(blocks)))()
+        for i, (d, c, n) in enumerate(blocks):
+            arr[i].data, arr[i].crc_be, arr[i].len = d, c, n
+        return arr
+
+    def verify_blocks_dev(self, blocks, bpc: int, check_short_tail: bool = False):
+        """blocks = [(d_data, d_crc, len)] -> first bad (block, chunk) or (-1, -1)."""
+        bb, bc = c_int64(-2), c_int64(-2)
+        check("hdfs3_crc32c_verify_blocks_dev",
+              self._lib.hdfs3_crc32c_verify_blocks_dev(self.ctx, self._blocks(blocks), len(blocks), bpc,
+                                                       int(check_short_tail), byref(bb), byref(bc)))
+        return bb.value, bc.value
+
+    def verify_blocks_dev_async(self, blocks, bpc: int, d_result: int, check_short_tail: bool = False) -> None:
+        check("hdfs3_crc32c_verify_blocks_dev_async",
+              self._lib.hdfs3_crc32c_verify_blocks_dev_async(self.ctx, self._blocks(blocks), len(blocks), bpc,
+                                                             int(check_short_tail), d_result))
+
+    def compute_blocks_dev(self, blocks, bpc: int) -> None:
+        check("hdfs3_crc32c_compute_blocks_dev",
+              self._lib.hdfs3_crc32c_compute_blocks_dev(self.ctx, self._blocks(blocks), len(blocks), bpc))
 
     # -- packet-stream API ------------------------------------------------------------
     @staticmethod

@@ -137,3 +137,54 @@ class Conn:
 
     def close(self):
         self.s.close()
+
+
+def serve_once(script):
+    """Test helper: a one-connection fake datanode on 127.0.0.1. After reading the client's
+    OP_READ_BLOCK request it sends the bytes `script(request_fields)` returns, then keeps
+    the socket open until the client goes away. Returns (port, thread)."""
+    import threading
+
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    port = srv.getsockname()[1]
+
+    def run():
+        c, _ = srv.accept()
+        try:
+            c.settimeout(10)
+            hdr = b""
+            while len(hdr) < 3:
+                hdr += c.recv(3 - len(hdr))
+            n = shift = 0
+            while True:
+                b = c.recv(1)[0]
+                n |= (b & 0x7F) << shift
+                shift += 7
+                if not b & 0x80:
+                    break
+            body = b""
+            while len(body) < n:
+                body += c.recv(n - len(body))
+            c.sendall(script(parse(body)))
+            try:
+                while c.recv(65536):
+                    pass
+            except OSError:
+                pass
+        finally:
+            c.close()
+            srv.close()
+
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    return port, t
+
+
+def block_op_response(bpc: int = 512, ctype: int = 2, chunk_offset: int = 0, status: int = 0) -> bytes:
+    """BlockOpResponseProto{status, readOpChecksumInfo{checksum{type, bpc}, chunkOffset}}, delimited."""
+    cs = field_varint(1, ctype) + field_varint(2, bpc)
+    info = field_bytes(1, cs) + field_varint(2, chunk_offset)
+    msg = field_varint(1, status) + field_bytes(4, info)
+    return varint(len(msg)) + msg

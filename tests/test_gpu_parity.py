@@ -220,7 +220,7 @@ def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
             assert gpu_ctx.verify(bad, 512, crc, True) == 3
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 14])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 14, 16])
 @pytest.mark.parametrize("bpc", [512, 1024, 2048, 4096, 8192])
 def test_every_kernel_variant_matches_oracle(gpu_ctx, variant, bpc):
     """All kernel designs kept for A/B (hdfs3x_set_variant) are parity-checked too:

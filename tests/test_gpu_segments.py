@@ -1,0 +1,147 @@
+"""GPU parity of the segmented wave kernel: the multi-block batch API
+(hdfs3_crc32c_{verify,compute}_blocks_dev*) and the packet API's fast path. Every block of
+a batch must get exactly the words and first-bad chunk it gets alone (oracle per block);
+the packet path must agree with the chunk-per-lane packet kernel (variant 17) and the
+oracle, including short tails (remote vs local semantics) and odd sizes."""
+import numpy as np
+import pytest
+
+from util import oracle_compute, splitmix_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+def make_blocks(ctx, sizes, bpc, seed, pad=0):
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    blocks, keep, datas = [], [], []
+    for i, n in enumerate(sizes):
+        d = splitmix_bytes(n, seed + i)
+        db = DeviceBuffer(n + pad + 16)
+        if n:
+            ctx.upload(d, db, offset=pad)
+        cb = DeviceBuffer(4 * ((n + bpc - 1) // bpc) + 8)
+        blocks.append((db.ptr + pad, cb.ptr, n))
+        keep += [db, cb]
+        datas.append(d)
+    return blocks, keep, datas
+
+
+@pytest.mark.parametrize("bpc", [512, 1024, 2048, 4096])
+@pytest.mark.parametrize("sizes", [
+    [1 << 20] * 8,                                     # uniform: direct unit -> segment map
+    [4096 * 5 + 700, 0, 300, 1 << 20, 4096, 8192 + 1],  # ragged: binary search, slow pass, empty
+    [65536] * 37 + [1000],                              # packet-like
+])
+def test_blocks_batch_matches_per_block_oracle(gpu_ctx, bpc, sizes):
+    blocks, keep, datas = make_blocks(gpu_ctx, sizes, bpc, bpc * 13 + len(sizes))
+    gpu_ctx.compute_blocks_dev(blocks, bpc)
+    for (d, c, n), data in zip(blocks, datas):
+        want = oracle_compute(data, bpc)
+        assert np.array_equal(gpu_ctx.download(c, want.nbytes), want), (bpc, n)
+    assert gpu_ctx.verify_blocks_dev(blocks, bpc, True) == (-1, -1)
+    # corrupt two blocks: the lexicographically first (block, chunk) is reported
+    nz = [i for i, n in enumerate(sizes) if n >= bpc]
+    hit = [nz[-1], nz[len(nz) // 2]]
+    for bi in hit:
+        d, c, n = blocks[bi]
+        pos = (n // bpc - 1) * bpc + 5
+        gpu_ctx.upload(np.array([datas[bi][pos] ^ 1], np.uint8), d, offset=pos)
+    first = min(hit)
+    assert gpu_ctx.verify_blocks_dev(blocks, bpc) == (first, sizes[first] // bpc - 1)
+
+
+def test_short_tail_semantics_and_async(gpu_ctx):
+    import ctypes
+
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    bpc = 512
+    sizes = [4096 * 3 + 100, 8192, 4096 * 2 + 512 + 33]
+    blocks, keep, datas = make_blocks(gpu_ctx, sizes, bpc, 77)
+    gpu_ctx.compute_blocks_dev(blocks, bpc)
+    d, c, n = blocks[2]
+    tail = n - 10  # inside block 2's short tail
+    gpu_ctx.upload(np.array([datas[2][tail] ^ 1], np.uint8), d, offset=tail)
+    assert gpu_ctx.verify_blocks_dev(blocks, bpc, check_short_tail=False) == (-1, -1)
+    assert gpu_ctx.verify_blocks_dev(blocks, bpc, check_short_tail=True) == (2, n // bpc)
+    res = DeviceBuffer(8)
+    gpu_ctx.memset(res, 0, 8)
+    gpu_ctx.verify_blocks_dev_async(blocks, bpc, res.ptr, check_short_tail=True)
+    gpu_ctx.synchronize()
+    word = int(gpu_ctx.download(res, 8).view(np.uint64)[0])
+    key = gpu_ctx.decode_result(word)
+    assert (key >> 32, key & 0xFFFFFFFF) == (2, n // bpc)
+
+
+def test_unaligned_and_odd_bpc_fall_back_with_same_keys(gpu_ctx):
+    for bpc, pad in [(512, 3), (100, 0)]:
+        sizes = [5000, 64 * 1024 + 7, 1234]
+        blocks, keep, datas = make_blocks(gpu_ctx, sizes, bpc, 900 + bpc, pad=pad)
+        gpu_ctx.compute_blocks_dev(blocks, bpc)
+        for (d, c, n), data in zip(blocks, datas):
+            want = oracle_compute(data, bpc)
+            assert np.array_equal(gpu_ctx.download(c, want.nbytes), want), (bpc, pad, n)
+        d, c, n = blocks[1]
+        gpu_ctx.upload(np.array([datas[1][777] ^ 4], np.uint8), d, offset=777)
+        assert gpu_ctx.verify_blocks_dev(blocks, bpc) == (1, 777 // bpc)
+
+
+def test_many_small_blocks_binary_search(gpu_ctx):
+    rng = np.random.default_rng(5)
+    sizes = [int(x) for x in rng.integers(0, 40000, size=300)]
+    blocks, keep, datas = make_blocks(gpu_ctx, sizes, 512, 4242)
+    gpu_ctx.compute_blocks_dev(blocks, 512)
+    for (d, c, n), data in zip(blocks[::17], datas[::17]):
+        want = oracle_compute(data, 512)
+        assert np.array_equal(gpu_ctx.download(c, want.nbytes), want)
+    assert gpu_ctx.verify_blocks_dev(blocks, 512, True) == (-1, -1)
+
+
+@pytest.mark.parametrize("bpc", [512, 4096])
+def test_packet_fast_path_agrees_with_packet_kernel(gpu_ctx, bpc):
+    from libhdfs3_amd import _native
+
+    lib = _native.lib()
+    rng = np.random.default_rng(bpc)
+    pk, parts, off = [], [], 0
+    lens = [65536] * 40 + [65536 - 100, 777, 4096, 20000, 65536]
+    for i, n in enumerate(lens):
+        data = splitmix_bytes(n, 3000 + i)
+        crc = oracle_compute(data, bpc)
+        pad = (-(off + crc.nbytes)) % 16
+        parts += [np.zeros(pad, np.uint8), crc, data]
+        pk.append((off + pad + crc.nbytes, off + pad, n))
+        off += pad + crc.nbytes + n
+    arena = np.concatenate(parts)
+    d = gpu_ctx.upload(arena)
+    try:
+        for v in (0, 17):
+            lib.hdfs3x_set_variant(v)
+            assert gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc) == (-1, -1)
+        for trial in range(4):
+            bad = arena.copy()
+            p = int(rng.integers(0, len(pk)))
+            q = int(rng.integers(0, pk[p][2]))
+            bad[pk[p][0] + q] ^= 0x80
+            gpu_ctx.upload(bad, d)
+            got = []
+            for v in (0, 17):
+                lib.hdfs3x_set_variant(v)
+                got.append((gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc),
+                            gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True)))
+            assert got[0] == got[1], (p, q, got)
+            chunk = q // bpc
+            short = pk[p][2] % bpc and chunk == pk[p][2] // bpc
+            assert got[0][1] == (p, chunk)
+            assert got[0][0] == ((-1, -1) if short else (p, chunk))
+        # compute through the fast path writes the same words
+        lib.hdfs3x_set_variant(0)
+        blank = arena.copy()
+        for data_off, crc_off, n in pk:
+            blank[crc_off:crc_off + 4 * ((n + bpc - 1) // bpc)] = 0
+        gpu_ctx.upload(blank, d)
+        gpu_ctx.compute_packets_dev(d.ptr, arena.nbytes, pk, bpc)
+        assert np.array_equal(gpu_ctx.download(d, arena.nbytes), arena)
+    finally:
+        lib.hdfs3x_set_variant(0)
