@@ -293,13 +293,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL for the timing barrier/all-reduce on a GPU node; HDFS3_BENCH_BACKEND=gloo lets
+    # a 1-GPU box rehearse N ranks (device = LOCAL_RANK mod visible GPUs, identity on 8)
+    backend = os.environ.get("HDFS3_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+        dist.init_process_group(backend, init_method="env://")
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local % ndev)
+    device = torch.device("cuda", local % ndev)
+    coll_device = device if backend == "nccl" else torch.device("cpu")
 
     from libhdfs3_amd.engine import CrcContext
-    ctx = CrcContext(local)
+    ctx = CrcContext(local % ndev)
     # One explicit stream for the kernels and the HIP events that time them (the
     # default stream's handle is 0, which the C-ABI reads as "use the ctx stream").
     stream = torch.cuda.Stream(device=device)
@@ -331,7 +336,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        elapsed = max_over_ranks(dist, elapsed, device)
+        elapsed = max_over_ranks(dist, elapsed, coll_device)
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the timed region")
     # (2) roofline pass: the same K launches, each bracketed by HIP events on the launch
