@@ -378,7 +378,7 @@ class OutputStream:
     packet in seqno order (PipelineImpl::send); by default packets are collected in .packets."""
 
     def __init__(self, *, device: int = 0, bytes_per_checksum: int = 512, packet_size: int = 65536,
-                 block_size: int = 64 << 20, batch_packets: int = 64, sink=None):
+                 block_size: int = 64 << 20, batch_packets: int = 64, sink=None, raw_sink=None, raw_user=None):
         self._lib = _native.lib()
         self.packets: list[tuple[bytes, dict]] = []
         user_sink = sink
@@ -393,10 +393,11 @@ class OutputStream:
             self.packets.append((b, d))
             return 0
 
-        self._cb = _native.PACKET_SINK(_sink)  # kept alive for the stream's lifetime
+        # a C sink (raw_sink: ctypes function pointer, raw_user: void*) skips the Python callback
+        self._cb = _native.PACKET_SINK(_sink) if raw_sink is None else ctypes.cast(raw_sink, _native.PACKET_SINK)
         opts = _native.WriterOpts(device, bytes_per_checksum, packet_size, block_size, batch_packets)
         p = c_void_p()
-        check("hdfs3_output_open", self._lib.hdfs3_output_open(byref(opts), self._cb, None, byref(p)))
+        check("hdfs3_output_open", self._lib.hdfs3_output_open(byref(opts), self._cb, raw_user, byref(p)))
         self.s = p.value
 
     def _posix(self, fn: str, rc: int) -> int:

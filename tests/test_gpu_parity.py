@@ -247,3 +247,49 @@ def test_every_kernel_variant_matches_oracle(gpu_ctx, variant, bpc):
                 gpu_ctx.upload(data[pos:pos + 1], d, offset=pos)
     finally:
         lib.hdfs3x_set_variant(0)
+
+
+def test_beyond_4gib_single_call_64bit_addressing(gpu_ctx):
+    """Maximum sizes: one verify over 4.5 GiB (the reference's Checksum::update takes an int,
+    so its callers never exceed 2 GiB per call; the batch API takes size_t). Distinct data
+    everywhere (aliasing past 4 GiB would read different bytes); words around the 4 GiB mark
+    are checked against the oracle and bit flips past it are located exactly. Uses only the
+    C-ABI: torch bundles its own HIP runtime, so it is not mixed in after ours."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    bpc, piece = 512, 256 << 20
+    n = (9 << 29) + 3 * bpc + 100  # 4.5 GiB + ragged tail
+    dbuf = DeviceBuffer(n)
+    host = {}
+    for i, off in enumerate(range(0, n, piece)):
+        part = splitmix_bytes(min(piece, n - off), 0xB16B00B5 + i)
+        gpu_ctx.upload(part, dbuf, offset=off)
+        host[off] = part
+
+    def host_bytes(start, length):
+        out = np.empty(length, np.uint8)
+        pos = 0
+        while pos < length:
+            off = (start + pos) // piece * piece
+            k = start + pos - off
+            take = min(length - pos, host[off].nbytes - k)
+            out[pos:pos + take] = host[off][k:k + take]
+            pos += take
+        return out
+
+    nch = (n + bpc - 1) // bpc
+    crc = DeviceBuffer(4 * nch)
+    gpu_ctx.compute_dev(dbuf.ptr, n, bpc, crc.ptr)
+    assert gpu_ctx.verify_dev(dbuf.ptr, n, bpc, crc.ptr, True) == -1
+    for start in (0, (1 << 32) - 8192, (1 << 32) + 4096 * 7, n - n % bpc - 8 * bpc):
+        start -= start % bpc
+        length = min(20 * bpc, n - start)
+        want = oracle_compute(host_bytes(start, length), bpc)
+        got = gpu_ctx.download(crc, want.nbytes, offset=4 * (start // bpc))
+        assert np.array_equal(got, want), start
+    for pos in ((1 << 32) + 12345, n - 50):
+        orig = host_bytes(pos, 1)
+        gpu_ctx.upload(orig ^ 1, dbuf, offset=pos)
+        assert gpu_ctx.verify_dev(dbuf.ptr, n, bpc, crc.ptr, True) == pos // bpc
+        gpu_ctx.upload(orig, dbuf, offset=pos)
+    dbuf.free()

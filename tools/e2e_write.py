@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Write path, PCIe-inclusive: hdfsWrite (hdfs3_output_write) of a 1 GiB
+host buffer in 1 MiB writes, 128 MiB blocks, 512 B chunks — user bytes copied into pinned
+packet arenas, H2D, GPU compute of every chunk's CRC, D2H of the words, packets assembled
+and handed to a C sink that reads every packet byte (a stand-in for the pipeline socket).
+Batch sizes are swept; the model check (tests/test_output_stream.py) covers correctness.
+Reports GiB/s of user data. Never bench `value`."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main():
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import OutputStream
+
+    lb = _native.loopback()
+    sink = ctypes.cast(lb.hdfs3_loopback_count_sink, ctypes.c_void_p).value
+    total = 1 << 30
+    data = np.random.default_rng(1).integers(0, 256, size=total, dtype=np.uint8)
+    for batch in (16, 64, 256):
+        best = 0.0
+        for rep in range(3):
+            counts = (ctypes.c_uint64 * 3)()
+            with OutputStream(block_size=128 << 20, batch_packets=batch, raw_sink=sink,
+                              raw_user=ctypes.addressof(counts)) as s:
+                t0 = time.perf_counter()
+                for off in range(0, total, 1 << 20):
+                    s.write(data[off:off + (1 << 20)])
+                s.close()
+                dt = time.perf_counter() - t0
+            best = max(best, total / dt / 2**30)
+            # every block: ceil(chunks / 127) data packets + its empty last packet
+            blocks, per_block = total // (128 << 20), (128 << 20) // 512
+            assert counts[0] == blocks * (-(-per_block // 127) + 1), counts[0]
+        print(json.dumps({"bench": "e2e_write", "mode": "hdfsWrite", "bytes": total, "bpc": 512,
+                          "batch_packets": batch, "packets": int(counts[0]), "wire_bytes": int(counts[1]),
+                          "gib_s": round(best, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

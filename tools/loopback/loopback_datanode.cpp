@@ -261,6 +261,21 @@ int hdfs3_loopback_last_status(int port) {
     return sv ? sv->last_status.load() : -1;
 }
 
+/* Test/bench packet sink for hdfs3_output_open: counts packets and bytes into
+ * user = uint64_t[3] {packets, wire bytes, data bytes} and touches every byte (a stand-in
+ * for the socket write of PipelineImpl::send). */
+int hdfs3_loopback_count_sink(void *user, const void *pkt, size_t len, const void *info) {
+    (void)info;
+    uint64_t *c = static_cast<uint64_t *>(user);
+    const uint8_t *p = static_cast<const uint8_t *>(pkt);
+    uint64_t x = 0;
+    for (size_t i = 0; i < len; i += 64) x += p[i];
+    c[0] += 1;
+    c[1] += len;
+    c[2] += x & 1;  // keeps the loop
+    return 0;
+}
+
 int hdfs3_loopback_stop(int port) {
     Server *sv = nullptr;
     {
