@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--sweep", action="store_true", help="extra diagnostics on stderr")
+    p.add_argument("--no-graph", action="store_true",
+                   help="launch the K steps eagerly instead of replaying captured HIP graphs")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -131,18 +133,19 @@ def check_against_oracle(work, ctx):
         raise SystemExit("PARITY FAILURE: clean block reported bad")
 
 
-def run_steps(work, ctx, mode, n, result, events=None):
-    for s in range(n):
+def run_steps(work, ctx, mode, n, result, events=None, base=0):
+    for i in range(n):
+        s = base + i
         b = s % work.blocks
         if events is not None:
-            events[2 * s].record()
+            events[2 * i].record()
         if mode == "verify":
             ctx.verify_dev_async(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b),
                                  result.data_ptr() + 8 * (s % result.numel()))
         else:
             ctx.compute_dev(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b))
         if events is not None:
-            events[2 * s + 1].record()
+            events[2 * i + 1].record()
 
 
 def batched_rate(torch, work, ctx, mode, reps=20):
@@ -178,6 +181,34 @@ def batched_rate(torch, work, ctx, mode, reps=20):
             "blocks_per_launch": work.blocks, "value": round(nbytes / t / 2**30, 2), "unit": "GiB/s",
             "avg_launch_us": round(t * 1e6, 2), "achieved_GBps": round(alg / t / 1e9, 1),
             "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}
+
+
+class StepGraphs:
+    """The timed K steps as replays of captured HIP graphs (torch.cuda.graph on the launch
+    stream; the library shares torch's HIP runtime). Graph i holds `per` consecutive steps
+    with exactly the eager loop's block rotation and result slots; a shorter graph covers
+    K % per. Each step is still one launch verifying one whole block — the graph only
+    removes per-launch CPU submission and shrinks the dispatch gap."""
+
+    def __init__(self, torch, work, ctx, mode, K, result, stream, per=64):
+        self.torch = torch
+        self.per = min(per, K)
+        self.full, rem = divmod(K, self.per)
+        self.graphs = []
+        for n, base in [(self.per, 0)] + ([(rem, self.full * self.per)] if rem else []):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                run_steps(work, ctx, mode, n, result, base=base)
+            self.graphs.append(g)
+        for g in self.graphs:  # first replay uploads/instantiates the graph: keep it untimed
+            g.replay()
+        torch.cuda.synchronize()
+
+    def run(self):
+        for _ in range(self.full):
+            self.graphs[0].replay()
+        if len(self.graphs) > 1:
+            self.graphs[1].replay()
 
 
 def stream_read_ceiling(torch, work, ctx, reps=10):
@@ -325,22 +356,32 @@ def main():
     K, W = args.steps, args.warmup
     result = torch.zeros(max(K, W, 1), dtype=torch.int64, device=device)
     run_steps(work, ctx, args.mode, W, result)
+    graphs = None if args.no_graph else StepGraphs(torch, work, ctx, args.mode, K, result, stream)
     result.zero_()
-    # (1) timed region for `value`: K back-to-back launches, nothing else on the stream
+    torch.cuda.synchronize()
+    # (1) timed region for `value`: K steps (graph replays, or K eager launches), nothing
+    # else on the stream; HIP events on the launch stream bracket the same region
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_steps(work, ctx, args.mode, K, result)
+    ev0.record(stream)
+    if graphs is not None:
+        graphs.run()
+    else:
+        run_steps(work, ctx, args.mode, K, result)
+    ev1.record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    region_launch_s = ev0.elapsed_time(ev1) * 1e-3 / K
     if world > 1:
         dist.barrier()
         elapsed = max_over_ranks(dist, elapsed, coll_device)
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the timed region")
-    # (2) roofline pass: the same K launches, each bracketed by HIP events on the launch
-    # stream -> the kernel's average launch duration
+    # (2) diagnostic pass: the same K launches eagerly, each bracketed by HIP events on the
+    # launch stream (per-launch duration including dispatch, without graph batching)
     events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
     result.zero_()
     run_steps(work, ctx, args.mode, K, result, events)
@@ -349,7 +390,8 @@ def main():
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the roofline pass")
 
     launch_ms = [events[2 * s].elapsed_time(events[2 * s + 1]) for s in range(K)]
-    avg_launch_s = sum(launch_ms) / K * 1e-3
+    eager_launch_s = sum(launch_ms) / K * 1e-3
+    avg_launch_s = region_launch_s
     payload = block_bytes
     alg_bytes = work.nchunks * (args.bpc + 4)  # verify reads data + CRC; compute reads data, writes CRC
     value = aggregate_rate(payload * K, world, elapsed)
@@ -363,7 +405,9 @@ def main():
     achieved = alg_bytes / avg_launch_s / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                "alg_bytes_per_launch": alg_bytes, "avg_launch_us": round(avg_launch_s * 1e6, 2)}
+                "alg_bytes_per_launch": alg_bytes, "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                "timing": "HIP events on the launch stream over the timed region / K",
+                "eager_per_launch_us": round(eager_launch_s * 1e6, 2)}
     extra = {}
     if world == 1:
         try:
@@ -390,6 +434,7 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": K,
         "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True,
+        "launch": "eager" if graphs is None else f"HIP graph replay, {graphs.per} single-block launches per graph",
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (torch.randint bytes)",
         "config": {"workload": f"{args.mode} of one {args.block_mib} MiB HDFS block per step, "
                                f"{args.bpc} B chunks, device-resident (BASELINE.json configs[1])",

@@ -50,10 +50,13 @@ uint64_t plan_segments(DevSegment *h_seg, size_t n, uint64_t *uniform);
 // True when the segmented wave kernel can take these segments: bpc in {512..4096},
 // every data pointer 16-byte aligned and every CRC pointer 4-byte aligned.
 bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc);
-// Launches over d_seg (a device copy of a planned h_seg array).
+// Launches over d_seg (a device copy of a planned h_seg array), or, with h_inline and
+// nseg <= 16, over descriptors carried in the kernel arguments (no copy before the kernel).
 hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,
                            uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
-                           const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream);
+                           const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream,
+                           const DevSegment *h_inline = nullptr);
+constexpr uint32_t kMaxInlineSegments = 16;
 
 // Packet batch (packets API, block reader, output stream): descriptors in host memory;
 // h_stage/d_stage are pinned/device staging for n DevSegments. Uses the segmented wave

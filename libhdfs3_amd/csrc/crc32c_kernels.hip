@@ -737,13 +737,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
 // binary search over the descriptor array (wave-uniform, so SALU + scalar loads). Each
 // round's segment view is resolved when the round is prefetched and travels with its
 // buffer. Leftover chunks and short tails of every segment go to a per-segment slow pass.
+constexpr uint32_t kInlineSegments = 16;  // small lists travel in the kernel arguments
+
 struct SegLaunch {
-    const DevSegment *seg;
+    const DevSegment *seg;  // device array, or nullptr: use inl[] (nseg <= kInlineSegments)
     uint32_t nseg;
     uint64_t units;
     uint64_t uniform;
     unsigned long long *result;
     int check_short_tail;
+    DevSegment inl[kInlineSegments];
 };
 
 struct RoundView {
@@ -753,7 +756,10 @@ struct RoundView {
     uint64_t key0;       // key_base + chunk0
 };
 
-template <int BPC, bool VERIFY>
+// UNI: every segment but the last has L.uniform units -> the segment is a 32-bit divide;
+// otherwise a binary search. They are separate instantiations on purpose: a search loop in
+// the hot loop's CFG (even untaken) makes the waitcnt pass drain the prefetch each step.
+template <int BPC, bool VERIFY, bool UNI>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, const uint32_t *__restrict__ g_tab,
                                                                    const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 64 == 0, "one-round units");
@@ -768,32 +774,53 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
     const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t K = wave < L.units ? (L.units - wave + nwaves - 1) / nwaves : 0;
 
+    // kernel-argument (inline) descriptors when the host passed no device array
+    auto segp = [&](uint32_t i) -> const DevSegment * { return L.seg ? L.seg + i : L.inl + i; };
+    static_assert(sizeof(DevSegment) == 40, "descriptor layout");
     auto seg_of = [&](uint64_t u) -> uint32_t {
-        if (L.uniform) {
-            const uint64_t s = u / L.uniform;
-            return uint32_t(s < L.nseg ? s : L.nseg - 1);
+        if constexpr (UNI) {  // unit counts stay < 2^32 (16 TiB per launch): 32-bit divide
+            const uint32_t s = uint32_t(u) / uint32_t(L.uniform);
+            return s < L.nseg ? s : L.nseg - 1;
+        } else {
+            uint32_t lo = 0, hi = L.nseg - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                const uint64_t ub = segp(mid)->unit_begin;
+                if (ub <= u) lo = mid;
+                else hi = mid - 1;
+            }
+            return lo;
         }
-        uint32_t lo = 0, hi = L.nseg - 1;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (L.seg[mid].unit_begin <= u) lo = mid;
-            else hi = mid - 1;
-        }
-        return lo;
     };
+    // The prefetch stream's current segment, cached in scalar registers: a round inside it
+    // needs only arithmetic; crossing into another segment costs one lookup (32-bit divide
+    // or binary search) and the descriptor's scalar loads. Keeping those loads off the
+    // common path matters: SMEM shares lgkmcnt with the LDS lookups and returns out of
+    // order, so any in flight turns the pipelined lookup waits into lgkmcnt(0).
+    uint64_t c_begin = 1, c_end = 0, c_key = 0;
+    const uint8_t *c_data = nullptr;
+    uint8_t *c_crc = nullptr;
     auto view = [&](uint64_t k) -> RoundView {
         RoundView v;
         if (k < K) {
             const uint64_t u = wave + k * nwaves;
-            const DevSegment *sd = L.seg + seg_of(u);
-            const uint64_t r = u - sd->unit_begin;
-            v.p = sd->data + r * kRoundBytes;
-            v.crc = sd->crc;
+            if (u < c_begin || u >= c_end) {
+                const DevSegment *sd = segp(seg_of(u));
+                c_begin = sd->unit_begin;
+                c_end = sd->unit_begin + sd->len / kRoundBytes;
+                c_data = sd->data;
+                c_crc = sd->crc;
+                c_key = sd->key_base;
+            }
+            const uint64_t r = u - c_begin;
+            v.p = c_data + r * kRoundBytes;
+            v.crc = c_crc;
             v.chunk0 = r * kChunksPerUnit;
-            v.key0 = sd->key_base + v.chunk0;
-        } else {  // unconditional prefetch target past the end (see crc32c_wave_kernel)
+            v.key0 = c_key + v.chunk0;
+        } else {  // past the wave's last round: loads stay unconditional and read the
+                  // cache-resident table image (see crc32c_wave_kernel); results are ignored
             v.p = reinterpret_cast<const uint8_t *>(g_tab);
-            v.crc = nullptr;
+            v.crc = const_cast<uint8_t *>(reinterpret_cast<const uint8_t *>(g_tab));
             v.chunk0 = 0;
             v.key0 = 0;
         }
@@ -804,11 +831,12 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
     fetch_tables(tv, g_tab);
     const u32x4 n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
     const u32x4 n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
-    RoundView rv[4] = {view(0), view(1), RoundView{}, RoundView{}};
+    // views: cv* = rounds being consumed, pv* = rounds being prefetched by this step
+    RoundView cv0 = view(0), cv1 = view(1);
     __builtin_amdgcn_sched_barrier(0);
     Round b[4];
-    load_round_buf<true>(b[0], rv[0].p, lane_off);
-    load_round_buf<true>(b[1], rv[1].p, lane_off);
+    load_round_buf<true>(b[0], cv0.p, lane_off);
+    load_round_buf<true>(b[1], cv1.p, lane_off);
     __builtin_amdgcn_sched_barrier(0);
     store_tables(lds, tv);
     {
@@ -820,31 +848,39 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
     const Lut t(lds);
     const NibFold nf(lds);
     const uint32_t init = j == 0 ? 0xFFFFFFFFu : 0u;
+    RoundView pv0 = view(2), pv1 = view(3);
 
-    auto want_of = [&](uint64_t k, const RoundView &v) -> uint32_t {
-        if constexpr (VERIFY) {
-            if (k >= K) return 0;
-            return *reinterpret_cast<const uint32_t *>(v.crc + 4 * (v.chunk0 + lane / G));
-        }
+    // Descriptor pointers carry no address space, so plain dereferences would compile to
+    // FLAT instructions, which count on lgkmcnt as well as vmcnt: every pipelined LDS wait
+    // would become lgkmcnt(0) and the prefetch would drain. Casting to the global address
+    // space keeps them global_load/store/atomic. Unconditional word loads (see the wave kernel).
+    typedef __attribute__((address_space(1))) const uint32_t gcu32;
+    typedef __attribute__((address_space(1))) uint32_t gu32;
+    typedef __attribute__((address_space(1))) unsigned long long gu64;
+    auto want_of = [&](const RoundView &v) -> uint32_t {
+        if constexpr (VERIFY) return *(gcu32 *)(v.crc + 4 * (v.chunk0 + lane / G));
         return 0;
     };
     auto finish = [&](uint64_t k, const RoundView &v, uint32_t y, uint32_t want) {
         if (k >= K || j != 0) return;
         const uint32_t c = ~y;
         if constexpr (VERIFY) {
-            if (__builtin_bswap32(want) != c) atomicMax(L.result, ~(unsigned long long)(v.key0 + lane / G));
+            if (__builtin_bswap32(want) != c)
+                __hip_atomic_fetch_max((gu64 *)L.result, ~(unsigned long long)(v.key0 + lane / G),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            *reinterpret_cast<uint32_t *>(v.crc + 4 * (v.chunk0 + lane / G)) = __builtin_bswap32(c);
+            *(gu32 *)(v.crc + 4 * (v.chunk0 + lane / G)) = __builtin_bswap32(c);
         }
     };
     auto word = [](const Round &r, int i) -> uint32_t { return r.w[i >> 2][i & 3]; };
 
-    // step: consume rounds k, k+1 (c0, c1 with views v0, v1), prefetch k+2, k+3 into p0, p1
-    auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, const RoundView &v0, const RoundView &v1,
-                    RoundView &pv0, RoundView &pv1, uint64_t k) {
-        const uint32_t w0 = want_of(k, v0), w1 = want_of(k + 1, v1);
-        pv0 = view(k + 2);
-        pv1 = view(k + 3);
+    // step: consume rounds k, k+1 (c0, c1; views cv0, cv1), prefetch k+2, k+3 (pv0, pv1).
+    // Straight-line from the stored-word loads through the prefetch: the next step's views
+    // (which branch) are resolved at the END of the step, after finish, so no branch sits
+    // between this step's loads (LLVM would otherwise sink the word loads past the
+    // prefetch and the waitcnt pass would drain it).
+    auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint64_t k) {
+        const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
         load_round_buf<true>(p0, pv0.p, lane_off);
         load_round_buf<true>(p1, pv1.p, lane_off);
         __builtin_amdgcn_sched_barrier(0);
@@ -864,20 +900,25 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
             x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
             __builtin_amdgcn_sched_barrier(0);
         }
-        finish(k, v0, group_xor<G>(nf.apply(x0)), w0);
-        finish(k + 1, v1, group_xor<G>(nf.apply(x1)), w1);
+        finish(k, cv0, group_xor<G>(nf.apply(x0)), w0);
+        finish(k + 1, cv1, group_xor<G>(nf.apply(x1)), w1);
+        __builtin_amdgcn_sched_barrier(0);
+        cv0 = pv0;
+        cv1 = pv1;
+        pv0 = view(k + 4);
+        pv1 = view(k + 5);
     };
     for (uint64_t k = 0; k < K; k += 4) {
-        step(b[0], b[1], b[2], b[3], rv[0], rv[1], rv[2], rv[3], k);
+        step(b[0], b[1], b[2], b[3], k);
         if (k + 2 >= K) break;
-        step(b[2], b[3], b[0], b[1], rv[2], rv[3], rv[0], rv[1], k + 2);
+        step(b[2], b[3], b[0], b[1], k + 2);
     }
 
     // slow pass: per segment, the chunks after its last whole round and its short tail
     const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
     const uint64_t nthreads = uint64_t(gridDim.x) * kBlockThreads;
     for (uint64_t si = gtid; si < L.nseg; si += nthreads) {
-        const DevSegment sd = L.seg[si];
+        const DevSegment sd = *segp(uint32_t(si));
         const uint64_t nfull = sd.len / BPC;
         const uint64_t first = (sd.len / kRoundBytes) * kChunksPerUnit;
         const uint64_t last = nfull + (sd.len % BPC ? 1 : 0);
@@ -1206,23 +1247,42 @@ bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc) {
     return true;
 }
 
+template <int BPC, bool UNI>
+hipError_t launch_seg_k(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *nib, int grid,
+                        hipStream_t s) {
+    if (verify)
+        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, true, UNI>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
+    else
+        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false, UNI>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
+    return hipGetLastError();
+}
+
 template <int BPC>
 hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *fold, int grid,
                         hipStream_t s) {
     constexpr int set = BPC == 512 ? 0 : BPC == 1024 ? 1 : BPC == 2048 ? 2 : 3;
     const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
-    if (verify)
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, true>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
-    else
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
-    return hipGetLastError();
+    return L.uniform ? launch_seg_k<BPC, true>(L, verify, tab, nib, grid, s)
+                     : launch_seg_k<BPC, false>(L, verify, tab, nib, grid, s);
 }
 
 hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,
                            uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
-                           const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream) {
+                           const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream,
+                           const DevSegment *h_inline) {
     if (nseg == 0) return hipSuccess;
-    const SegLaunch L{d_seg, nseg, units, uniform, result, check_short_tail};
+    SegLaunch L{};
+    L.seg = d_seg;
+    L.nseg = nseg;
+    L.units = units;
+    L.uniform = uniform;
+    L.result = result;
+    L.check_short_tail = check_short_tail;
+    if (h_inline) {
+        if (nseg > kInlineSegments) return hipErrorInvalidValue;
+        L.seg = nullptr;
+        for (uint32_t i = 0; i < nseg; ++i) L.inl[i] = h_inline[i];
+    }
     const uint64_t need = (units + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock);
     const uint64_t slow_need = (nseg + kBlockThreads - 1) / kBlockThreads;
     uint64_t g = need > slow_need ? need : slow_need;
@@ -1248,8 +1308,13 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
     if (g_variant != 17 && segments_fast(h_stage, n, bpc)) {
         uint64_t uniform = 0;
         const uint64_t units = plan_segments(h_stage, n, &uniform);
-        hipError_t e = hipMemcpyAsync(d_stage, h_stage, n * sizeof(DevSegment), hipMemcpyHostToDevice, stream);
-        if (e != hipSuccess) return e;
+        if (n > kInlineSegments) {
+            hipError_t e = hipMemcpyAsync(d_stage, h_stage, n * sizeof(DevSegment), hipMemcpyHostToDevice, stream);
+            if (e != hipSuccess) return e;
+        }
+        if (n <= kInlineSegments)  // no descriptor copy in front of the kernel
+            return launch_segments(nullptr, uint32_t(n), units, uniform, bpc, verify, check_short_tail, result,
+                                   d_tables, d_fold, grid_cap, stream, h_stage);
         return launch_segments(d_stage, uint32_t(n), units, uniform, bpc, verify, check_short_tail, result,
                                d_tables, d_fold, grid_cap, stream);
     }

@@ -267,9 +267,14 @@ int blocks_common(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, u
     if (segments_fast(st->h, n, bpc)) {
         uint64_t uniform = 0;
         const uint64_t units = plan_segments(st->h, n, &uniform);
-        HIP_TRY(hipMemcpyAsync(st->d, st->h, n * sizeof(DevSegment), hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(launch_segments(st->d, uint32_t(n), units, uniform, bpc, verify, check_short_tail, d_result,
-                                ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
+        if (n <= kMaxInlineSegments) {  // descriptors in the kernel arguments: no copy first
+            HIP_TRY(launch_segments(nullptr, uint32_t(n), units, uniform, bpc, verify, check_short_tail, d_result,
+                                    ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, st->h));
+        } else {
+            HIP_TRY(hipMemcpyAsync(st->d, st->h, n * sizeof(DevSegment), hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(launch_segments(st->d, uint32_t(n), units, uniform, bpc, verify, check_short_tail, d_result,
+                                    ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
+        }
         ++ctx->launches;
     } else {  // other chunk sizes or unaligned buffers: one launch per block, same keys
         for (size_t i = 0; i < n; ++i) {
