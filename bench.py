@@ -52,8 +52,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--sweep", action="store_true", help="extra diagnostics on stderr")
-    p.add_argument("--no-graph", action="store_true",
-                   help="launch the K steps eagerly instead of replaying captured HIP graphs")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the K steps from captured HIP graphs instead of launching them eagerly "
+                        "(no consistent gain measured: DESIGN.md §5)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -356,7 +357,7 @@ def main():
     K, W = args.steps, args.warmup
     result = torch.zeros(max(K, W, 1), dtype=torch.int64, device=device)
     run_steps(work, ctx, args.mode, W, result)
-    graphs = None if args.no_graph else StepGraphs(torch, work, ctx, args.mode, K, result, stream)
+    graphs = StepGraphs(torch, work, ctx, args.mode, K, result, stream) if args.graph else None
     result.zero_()
     torch.cuda.synchronize()
     # (1) timed region for `value`: K steps (graph replays, or K eager launches), nothing
