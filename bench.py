@@ -272,10 +272,19 @@ def cpu_baseline(work, seconds, bpc):
     if bad.value != -1:
         raise SystemExit(f"cpu baseline reported a bad chunk {bad.value} on a clean block")
     gib = data.nbytes * reps / t / 2**30
-    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{reps} x verify of one {data.nbytes >> 20} MiB block ({bpc} B chunks, "
-                      f"RemoteBlockReader::verifyChecksum loop) split over {threads} threads, {t:.1f} s; "
-                      f"engine: {engine}"}
+    out = {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+           "sample": f"{reps} x verify of one {data.nbytes >> 20} MiB block ({bpc} B chunks, "
+                     f"RemoteBlockReader::verifyChecksum loop) split over {threads} threads, {t:.1f} s; "
+                     f"engine: {engine}"}
+    # BASELINE.json configs[0]: one 64 KiB packet (128 x 512 B chunks) through the reference
+    # CPU path on one core, 10^4 repetitions timed inside the C loop
+    if ref is not None and ref.ref_hw_available():
+        pkt = 65536
+        tp = ref.ref_hw_bench_verify(data.ctypes.data, pkt, bpc, crc.ctypes.data, 1, 10000, ctypes.byref(bad))
+        if bad.value == -1:
+            out["config0_packet_us"] = round(tp / 10000 * 1e6, 3)
+            out["config0_packet_GiBps_1core"] = round(pkt * 10000 / tp / 2**30, 3)
+    return out
 
 
 def pmc_traffic(args):
