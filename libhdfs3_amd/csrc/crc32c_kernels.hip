@@ -542,6 +542,21 @@ struct NibFold {
         const uint32_t a7 = ld(((x >> 20) & 0xF00u) + 7 * 4096);
         return xor3(xor3(a0, a1, a2), xor3(a3, a4, a5), a6 ^ a7);
     }
+    // Same product. Spreading the nibbles over bytes lets ONE v_perm build each address:
+    // byte 0 = lane*4 and byte 2 = the fold region (from the lane base), byte 1 = nibble;
+    // the table (k*4096) rides in the ds_read offset.
+    __device__ __forceinline__ uint32_t apply_perm(uint32_t x) const {
+        const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
+        const uint32_t fb = kFoldLdsOff + 4 * (threadIdx.x & 63);
+        const uint8_t *l0 = f - fb;  // LDS base
+        auto at = [&](uint32_t src, uint32_t byte, int k) {
+            const uint32_t addr = __builtin_amdgcn_perm(src, fb, 0x0C020000u | ((4u + byte) << 8));
+            return *reinterpret_cast<const uint32_t *>(l0 + addr + k * 4096);
+        };
+        const uint32_t a0 = at(lo, 0, 0), a1 = at(hi, 0, 1), a2 = at(lo, 1, 2), a3 = at(hi, 1, 3);
+        const uint32_t a4 = at(lo, 2, 4), a5 = at(hi, 2, 5), a6 = at(lo, 3, 6), a7 = at(hi, 3, 7);
+        return xor3(xor3(a0, a1, a2), xor3(a3, a4, a5), a6 ^ a7);
+    }
 };
 
 // The 4 table reads of one word step, and their fold into the next state.
@@ -556,11 +571,59 @@ __device__ __forceinline__ Look lookups(const Lut &t, uint32_t x) {
     l.v[3] = t.at<3>(0, x);
     return l;
 }
+// Diagnostic (kOptFakeLut): the same v_perm address math with a VALU op where the
+// ds_read would be (no LDS traffic, wrong results).
+__device__ __forceinline__ Look fake_lookups(const Lut &t, uint32_t x) {
+    Look l;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t addr = __builtin_amdgcn_perm(x, t.base[i], 0x0C020000u | ((7u - i) << 8));
+        l.v[i] = __builtin_amdgcn_alignbit(addr, addr, 7 + i);
+    }
+    return l;
+}
 __device__ __forceinline__ uint32_t combine(const Look &l, uint32_t next) {
     return xor3(xor3(l.v[0], l.v[1], l.v[2]), l.v[3], next);
 }
 
-template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false>
+// OPT bits (experiments kept for A/B, tools/ab.py):
+//  kOptFillFirst: every wave of the workgroup issues its table/fold-image loads before any
+//    wave issues data loads (s_barrier between). The CU returns loads in order, so a table
+//    load queued behind other waves' HBM rounds waits for them at the CU's HBM share.
+constexpr int kOptFillFirst = 1;
+//  kOptFillWait: the LDS fill completes (table loads returned) before any data load issues.
+constexpr int kOptFillWait = 2;
+//  kOptNoHbm (diagnostic only, wrong results): every round reads the cache-resident table
+//    image instead of the block, so the launch runs at the kernel's compute/LDS rate.
+constexpr int kOptNoHbm = 4;
+//  kOptNoFill / kOptNoMath (diagnostics only, wrong results): skip the LDS table fill
+//    (tables are garbage) / replace the table CRC of a round by an xor of its words.
+constexpr int kOptNoFill = 8;
+constexpr int kOptNoMath = 16;
+//  kOptNibPerm: fold addresses by v_perm from the nibble-spread state (x & 0x0F0F0F0F,
+//    (x >> 4) & 0x0F0F0F0F): 11 VALU for the 8 addresses instead of 22.
+constexpr int kOptNibPerm = 32;
+//  kOptPf2: (PAIR 2) loads run two steps ahead of the lookups (6 round buffers, not 4).
+constexpr int kOptPf2 = 64;
+//  kOptWantBuf: (verify) stored CRC words through a buffer resource on the wave-uniform
+//    word base (lane offset the only VGPR): no 64-bit VGPR address temporaries, which the
+//    allocator can put on registers of in-flight round loads (a vmcnt(0) drain per step).
+constexpr int kOptWantBuf = 128;
+//  kOptLate: the step's prefetch issues after its own rounds arrived (0-8 KiB in flight
+//    per wave instead of 8-16). kOptSplit: the second prefetch round issues mid-step.
+constexpr int kOptLate = 256;
+constexpr int kOptSplit = 512;
+//  kOptFakeLut (diagnostic only, wrong results): table reads replaced by a VALU op.
+constexpr int kOptFakeLut = 2048;
+//  kOptSlotRegion: the 16 wave slots of a workgroup own 16 contiguous regions of the
+//    block; the 256 waves of one slot walk their region together (workgroup-interleaved
+//    4 KiB rounds). The SIMD arbiter favours older waves, so slots drift apart: with the
+//    round-robin mapping the in-flight requests then scatter over the whole block, with
+//    regions each slot's requests stay in one compact window.
+constexpr int kOptSlotRegion = 4096;
+
+template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
+          int OPT = 0>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a,
                                                                     const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
@@ -578,13 +641,25 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     // the end-of-stream prefetch guards below are scalar branches, not exec masks
     const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock +
                           __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t K = wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0;
+    // this wave's rounds: unit first + k * stride for k < K
+    uint64_t first = wave, stride = nwaves, K;
+    if constexpr ((OPT & kOptSlotRegion) != 0) {
+        const uint64_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const uint64_t R = (nunits + kWavesPerBlock - 1) / kWavesPerBlock;
+        const uint64_t lo = slot * R, hi = lo + R < nunits ? lo + R : nunits;
+        first = lo + blockIdx.x;
+        stride = gridDim.x;
+        K = first < hi ? (hi - first + stride - 1) / stride : 0;
+    } else {
+        K = wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0;
+    }
     // Prefetches past the wave's last round stay unconditional (a branch around them
     // makes the waitcnt pass drain every load at the loop head) but read the 4 KiB slice
     // table image instead: cache-resident, so they cost no HBM bytes (re-reading data
     // would, since the non-temporal stream is not kept in L2).
     auto round_ptr = [&](uint64_t k) -> const uint8_t * {
-        return k < K ? a.data + (wave + k * nwaves) * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
+        if constexpr ((OPT & kOptNoHbm) != 0) return reinterpret_cast<const uint8_t *>(g_tab);
+        return k < K ? a.data + (first + k * stride) * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
     };
 
     // TRACE (variant 13): lane 0 of each wave stamps entry, post-fill, post-first-step
@@ -603,17 +678,26 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     const u32x4 n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
     const u32x4 n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
     __builtin_amdgcn_sched_barrier(0);
-    Round b[2 * PAIR];
-#pragma unroll
-    for (int i = 0; i < PAIR; ++i) load_any<NT, BUF>(b[i], round_ptr(i), lane_off);
+    if constexpr ((OPT & kOptFillFirst) != 0) asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    store_tables(lds, tv);
-    {
+    auto fill = [&]() {
+        if constexpr ((OPT & kOptNoFill) != 0) return;
+        store_tables(lds, tv);
         u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * threadIdx.x;
         dst[0] = n0;
         dst[1] = n1;
+        lds_barrier();
+    };
+    if constexpr ((OPT & kOptFillWait) != 0) fill();
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int kPro = (OPT & kOptPf2) != 0 && PAIR == 2 ? 4 : PAIR;  // rounds loaded before the loop
+    Round b[kPro == 4 ? 6 : 2 * PAIR];
+#pragma unroll
+    for (int i = 0; i < kPro; ++i) {
+        load_any<NT, BUF>(b[i], round_ptr(i), lane_off);
+        __builtin_amdgcn_sched_barrier(0);
     }
-    lds_barrier();
+    if constexpr ((OPT & kOptFillWait) == 0) fill();
     stamp(1);
     const Lut t(lds);
     const NibFold nf(lds);
@@ -622,17 +706,27 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     auto want_of = [&](uint64_t k) -> uint32_t {
         if constexpr (VERIFY) {
             const uint64_t kk = k < K ? k : K - 1;
-            const uint64_t chunk = (wave + kk * nwaves) * kChunksPerUnit + lane / G;
+            if constexpr ((OPT & kOptWantBuf) != 0) {
+                const uint64_t b = reinterpret_cast<uint64_t>(a.crc_be + 4 * (first + kk * stride) * kChunksPerUnit);
+                const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(b));
+                const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(b >> 32));
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, 4 * kChunksPerUnit, 0x00020000);
+                return __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (lane / G), 0, 0);
+            }
+            const uint64_t chunk = (first + kk * stride) * kChunksPerUnit + lane / G;
             return *reinterpret_cast<const uint32_t *>(a.crc_be + 4 * chunk);
         }
         return 0;
     };
     auto finish = [&](uint64_t k, uint32_t y, uint32_t want) {
         if (k >= K || j != 0) return;
-        const uint64_t chunk = (wave + k * nwaves) * kChunksPerUnit + lane / G;
+        const uint64_t chunk = (first + k * stride) * kChunksPerUnit + lane / G;
         const uint32_t c = ~y;
         if constexpr (VERIFY) {
-            if (__builtin_bswap32(want) != c) atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
+            const bool bad = (OPT & (kOptNoHbm | kOptNoFill | kOptNoMath | kOptFakeLut)) != 0 ? __builtin_bswap32(want) == ~c
+                                                                               : __builtin_bswap32(want) != c;
+            if (bad) atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
         } else {
             *reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk) = __builtin_bswap32(c);
         }
@@ -657,18 +751,43 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             step(b[1], b[0], k + 1);
         }
     } else {
+        constexpr int PF = (OPT & kOptPf2) != 0 ? 2 : 1;  // steps of loads in flight
         auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint64_t k) {
             const uint32_t w0 = want_of(k), w1 = want_of(k + 1);
-            load_any<NT, BUF>(p0, round_ptr(k + 2), lane_off);
-            load_any<NT, BUF>(p1, round_ptr(k + 3), lane_off);
+            constexpr bool kLate = (OPT & kOptLate) != 0, kSplit = (OPT & kOptSplit) != 0;
+            if constexpr (!kLate) load_any<NT, BUF>(p0, round_ptr(k + 2 * PF), lane_off);
+            if constexpr (!kLate && !kSplit) load_any<NT, BUF>(p1, round_ptr(k + 2 * PF + 1), lane_off);
             __builtin_amdgcn_sched_barrier(0);
             regroup(c0);
             regroup(c1);
+            if constexpr (kLate) {
+                __builtin_amdgcn_sched_barrier(0);
+                load_any<NT, BUF>(p0, round_ptr(k + 2 * PF), lane_off);
+                load_any<NT, BUF>(p1, round_ptr(k + 2 * PF + 1), lane_off);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             uint32_t x0 = init ^ word(c0, 0), x1 = init ^ word(c1, 0);
+            if constexpr ((OPT & kOptNoMath) != 0) {
+#pragma unroll
+                for (int i = 1; i < 16; ++i) {
+                    x0 ^= word(c0, i);
+                    x1 ^= word(c1, i);
+                }
+            } else {
+            auto lookups = [&](const Lut &t, uint32_t x) {
+                if constexpr ((OPT & kOptFakeLut) != 0) return fake_lookups(t, x);
+                return ::hdfs3crc::lookups(t, x);
+            };
             Look l0 = lookups(t, x0), l1;
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
+                if constexpr (kSplit && !kLate) {
+                    if (i == 8) {
+                        load_any<NT, BUF>(p1, round_ptr(k + 2 * PF + 1), lane_off);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
                 l1 = lookups(t, x1);
                 __builtin_amdgcn_sched_barrier(0);
                 x0 = combine(l0, i < 15 ? word(c0, i < 15 ? i + 1 : 15) : 0u);
@@ -678,8 +797,9 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                 x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            const uint32_t y0 = group_xor<G>(nf.apply(x0));
-            const uint32_t y1 = group_xor<G>(nf.apply(x1));
+            }
+            const uint32_t y0 = group_xor<G>((OPT & kOptNibPerm) != 0 ? nf.apply_perm(x0) : nf.apply(x0));
+            const uint32_t y1 = group_xor<G>((OPT & kOptNibPerm) != 0 ? nf.apply_perm(x1) : nf.apply(x1));
             finish(k, y0, w0);
             finish(k + 1, y1, w1);
         };
@@ -699,13 +819,24 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                 }
             }
         };
-        for (uint64_t k = 0; k < K; k += 4) {
-            prio(k);
-            step(b[0], b[1], b[2], b[3], k);
-            if (k == 0) stamp(2);
-            if (k + 2 >= K) break;
-            prio(k + 2);
-            step(b[2], b[3], b[0], b[1], k + 2);
+        if constexpr (PF == 1) {
+            for (uint64_t k = 0; k < K; k += 4) {
+                prio(k);
+                step(b[0], b[1], b[2], b[3], k);
+                if (k == 0) stamp(2);
+                if (k + 2 >= K) break;
+                prio(k + 2);
+                step(b[2], b[3], b[0], b[1], k + 2);
+            }
+        } else {
+            for (uint64_t k = 0; k < K; k += 6) {
+                step(b[0], b[1], b[4], b[5], k);
+                if (k == 0) stamp(2);
+                if (k + 2 >= K) break;
+                step(b[2], b[3], b[0], b[1], k + 2);
+                if (k + 4 >= K) break;
+                step(b[4], b[5], b[2], b[3], k + 4);
+            }
         }
     }
     stamp(3);
@@ -720,6 +851,188 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         const uint64_t chunk = first_slow + gtid;
         const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(a.len % BPC);
         const uint32_t c = ~crc_run_any(t, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
+        if constexpr (VERIFY) {
+            if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(a.crc_be + 4 * chunk, crc_al4) != c)
+                atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
+        } else {
+            store_be32(a.out_be + 4 * chunk, c, crc_al4);
+        }
+    }
+}
+
+// ---- pool kernel: the wave kernel with per-CU dynamic round pairs (bpc <= 2048) ----
+//
+// The wave kernel assigns rounds statically (wave w: rounds w, w + W, ...). The SIMD
+// arbiter favours older waves, so the 16 waves of a CU drift apart: the oldest finish
+// their 8 rounds first and the youngest run their last steps alone, latency-bound, while
+// the CU's in-flight reads spread over a wider address window (tools/wave_trace.py).
+// Here the rounds of a workgroup form a POOL in address order (16-round segments at the
+// round-robin stride W = 16 * grid: unit wg*16 + i % 16 + (i / 16) * W for pool index i),
+// and every wave takes the next pair from an LDS counter (ds_add_rtn, lane 0) one step
+// ahead of its prefetch: faster waves take more pairs, the CU's reads stay the next
+// pairs of the pool, and all waves of a CU end within one step of each other.
+//
+// LDS: slice tables 128 KiB, then a HALF-size fold image (16 KiB): for G <= 32 lanes l and
+// l + 32 hold the same fold tables and never share a ds_read cycle, so 32 columns serve the
+// wave. Word (k >> 1) * 1024 + e * 64 + (k & 1) * 32 + (lane & 31) = M_j(e << 4k): the
+// nibble sits in address byte 1, so ONE v_perm on the nibble-spread state builds each
+// fold address; (k >> 1) * 4096 + (k & 1) * 128 rides in the ds_read offset. Then the
+// pool counter.
+constexpr int kPoolFoldOff = kLdsBytes;                 // 128 KiB
+constexpr int kPoolCtrOff = kLdsBytes + 16 * 1024;      // 144 KiB
+constexpr int kPoolLdsBytes = kPoolCtrOff + 16;
+
+__device__ __forceinline__ uint32_t fold_half(const uint8_t *lds, uint32_t x) {
+    const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
+    const uint32_t fb = kPoolFoldOff + 4 * (threadIdx.x & 31);
+    auto at = [&](uint32_t src, uint32_t byte, int off) {
+        const uint32_t addr = __builtin_amdgcn_perm(src, fb, 0x0C020000u | ((4u + byte) << 8));
+        return *reinterpret_cast<const uint32_t *>(lds + addr + off);
+    };
+    const uint32_t a0 = at(lo, 0, 0), a1 = at(hi, 0, 128), a2 = at(lo, 1, 4096), a3 = at(hi, 1, 4096 + 128);
+    const uint32_t a4 = at(lo, 2, 8192), a5 = at(hi, 2, 8192 + 128), a6 = at(lo, 3, 12288);
+    const uint32_t a7 = at(hi, 3, 12288 + 128);
+    return xor3(xor3(a0, a1, a2), xor3(a3, a4, a5), a6 ^ a7);
+}
+
+template <int BPC, bool VERIFY, bool TRACE = false>
+__global__ __launch_bounds__(kBlockThreads) void crc32c_pool_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
+                                                                    const uint32_t *__restrict__ g_nib) {
+    static_assert(BPC <= 2048 && BPC % 64 == 0, "G <= 32: lanes l and l + 32 share fold tables");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kPoolLdsBytes / 4];
+    constexpr int G = BPC / 64;
+    constexpr int kChunksPerUnit = kRoundBytes / BPC;
+    const uint8_t *lds8 = reinterpret_cast<const uint8_t *>(lds);
+    uint32_t *ctr = lds + kPoolCtrOff / 4;  // LDS byte kPoolCtrOff (the array starts at LDS 0)
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t j = lane % G;
+    const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nunits = a.len / kRoundBytes;
+    const uint64_t W = uint64_t(gridDim.x) * kWavesPerBlock;
+    const uint64_t wg0 = uint64_t(blockIdx.x) * kWavesPerBlock;
+    // pool index -> unit (monotone: once a pool index is past the end, so is every later one)
+    auto unit_of = [&](uint32_t i) -> uint64_t { return wg0 + (i & 15u) + uint64_t(i >> 4) * W; };
+    // past the end, loads stay unconditional but read the cache-resident table image
+    auto round_ptr = [&](uint64_t u) -> const uint8_t * {
+        return u < nunits ? a.data + u * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
+    };
+
+    uint64_t *tr = TRACE ? a.trace + 4 * (wg0 + slot) : nullptr;
+    auto stamp = [&](int i) {
+        if constexpr (TRACE) {
+            const uint64_t t = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) tr[i] = t;
+        }
+    };
+    stamp(0);
+    uint32_t tv[kFillPerThread];
+    fetch_tables(tv, g_tab);
+    // half fold image: this thread's 4 LDS words w = 4 * tid
+    const uint32_t t = threadIdx.x;
+    const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
+    const u32x4 nv = *reinterpret_cast<const u32x4 *>(g_nib + (fk * 16 + fe) * 64 + fc);
+    __builtin_amdgcn_sched_barrier(0);
+    // the first two pairs are static (pool indices 2 slot and 32 + 2 slot); the counter
+    // hands out pairs from 64 on
+    uint32_t ic = 2 * slot, in = 32 + 2 * slot;
+    Round b[4];
+    load_round_buf<true>(b[0], round_ptr(unit_of(ic)), lane_off);
+    __builtin_amdgcn_sched_barrier(0);
+    load_round_buf<true>(b[1], round_ptr(unit_of(ic + 1)), lane_off);
+    __builtin_amdgcn_sched_barrier(0);
+    store_tables(lds, tv);
+    reinterpret_cast<u32x4 *>(lds + kPoolFoldOff / 4)[t] = nv;
+    if (t == 0) *ctr = 64;
+    lds_barrier();
+    stamp(1);
+    const Lut tb(lds);
+    const uint32_t init = j == 0 ? 0xFFFFFFFFu : 0u;
+
+    auto want_of = [&](uint64_t u) -> uint32_t {
+        if constexpr (VERIFY) {
+            const uint64_t uu = u < nunits ? u : nunits - 1;
+            const uint64_t base = reinterpret_cast<uint64_t>(a.crc_be + 4 * uu * kChunksPerUnit);
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(base));
+            const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(base >> 32));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, 4 * kChunksPerUnit, 0x00020000);
+            return __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (lane / G), 0, 0);
+        }
+        return 0;
+    };
+    auto finish = [&](uint64_t u, uint32_t y, uint32_t want) {
+        if (u >= nunits || j != 0) return;
+        const uint64_t chunk = u * kChunksPerUnit + lane / G;
+        const uint32_t c = ~y;
+        if constexpr (VERIFY) {
+            if (__builtin_bswap32(want) != c) atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
+        } else {
+            *reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk) = __builtin_bswap32(c);
+        }
+    };
+    auto word = [](const Round &r, int i) -> uint32_t { return r.w[i >> 2][i & 3]; };
+
+    uint32_t grab = 0;
+    bool first_step = true;
+    auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1) {
+        const uint64_t u0 = unit_of(ic), u1 = unit_of(ic + 1);
+        const uint32_t w0 = want_of(u0), w1 = want_of(u1);
+        load_round_buf<true>(p0, round_ptr(unit_of(in)), lane_off);
+        load_round_buf<true>(p1, round_ptr(unit_of(in + 1)), lane_off);
+        // the pair after next: one LDS atomic by lane 0, issued as asm so the compiler neither
+        // spreads it over the wave nor waits for its result here (the step's table reads
+        // return after it, so it is long back when `grab` is read at the end of the step)
+        if (lane == 0)
+            asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(grab) : "v"(kPoolCtrOff), "v"(2u) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        regroup(c0);
+        regroup(c1);
+        uint32_t x0 = init ^ word(c0, 0), x1 = init ^ word(c1, 0);
+        Look l0 = lookups(tb, x0), l1;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            l1 = lookups(tb, x1);
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = combine(l0, i < 15 ? word(c0, i < 15 ? i + 1 : 15) : 0u);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i < 15) l0 = lookups(tb, x0);
+            __builtin_amdgcn_sched_barrier(0);
+            x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const uint32_t y0 = group_xor<G>(fold_half(lds8, x0));
+        const uint32_t y1 = group_xor<G>(fold_half(lds8, x1));
+        finish(u0, y0, w0);
+        finish(u1, y1, w1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ic = in;
+        in = __builtin_amdgcn_readfirstlane(grab);
+        if (first_step) {
+            stamp(2);
+            first_step = false;
+        }
+    };
+    for (;;) {
+        if (unit_of(ic) >= nunits) break;
+        step(b[0], b[1], b[2], b[3]);
+        if (unit_of(ic) >= nunits) break;
+        step(b[2], b[3], b[0], b[1]);
+    }
+    stamp(3);
+
+    // slow region: chunks after the last whole round, plus the short tail chunk
+    const uint64_t nfull = a.len / BPC;
+    const uint64_t first_slow = nunits * kChunksPerUnit;
+    const uint64_t nslow = nfull - first_slow + (a.len % BPC ? 1 : 0);
+    const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
+    const bool crc_al4 = (reinterpret_cast<uintptr_t>(VERIFY ? a.crc_be : a.out_be) & 3u) == 0;
+    if (gtid < nslow) {
+        const uint64_t chunk = first_slow + gtid;
+        const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(a.len % BPC);
+        const uint32_t c = ~crc_run_any(tb, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
         if constexpr (VERIFY) {
             if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(a.crc_be + 4 * chunk, crc_al4) != c)
                 atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
@@ -1099,7 +1412,7 @@ hipError_t launch_r3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *
 }
 
 template <int BPC, bool V, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
-          bool ANY_ORDER = false>
+          bool ANY_ORDER = false, int OPT = 0>
 hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                        hipStream_t s) {
     if constexpr (BPC > kRoundBytes) {
@@ -1112,11 +1425,28 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
         const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
         if constexpr (ANY_ORDER)  // experiment (variant 16): AQL packet without the barrier bit
-            hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO>), dim3(grid),
+            hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
                                   dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
         else
-            hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO>), dim3(grid),
+            hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
                                dim3(kBlockThreads), 0, s, a, tab, nib);
+        return hipGetLastError();
+    }
+}
+
+template <int BPC, bool V, bool TRACE = false>
+hipError_t launch_pool(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
+    if constexpr (BPC > 2048) {
+        return launch_wave<BPC, V, 2, true>(a, tab, fold, grid_cap, s);
+    } else {
+        constexpr int G = BPC / 64;
+        constexpr int set = G == 8 ? 0 : G == 16 ? 1 : 2;
+        const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
+        const uint64_t units = a.len / kRoundBytes;
+        const uint64_t need = (units + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock);
+        const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
+        hipLaunchKernelGGL((crc32c_pool_kernel<BPC, V, TRACE>), dim3(grid > 0 ? grid : 1), dim3(kBlockThreads), 0, s, a,
+                           tab, nib);
         return hipGetLastError();
     }
 }
@@ -1169,6 +1499,70 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
         ChunkLaunch e = a;
         e.trace = g_trace;
         return launch_wave<BPC, V, 2, true, true, true, true>(e, tab, fold, grid_cap, s);
+    }
+    case 18: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptFillFirst>(a, tab, fold, grid_cap, s);
+    case 19: {  // 18 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptFillFirst>(e, tab, fold, grid_cap, s);
+    }
+    case 20: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptFillWait>(a, tab, fold, grid_cap, s);
+    case 21: {  // 20 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptFillWait>(e, tab, fold, grid_cap, s);
+    }
+    case 22: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNoHbm>(a, tab, fold, grid_cap, s);
+    case 23: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNoFill>(a, tab, fold, grid_cap, s);
+    case 24: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNoMath>(a, tab, fold, grid_cap, s);
+    case 25:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNoMath | kOptNoFill>(a, tab, fold, grid_cap, s);
+    case 26: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNibPerm | kOptWantBuf>(a, tab, fold, grid_cap, s);
+    case 27: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptPf2 | kOptWantBuf>(a, tab, fold, grid_cap, s);
+    case 28:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptPf2 | kOptNibPerm | kOptWantBuf>(a, tab, fold,
+                                                                                                       grid_cap, s);
+    case 29: {  // 28 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptPf2 | kOptNibPerm | kOptWantBuf>(e, tab, fold,
+                                                                                                      grid_cap, s);
+    }
+    case 30: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptWantBuf>(a, tab, fold, grid_cap, s);
+    case 31:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptWantBuf | kOptLate>(a, tab, fold, grid_cap, s);
+    case 32:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptWantBuf | kOptSplit>(a, tab, fold, grid_cap, s);
+    case 33: return launch_wave<BPC, V, 2, true, true, false, true, false, kOptWantBuf | kOptLate>(a, tab, fold, grid_cap, s);
+    case 35: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptFakeLut>(a, tab, fold, grid_cap, s);
+    case 40: return launch_pool<BPC, V>(a, tab, fold, grid_cap, s);
+    case 41: {  // 40 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_pool<BPC, V, true>(e, tab, fold, grid_cap, s);
+    }
+    case 36:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptSlotRegion | kOptWantBuf>(a, tab, fold, grid_cap,
+                                                                                                    s);
+    case 37: {  // 36 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptSlotRegion | kOptWantBuf>(e, tab, fold,
+                                                                                                   grid_cap, s);
+    }
+    case 38:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptSlotRegion | kOptWantBuf | kOptNoMath>(
+            a, tab, fold, grid_cap, s);
+    case 34: {  // 24 (no table math) with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptNoMath>(e, tab, fold, grid_cap, s);
     }
     default: return launch_wave<BPC, V, 2, true>(a, tab, fold, grid_cap, s);
     }

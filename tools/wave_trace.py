@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--bpc", type=int, default=512)
     ap.add_argument("--block-mib", type=int, default=128)
     ap.add_argument("--variant", type=int, default=13, help="13 = production + stamps, 15 = + s_setprio")
+    ap.add_argument("--dump", default="", help="save the per-wave relative stamps (npz) of the first launches here")
     args = ap.parse_args()
 
     import torch
@@ -67,7 +68,7 @@ def main():
         e1.record(st)
         torch.cuda.synchronize()
         ev[v] = e0.elapsed_time(e1) * 1000 / 64
-    rows, groups = [], []
+    rows, groups, raw = [], [], []
     for i in range(args.launches):
         trace.zero_()
         launch(args.variant, i % blocks)
@@ -87,14 +88,22 @@ def main():
         if len(t) == 4096:
             wid = np.arange(4096)
             blk = wid // 16
+            if len(raw) < 4:
+                raw.append(rel)
+            wg_end = rel[:, 3].reshape(256, 16).max(axis=1)
             groups.append({
                 # WGs go round-robin over the 8 XCDs: blockIdx % 8 (cdna_hip_programming.md)
                 "end_by_xcd": [round(float(np.median(rel[blk % 8 == x, 3])), 2) for x in range(8)],
                 "end_by_wave_in_wg": [round(float(np.median(rel[wid % 16 == w, 3])), 2) for w in range(16)],
                 "end_by_blk_quartile": [round(float(np.median(rel[(blk // 64) == q, 3])), 2) for q in range(4)],
                 "first_by_xcd": [round(float(np.median(rel[blk % 8 == x, 2])), 2) for x in range(8)],
+                # per-CU (workgroup) completion: the last wave of each workgroup
+                "cu_end_pcts": [pct(wg_end, q) for q in (0, 10, 50, 90, 100)],
+                "cu_end_max_by_xcd": [round(float(wg_end[np.arange(256) % 8 == x].max()), 2) for x in range(8)],
             })
     lib.hdfs3x_set_variant(0)
+    if args.dump and raw:
+        np.savez_compressed(args.dump, rel=np.stack(raw))
     assert int(res.sum()) == 0, "verify reported a mismatch"
     med = {k: round(float(np.median([r[k] for r in rows])), 3) for k in rows[0]}
     print(json.dumps({"bench": "wave_trace", "bpc": args.bpc, "block_mib": args.block_mib,
