@@ -42,8 +42,11 @@ METRIC = "device-resident CRC32C GiB/s over 512 B HDFS chunks; % of HBM roofline
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=10)
+    # 1000 warmup launches (~25 ms): the GPU needs ~25 ms of sustained load to leave its
+    # idle power state; with 10 warmup launches the first ~1000 timed launches run ~15 %
+    # slower (W=10 27.0 us/launch, W=100 24.2, W>=1000 23.3, same box)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=1000)
     p.add_argument("--bpc", type=int, default=512)
     p.add_argument("--mode", choices=["verify", "compute"], default="verify")
     p.add_argument("--block-mib", type=int, default=128)
