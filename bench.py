@@ -216,23 +216,34 @@ class StepGraphs:
 
 
 def stream_read_ceiling(torch, work, ctx, reps=10):
-    """Achievable HBM read rate on the same 1 GiB arena: a coalesced 16 B/lane read-only
-    stream (best of two grid shapes), measured in this run for comparison."""
+    """Achievable HBM read on the same arena with a plain coalesced 16 B/lane read kernel
+    (no CRC): best of grid 256/512 x default/non-temporal loads.
+    Returns (1 GiB-per-launch GB/s, per-launch GB/s at the bench's own shape: one block per
+    launch rotating over the blocks, back to back, i.e. including the per-launch head and
+    dependent-launch overhead the CRC launches pay too)."""
     from libhdfs3_amd import _native
     lib = _native.lib()
     sink = torch.zeros(4, dtype=torch.int32, device=work.data.device)
     total = work.blocks * work.block_bytes
-    best = 0.0
-    for grid in (256, 512):
+
+    def rate(grid, nbytes, n, ptr_of):
+        for i in range(3):
+            lib.hdfs3x_stream_read(ctx.ctx, ptr_of(i), nbytes, grid, sink.data_ptr())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        lib.hdfs3x_stream_read(ctx.ctx, work.data.data_ptr(), total, grid, sink.data_ptr())
         e0.record()
-        for _ in range(reps):
-            lib.hdfs3x_stream_read(ctx.ctx, work.data.data_ptr(), total, grid, sink.data_ptr())
+        for i in range(n):
+            lib.hdfs3x_stream_read(ctx.ctx, ptr_of(i), nbytes, grid, sink.data_ptr())
         e1.record()
         torch.cuda.synchronize()
-        best = max(best, total * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9)
-    return best
+        return nbytes * n / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+    best, best_grid = 0.0, 256
+    for grid in (256, 512, -256, -512):  # negative: non-temporal loads
+        r = rate(grid, total, reps, lambda i: work.data.data_ptr())
+        if r > best:
+            best, best_grid = r, grid
+    per_block = rate(best_grid, work.block_bytes, 400, lambda i: work.data_ptr(i % work.blocks))
+    return best, per_block
 
 
 def lane_read_rate(torch, work, ctx, reps=10):
@@ -424,8 +435,11 @@ def main():
     extra = {}
     if world == 1:
         try:
-            extra["achievable_read_GBps"] = round(stream_read_ceiling(torch, work, ctx), 1)
-            roofline["achievable_read_GBps"] = extra["achievable_read_GBps"]
+            whole, per_block = stream_read_ceiling(torch, work, ctx)
+            roofline["achievable_read_GBps"] = round(whole, 1)
+            # the same shape as the timed steps: a plain read of one block per launch
+            roofline["achievable_read_per_block_launch_GBps"] = round(per_block, 1)
+            roofline["frac_of_achievable_per_block"] = round(achieved / (per_block * alg_bytes / payload), 4)
         except Exception as e:
             log("stream ceiling failed:", e)
         try:

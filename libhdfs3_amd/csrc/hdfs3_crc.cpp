@@ -641,7 +641,7 @@ int hdfs3x_stream_read(hdfs3_crc_ctx *ctx, const void *d, size_t len, int grid, 
     if (!ctx) return fail(-EINVAL, "null ctx");
     DeviceGuard g(ctx->device);
     HIP_TRY(launch_stream_read(static_cast<const uint8_t *>(d), len, static_cast<uint32_t *>(d_sink),
-                               grid > 0 ? grid : ctx->grid_cap * 8, ctx->stream));
+                               grid != 0 ? grid : ctx->grid_cap * 8, ctx->stream));
     return 0;
 }
 
