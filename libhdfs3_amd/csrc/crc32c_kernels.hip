@@ -621,6 +621,9 @@ constexpr int kOptFakeLut = 2048;
 //    round-robin mapping the in-flight requests then scatter over the whole block, with
 //    regions each slot's requests stay in one compact window.
 constexpr int kOptSlotRegion = 4096;
+//  kOptVgprFold: the lane fold as a 32-column GF(2) product in VGPRs (gf2_apply4, 64 VALU)
+//    instead of 8 nibble-table reads: trades LDS returns for VALU (§5.0).
+constexpr int kOptVgprFold = 8192;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -702,6 +705,19 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     const Lut t(lds);
     const NibFold nf(lds);
     const uint32_t init = j == 0 ? 0xFFFFFFFFu : 0u;
+    uint32_t col[32];
+    if constexpr ((OPT & kOptVgprFold) != 0) {
+        constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
+        constexpr int kFoldOff[4] = {0, 8, 24, 56};
+        const uint32_t *g_fold = g_nib - kFoldWords - set * kFoldNibbleWords;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) col[i] = g_fold[(kFoldOff[set] + j) * 32 + i];
+    }
+    auto fold = [&](uint32_t x) -> uint32_t {
+        if constexpr ((OPT & kOptVgprFold) != 0) return gf2_apply4(col, x);
+        if constexpr ((OPT & kOptNibPerm) != 0) return nf.apply_perm(x);
+        return nf.apply(x);
+    };
 
     auto want_of = [&](uint64_t k) -> uint32_t {
         if constexpr (VERIFY) {
@@ -798,8 +814,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                 __builtin_amdgcn_sched_barrier(0);
             }
             }
-            const uint32_t y0 = group_xor<G>((OPT & kOptNibPerm) != 0 ? nf.apply_perm(x0) : nf.apply(x0));
-            const uint32_t y1 = group_xor<G>((OPT & kOptNibPerm) != 0 ? nf.apply_perm(x1) : nf.apply(x1));
+            const uint32_t y0 = group_xor<G>(fold(x0));
+            const uint32_t y1 = group_xor<G>(fold(x1));
             finish(k, y0, w0);
             finish(k + 1, y1, w1);
         };
@@ -1544,6 +1560,9 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
     case 33: return launch_wave<BPC, V, 2, true, true, false, true, false, kOptWantBuf | kOptLate>(a, tab, fold, grid_cap, s);
     case 35: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptFakeLut>(a, tab, fold, grid_cap, s);
     case 40: return launch_pool<BPC, V>(a, tab, fold, grid_cap, s);
+    case 42:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptVgprFold | kOptWantBuf>(a, tab, fold, grid_cap,
+                                                                                                   s);
     case 41: {  // 40 with timestamps
         if (!g_trace) return hipErrorInvalidValue;
         ChunkLaunch e = a;
