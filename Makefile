@@ -16,7 +16,9 @@ OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc3
             $(OBJDIR)/client_input_stream.o $(OBJDIR)/client_output_stream.o \
             $(OBJDIR)/client_local_reader.o
 
-all: $(LIB) $(LOOPBACK) oracle
+CONSUMER := tests/native/abi_consumer
+
+all: $(LIB) $(LOOPBACK) oracle $(CONSUMER)
 
 $(OBJDIR)/crc32c_kernels.o: $(CSRC)/crc32c_kernels.hip $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
 	@mkdir -p $(OBJDIR)
@@ -63,12 +65,18 @@ $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS)
 
+# test infrastructure: a C++ consumer of the C-ABI, checked against the oracle
+$(CONSUMER): tests/native/abi_consumer.cpp include/hdfs3_crc.h oracle/crc32c_oracle.c oracle/crc32c_oracle.h $(LIB)
+	gcc -O2 -msse4.2 -mpclmul -c oracle/crc32c_oracle.c -o $(OBJDIR)/consumer_oracle.o
+	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ tests/native/abi_consumer.cpp $(OBJDIR)/consumer_oracle.o \
+	    -L$(LIBDIR) -lhdfs3_crc -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath-link,/opt/rocm/lib -pthread
+
 oracle:
 	$(MAKE) -C oracle all
 	@if [ -d /root/reference/src/common ]; then $(MAKE) -C oracle ref; fi
 
 clean:
-	rm -rf build $(LIB) $(LOOPBACK)
+	rm -rf build $(LIB) $(LOOPBACK) $(CONSUMER)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -1,0 +1,34 @@
+"""The drop-in boundary as a C++ caller sees it: tests/native/abi_consumer.cpp includes only
+include/hdfs3_crc.h, links libhdfs3_crc.so (built by `make`, no Python or torch in the
+process) and runs the reference call-site shapes — RemoteBlockReader::verifyChecksum,
+LocalBlockReader::readAndVerify, OutputStreamImpl compute, a wire-layout packet arena with
+odd offsets, device-resident blocks — checked word for word against the oracle."""
+import os
+import subprocess
+
+import pytest
+
+from util import REPO
+
+BIN = os.path.join(REPO, "tests", "native", "abi_consumer")
+
+
+def _run(*args):
+    if not os.path.exists(BIN):
+        pytest.fail("tests/native/abi_consumer not built (run `make`)")
+    return subprocess.run([BIN, *args], capture_output=True, text=True, timeout=120)
+
+
+def test_cpp_consumer_refuses_without_device():
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("a GPU is visible; the -m gpu test runs the consumer")
+    r = _run("nodevice")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "nodevice ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_consumer_on_gpu():
+    r = _run()
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "abi_consumer ok" in r.stdout
