@@ -215,6 +215,54 @@ __global__ __launch_bounds__(1024) void k_lds(uint32_t *sink) {
     if ((acc0 ^ acc1) == 0x9E3779B9u) sink[0] = 1;
 }
 
+// rounds_rr with NG L1-resident gathers per round: dword loads at data-derived offsets in
+// a 4 KiB table image (buffer descriptor, lane-varying offset), issued BEFORE the round's
+// prefetch (so in-order vmcnt never makes them wait for HBM) and consumed after it.
+template <int NG>
+__global__ __launch_bounds__(1024) void k_rounds_gather(const uint8_t *__restrict__ d, uint64_t len,
+                                                       const uint32_t *__restrict__ tab, uint32_t *sink) {
+    extern __shared__ uint32_t lds_pad[];
+    constexpr int D = 2;
+    const uint64_t nunits = len / 4096;
+    const uint64_t W = uint64_t(gridDim.x) * 16;
+    const uint64_t wave = uint64_t(blockIdx.x) * 16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint8_t *dummy = reinterpret_cast<const uint8_t *>(sink) + 4096;
+    auto src = [&](uint64_t kk) { return kk < nunits ? d + kk * 4096 : dummy; };
+    const __amdgpu_buffer_rsrc_t trs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(tab), 0, 4096, 0x00020000);
+    uint32_t acc = 0;
+    u32x4 b[D][4];
+    uint64_t k = wave;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        ld_round<true>(b[i], src(k + i * W), 16 * lane);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    for (; k < nunits; k += D * W) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const uint64_t kk = k + i * W;
+            uint32_t x[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) x[t] = fold(b[i][t]);
+            uint32_t g[NG > 0 ? NG : 1];
+#pragma unroll
+            for (int n = 0; n < NG; ++n)
+                g[n] = __builtin_amdgcn_raw_buffer_load_b32(
+                    trs, ((x[n & 3] >> (8 * ((n >> 2) & 3))) & 0xFFu) * 4 + ((n >> 4) & 3) * 1024, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            ld_round<true>(b[i], src(kk + D * W), 16 * lane);
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t y = x[0] ^ x[1] ^ x[2] ^ x[3];
+#pragma unroll
+            for (int n = 0; n < NG; ++n) y ^= g[n];
+            acc ^= kk < nunits ? y : 0u;
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc + lds_pad[0];
+}
+
 __global__ void k_empty(uint32_t *sink) {
     extern __shared__ uint32_t lds_pad[];
     if (threadIdx.x == 0 && blockIdx.x == 0 && sink[1] == 0x12345678u) sink[0] = lds_pad[0];
@@ -323,6 +371,19 @@ static void run_lds() {
     fflush(stdout);
 }
 
+template <int NG>
+static void run_gather() {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rounds_gather<NG>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const uint32_t *tab = g_sink + 2048;  // bytes 8 KiB.. of the sink buffer
+    Res r = measure([&](const uint8_t *p, uint64_t n) {
+        hipLaunchKernelGGL((k_rounds_gather<NG>), dim3(256), dim3(1024), 160 * 1024, g_st, p, n, tab, g_sink);
+    });
+    char name[64];
+    snprintf(name, sizeof name, "gather_%d", NG);
+    report(name, 256, 1024, 2, 1, 160, r);
+}
+
 static void run_empty(int grid, int block, int lds_kib) {
     CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_empty), hipFuncAttributeMaxDynamicSharedMemorySize,
                            lds_kib * 1024));
@@ -346,9 +407,9 @@ int main(int argc, char **argv) {
     const int only = argc > 1 ? atoi(argv[1]) : -1;
     CK(hipStreamCreateWithFlags(&g_st, hipStreamNonBlocking));
     CK(hipMalloc(&g_buf, kAll));
-    CK(hipMalloc(&g_sink, 8192));
+    CK(hipMalloc(&g_sink, 16384));
     CK(hipMemset(g_buf, 0x5A, kAll));
-    CK(hipMemset(g_sink, 0, 8192));
+    CK(hipMemset(g_sink, 0, 16384));
     CK(hipDeviceSynchronize());
 
     if (only < 0 || only == 0) {
@@ -401,6 +462,16 @@ int main(int argc, char **argv) {
             run_lds<16, 4096>();
             run_lds<4, 16384>();
             run_lds<8, 16384>();
+        }
+    }
+    if (only == 5) {
+        for (int rep = 0; rep < 3; ++rep) {
+            run_rounds<2, true, 0>(256, 1024, 160);
+            run_gather<0>();
+            run_gather<8>();
+            run_gather<16>();
+            run_gather<32>();
+            run_work<2, 0, 32>(160);
         }
     }
     CK(hipFree(g_buf));
