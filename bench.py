@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--graph", action="store_true",
                    help="replay the K steps from captured HIP graphs instead of launching them eagerly "
                         "(no consistent gain measured: DESIGN.md §5)")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="barrier every timed launch (no HDFS3_LAUNCH_OVERLAP_PREVIOUS); the overlapped "
+                        "run is the default and the barriered one is reported beside it")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -137,7 +140,12 @@ def check_against_oracle(work, ctx):
         raise SystemExit("PARITY FAILURE: clean block reported bad")
 
 
-def run_steps(work, ctx, mode, n, result, events=None, base=0):
+def run_steps(work, ctx, mode, n, result, events=None, base=0, overlap=False):
+    """n steps, one launch each. overlap: every launch after the first of this run goes out
+    with HDFS3_LAUNCH_OVERLAP_PREVIOUS (include/hdfs3_crc.h) — its predecessor on the stream
+    is a verify of this run and all blocks, CRC arrays and zeroed result words were ready
+    before the run started; the first launch of a run stays barriered behind whatever the
+    stream held before (the result memset, events)."""
     for i in range(n):
         s = base + i
         b = s % work.blocks
@@ -145,7 +153,8 @@ def run_steps(work, ctx, mode, n, result, events=None, base=0):
             events[2 * i].record()
         if mode == "verify":
             ctx.verify_dev_async(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b),
-                                 result.data_ptr() + 8 * (s % result.numel()))
+                                 result.data_ptr() + 8 * (s % result.numel()),
+                                 overlap_previous=overlap and i > 0 and events is None)
         else:
             ctx.compute_dev(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b))
         if events is not None:
@@ -387,8 +396,9 @@ def main():
     torch.cuda.synchronize()
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the roofline pass")
+    overlap = args.mode == "verify" and not args.no_overlap
     result.zero_()
-    run_steps(work, ctx, args.mode, W, result)
+    run_steps(work, ctx, args.mode, W, result, overlap=overlap)
     graphs = StepGraphs(torch, work, ctx, args.mode, K, result, stream) if args.graph else None
     result.zero_()
     torch.cuda.synchronize()
@@ -403,7 +413,7 @@ def main():
     if graphs is not None:
         graphs.run()
     else:
-        run_steps(work, ctx, args.mode, K, result)
+        run_steps(work, ctx, args.mode, K, result, overlap=overlap)
     ev1.record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -442,6 +452,24 @@ def main():
             roofline["frac_of_achievable_per_block"] = round(achieved / (per_block * alg_bytes / payload), 4)
         except Exception as e:
             log("stream ceiling failed:", e)
+        if overlap:
+            # the same K steps with every launch barriered (plain hdfs3_crc32c_verify_dev_async)
+            result.zero_()
+            run_steps(work, ctx, args.mode, W, result)
+            torch.cuda.synchronize()
+            b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            b0.record(stream)
+            run_steps(work, ctx, args.mode, K, result)
+            b1.record(stream)
+            torch.cuda.synchronize()
+            if bool((result != 0).any().item()):
+                raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the barriered pass")
+            bl = b0.elapsed_time(b1) * 1e-3 / K
+            extra["barriered"] = {"api": "hdfs3_crc32c_verify_dev_async (AQL barrier bit on every launch)",
+                                  "value": round(payload / bl / 2**30, 2), "unit": "GiB/s",
+                                  "avg_launch_us": round(bl * 1e6, 2),
+                                  "achieved_GBps": round(alg_bytes / bl / 1e9, 1),
+                                  "frac": round(alg_bytes / bl / 1e9 / HBM_PEAK_GBPS, 4)}
         try:
             extra["batched"] = batched_rate(torch, work, ctx, args.mode)
         except SystemExit:
@@ -461,7 +489,9 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": K,
         "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True,
-        "launch": "eager" if graphs is None else f"HIP graph replay, {graphs.per} single-block launches per graph",
+        "launch": (f"HIP graph replay, {graphs.per} single-block launches per graph" if graphs is not None
+                   else "eager, one launch per step; launches after the first overlap their predecessor "
+                        "(HDFS3_LAUNCH_OVERLAP_PREVIOUS)" if overlap else "eager, one barriered launch per step"),
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (torch.randint bytes)",
         "config": {"workload": f"{args.mode} of one {args.block_mib} MiB HDFS block per step, "
                                f"{args.bpc} B chunks, device-resident (BASELINE.json configs[1])",
@@ -470,6 +500,8 @@ def main():
                    "parallelism": f"{world} GPU(s), independent blocks one set per GPU, no collectives"},
         "roofline": roofline, "cpu_baseline": cpu,
     }
+    if "barriered" in extra:
+        line["barriered"] = extra["barriered"]
     if "batched" in extra:
         line["batched"] = extra["batched"]
     if cpu:

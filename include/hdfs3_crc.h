@@ -110,6 +110,25 @@ int hdfs3_crc32c_verify_dev_async(hdfs3_crc_ctx *ctx, const void *d_data, size_t
                                   uint64_t *d_result);
 int64_t hdfs3_crc_decode_result(uint64_t result_word);
 
+/* Same as hdfs3_crc32c_verify_dev_async, with launch flags.
+ * HDFS3_LAUNCH_OVERLAP_PREVIOUS: the kernel may start before the PREVIOUS operation on
+ * the ctx stream has completed (its AQL packet is launched without the barrier bit), so
+ * back-to-back verifies of resident blocks overlap one launch's tail with the next one's
+ * head instead of draining the GPU between them. The caller guarantees:
+ *   - the previous operation enqueued on the stream is itself a verify launch of this
+ *     library (either form), and
+ *   - this launch's data, CRC words and zeroed result word were ready before that
+ *     previous verify was enqueued.
+ * Never pass it for the first verify after any other work on the stream (an upload,
+ * a memset of the result word, a kernel of the caller's): that one must be barriered.
+ * Verifies only read their inputs and atomically fold into their own result word, so
+ * overlapping verifies cannot affect each other's results. Without the flag (0) the
+ * call is exactly hdfs3_crc32c_verify_dev_async. */
+#define HDFS3_LAUNCH_OVERLAP_PREVIOUS 1u
+int hdfs3_crc32c_verify_dev_async_ex(hdfs3_crc_ctx *ctx, const void *d_data, size_t len,
+                                     uint32_t bpc, const void *d_crc_be, int check_short_tail,
+                                     uint64_t *d_result, uint32_t flags);
+
 /* ---- batch of independent device-resident blocks -------------------------------
  * n blocks (each its own data, CRC array and length; chunk counts < 2^32) verified or
  * computed in ONE launch of the segmented wave kernel — the batch form of the calls

@@ -52,6 +52,8 @@ PUBLIC_API = {
                                         POINTER(c_int64)]),
     "hdfs3_crc32c_verify_dev_async": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p,
                                               c_int, c_void_p]),
+    "hdfs3_crc32c_verify_dev_async_ex": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p,
+                                                 c_int, c_void_p, c_uint32]),
     "hdfs3_crc_decode_result": (c_int64, [c_uint64]),
     "hdfs3_crc32c_verify_packets": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PktDesc),
                                             c_size_t, c_uint32, c_int, POINTER(c_int64),

@@ -22,6 +22,7 @@ struct ChunkLaunch {
     uint64_t chunk_base;      // added to chunk indices reported in *result
     int check_short_tail;     // 1: tail chunk checked (LocalBlockReader semantics)
     uint64_t *trace = nullptr;  // diagnostic variant 13 only: 4 s_memrealtime stamps per wave
+    bool overlap_previous = false;  // HDFS3_LAUNCH_OVERLAP_PREVIOUS: AQL packet without barrier bit
 };
 
 // Packet-descriptor as seen by the device (mirrors hdfs3_pkt_desc).

@@ -1588,7 +1588,11 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
         e.trace = g_trace;
         return launch_wave<BPC, V, 2, true, true, true, false, false, kOptNoMath>(e, tab, fold, grid_cap, s);
     }
-    default: return launch_wave<BPC, V, 2, true>(a, tab, fold, grid_cap, s);
+    default:
+        // production wave kernel; an opted-in overlapped launch (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
+        // goes out as an AQL packet without the barrier bit (the same kernel)
+        if (a.overlap_previous) return launch_wave<BPC, V, 2, true, true, false, false, true>(a, tab, fold, grid_cap, s);
+        return launch_wave<BPC, V, 2, true>(a, tab, fold, grid_cap, s);
     }
 }
 

@@ -507,7 +507,14 @@ int hdfs3_crc32c_compute_dev(hdfs3_crc_ctx *ctx, const void *d_data, size_t len,
 int hdfs3_crc32c_verify_dev_async(hdfs3_crc_ctx *ctx, const void *d_data, size_t len,
                                   uint32_t bpc, const void *d_crc_be, int check_short_tail,
                                   uint64_t *d_result) {
+    return hdfs3_crc32c_verify_dev_async_ex(ctx, d_data, len, bpc, d_crc_be, check_short_tail, d_result, 0);
+}
+
+int hdfs3_crc32c_verify_dev_async_ex(hdfs3_crc_ctx *ctx, const void *d_data, size_t len,
+                                     uint32_t bpc, const void *d_crc_be, int check_short_tail,
+                                     uint64_t *d_result, uint32_t flags) {
     if (int rc = check_args(ctx, bpc)) return rc;
+    if (flags & ~HDFS3_LAUNCH_OVERLAP_PREVIOUS) return fail(-EINVAL, "unknown launch flags 0x%x", flags);
     if (len == 0) return 0;
     if (!d_data || !d_crc_be || !d_result) return fail(-EINVAL, "null buffer");
     DeviceGuard g(ctx->device);
@@ -518,6 +525,7 @@ int hdfs3_crc32c_verify_dev_async(hdfs3_crc_ctx *ctx, const void *d_data, size_t
     a.crc_be = static_cast<const uint8_t *>(d_crc_be);
     a.result = reinterpret_cast<unsigned long long *>(d_result);
     a.check_short_tail = check_short_tail;
+    a.overlap_previous = (flags & HDFS3_LAUNCH_OVERLAP_PREVIOUS) != 0;
     return launch(ctx, a, true);
 }
 

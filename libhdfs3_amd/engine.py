@@ -152,7 +152,15 @@ class CrcContext:
         return bad.value
 
     def verify_dev_async(self, d_data: int, nbytes: int, bpc: int, d_crc: int, d_result: int,
-                         check_short_tail: bool = False) -> None:
+                         check_short_tail: bool = False, overlap_previous: bool = False) -> None:
+        """overlap_previous: HDFS3_LAUNCH_OVERLAP_PREVIOUS (see include/hdfs3_crc.h for the
+        caller's guarantee: the previous op on the stream is a verify and this one's inputs
+        were ready before it)."""
+        if overlap_previous:
+            check("hdfs3_crc32c_verify_dev_async_ex",
+                  self._lib.hdfs3_crc32c_verify_dev_async_ex(self.ctx, d_data, nbytes, bpc, d_crc,
+                                                             int(check_short_tail), d_result, 1))
+            return
         check("hdfs3_crc32c_verify_dev_async",
               self._lib.hdfs3_crc32c_verify_dev_async(self.ctx, d_data, nbytes, bpc, d_crc,
                                                       int(check_short_tail), d_result))

@@ -295,3 +295,35 @@ def test_beyond_4gib_single_call_64bit_addressing(gpu_ctx):
         assert gpu_ctx.verify_dev(dbuf.ptr, n, bpc, crc.ptr, True) == pos // bpc
         gpu_ctx.upload(orig, dbuf, offset=pos)
     dbuf.free()
+
+
+@pytest.mark.parametrize("bpc", [512, 2048, 4096])
+def test_overlapped_verify_chain_matches_oracle(gpu_ctx, bpc):
+    """HDFS3_LAUNCH_OVERLAP_PREVIOUS: a chain of verifies whose launches overlap (AQL packets
+    without the barrier bit) gives every block exactly its own result: clean blocks 0, the
+    corrupted block its first bad chunk, over many launches and ragged block lengths."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    nblk, reps = 6, 8
+    lens = [(8 << 20) + (i * 4099 if i % 2 else 0) for i in range(nblk)]
+    blocks = []
+    for i, n in enumerate(lens):
+        data = splitmix_bytes(n, 0xC4A1 + i + bpc)
+        want = oracle_compute(data, bpc)
+        blocks.append((gpu_ctx.upload(data), gpu_ctx.upload(want), n, data))
+    bad_blk, bad_chunk = 3, (lens[3] // bpc) // 2 + 5
+    pos = bad_chunk * bpc + 11
+    gpu_ctx.upload(np.array([blocks[bad_blk][3][pos] ^ 0x40], np.uint8), blocks[bad_blk][0], offset=pos)
+    res = DeviceBuffer(8 * nblk * reps)
+    gpu_ctx.memset(res, 0, 8 * nblk * reps)
+    gpu_ctx.synchronize()
+    for r in range(reps):
+        for i, (d, c, n, _) in enumerate(blocks):
+            gpu_ctx.verify_dev_async(d.ptr, n, bpc, c.ptr, res.ptr + 8 * (r * nblk + i), check_short_tail=True,
+                                     overlap_previous=(r, i) != (0, 0))
+    gpu_ctx.synchronize()
+    words = gpu_ctx.download(res, 8 * nblk * reps).view(np.uint64)
+    for r in range(reps):
+        for i in range(nblk):
+            got = gpu_ctx.decode_result(int(words[r * nblk + i]))
+            assert got == (bad_chunk if i == bad_blk else -1), (r, i, got)
