@@ -224,7 +224,7 @@ class StepGraphs:
             self.graphs[1].replay()
 
 
-def stream_read_ceiling(torch, work, ctx, reps=10):
+def stream_read_ceiling(torch, work, ctx, reps=10, overlap=False):
     """Achievable HBM read on the same arena with a plain coalesced 16 B/lane read kernel
     (no CRC): best of grid 256/512 x default/non-temporal loads.
     Returns (1 GiB-per-launch GB/s, per-launch GB/s at the bench's own shape: one block per
@@ -235,13 +235,13 @@ def stream_read_ceiling(torch, work, ctx, reps=10):
     sink = torch.zeros(4, dtype=torch.int32, device=work.data.device)
     total = work.blocks * work.block_bytes
 
-    def rate(grid, nbytes, n, ptr_of):
+    def rate(grid, nbytes, n, ptr_of, overlap=False):
         for i in range(3):
             lib.hdfs3x_stream_read(ctx.ctx, ptr_of(i), nbytes, grid, sink.data_ptr())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for i in range(n):
-            lib.hdfs3x_stream_read(ctx.ctx, ptr_of(i), nbytes, grid, sink.data_ptr())
+            lib.hdfs3x_stream_read_ex(ctx.ctx, ptr_of(i), nbytes, grid, sink.data_ptr(), int(overlap and i > 0))
         e1.record()
         torch.cuda.synchronize()
         return nbytes * n / (e0.elapsed_time(e1) * 1e-3) / 1e9
@@ -251,7 +251,7 @@ def stream_read_ceiling(torch, work, ctx, reps=10):
         r = rate(grid, total, reps, lambda i: work.data.data_ptr())
         if r > best:
             best, best_grid = r, grid
-    per_block = rate(best_grid, work.block_bytes, 400, lambda i: work.data_ptr(i % work.blocks))
+    per_block = rate(best_grid, work.block_bytes, 400, lambda i: work.data_ptr(i % work.blocks), overlap)
     return best, per_block
 
 
@@ -445,9 +445,10 @@ def main():
     extra = {}
     if world == 1:
         try:
-            whole, per_block = stream_read_ceiling(torch, work, ctx)
+            whole, per_block = stream_read_ceiling(torch, work, ctx, overlap=overlap)
             roofline["achievable_read_GBps"] = round(whole, 1)
-            # the same shape as the timed steps: a plain read of one block per launch
+            # the same shape as the timed steps: a plain read of one block per launch, with
+            # the same launch mode (overlapped or barriered)
             roofline["achievable_read_per_block_launch_GBps"] = round(per_block, 1)
             roofline["frac_of_achievable_per_block"] = round(achieved / (per_block * alg_bytes / payload), 4)
         except Exception as e:

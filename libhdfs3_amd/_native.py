@@ -167,6 +167,7 @@ CLIENT_API = {
 # measurement hooks (bench.py only; not in the public header)
 BENCH_API = {
     "hdfs3x_stream_read": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    "hdfs3x_stream_read_ex": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_uint32]),
     "hdfs3x_lane_read": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p]),
     "hdfs3x_grid_cap": (c_int, [c_void_p]),
     "hdfs3x_set_variant": (None, [c_int]),

@@ -83,7 +83,7 @@ void set_trace(uint64_t *d_trace);  // buffer for variant 13 (4 x u64 per wave)
 // Measurement-only kernels (bench/profiling): HBM read ceiling and the CRC
 // kernel's access pattern without the table arithmetic.
 hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,
-                              hipStream_t stream);
+                              hipStream_t stream, bool overlap_previous = false);
 hipError_t launch_lane_read(const uint8_t *d, uint64_t len, uint32_t bpc, uint32_t *sink,
                             int grid_cap, hipStream_t stream);
 

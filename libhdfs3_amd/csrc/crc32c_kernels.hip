@@ -1753,12 +1753,16 @@ void set_variant(int v) { g_variant = v; }
 void set_trace(uint64_t *d_trace) { g_trace = d_trace; }
 
 hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,
-                              hipStream_t stream) {
-    // grid < 0: non-temporal loads over |grid| workgroups (the production kernels' policy)
-    if (grid < 0)
-        hipLaunchKernelGGL(stream_read_kernel<true>, dim3(-grid), dim3(256), 0, stream, d, len / 16, sink);
+                              hipStream_t stream, bool overlap_previous) {
+    // grid < 0: non-temporal loads over |grid| workgroups (the production kernels' policy);
+    // overlap_previous: AQL packet without the barrier bit, as the overlapped verify launches
+    const bool nt = grid < 0;
+    const dim3 g(nt ? -grid : grid), b(256);
+    auto k = nt ? stream_read_kernel<true> : stream_read_kernel<false>;
+    if (overlap_previous)
+        hipExtLaunchKernelGGL(k, g, b, 0, stream, nullptr, nullptr, hipExtAnyOrderLaunch, d, len / 16, sink);
     else
-        hipLaunchKernelGGL(stream_read_kernel<false>, dim3(grid), dim3(256), 0, stream, d, len / 16, sink);
+        hipLaunchKernelGGL(k, g, b, 0, stream, d, len / 16, sink);
     return hipGetLastError();
 }
 

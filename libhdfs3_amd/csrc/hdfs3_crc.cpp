@@ -645,11 +645,18 @@ int hdfs3_memset_dev(hdfs3_crc_ctx *ctx, void *d_dst, int value, size_t bytes) {
 extern "C" {
 
 // Coalesced read-only stream over [d, d+len): the achievable HBM read ceiling.
+int hdfs3x_stream_read_ex(hdfs3_crc_ctx *ctx, const void *d, size_t len, int grid, void *d_sink, uint32_t flags);
 int hdfs3x_stream_read(hdfs3_crc_ctx *ctx, const void *d, size_t len, int grid, void *d_sink) {
+    return hdfs3x_stream_read_ex(ctx, d, len, grid, d_sink, 0);
+}
+
+// flags: HDFS3_LAUNCH_OVERLAP_PREVIOUS, for the same-shape ceiling of overlapped verifies
+int hdfs3x_stream_read_ex(hdfs3_crc_ctx *ctx, const void *d, size_t len, int grid, void *d_sink, uint32_t flags) {
     if (!ctx) return fail(-EINVAL, "null ctx");
     DeviceGuard g(ctx->device);
     HIP_TRY(launch_stream_read(static_cast<const uint8_t *>(d), len, static_cast<uint32_t *>(d_sink),
-                               grid != 0 ? grid : ctx->grid_cap * 8, ctx->stream));
+                               grid != 0 ? grid : ctx->grid_cap * 8, ctx->stream,
+                               (flags & HDFS3_LAUNCH_OVERLAP_PREVIOUS) != 0));
     return 0;
 }
 
