@@ -624,6 +624,8 @@ constexpr int kOptSlotRegion = 4096;
 //  kOptVgprFold: the lane fold as a 32-column GF(2) product in VGPRs (gf2_apply4, 64 VALU)
 //    instead of 8 nibble-table reads: trades LDS returns for VALU (§5.0).
 constexpr int kOptVgprFold = 8192;
+//  kOptNtStore: (compute) the CRC words go out as non-temporal stores.
+constexpr int kOptNtStore = 16384;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -743,6 +745,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             const bool bad = (OPT & (kOptNoHbm | kOptNoFill | kOptNoMath | kOptFakeLut)) != 0 ? __builtin_bswap32(want) == ~c
                                                                                : __builtin_bswap32(want) != c;
             if (bad) atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
+        } else if constexpr ((OPT & kOptNtStore) != 0) {
+            __builtin_nontemporal_store(__builtin_bswap32(c), reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk));
         } else {
             *reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk) = __builtin_bswap32(c);
         }
@@ -1560,6 +1564,7 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
     case 33: return launch_wave<BPC, V, 2, true, true, false, true, false, kOptWantBuf | kOptLate>(a, tab, fold, grid_cap, s);
     case 35: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptFakeLut>(a, tab, fold, grid_cap, s);
     case 40: return launch_pool<BPC, V>(a, tab, fold, grid_cap, s);
+    case 43: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNtStore>(a, tab, fold, grid_cap, s);
     case 42:
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptVgprFold | kOptWantBuf>(a, tab, fold, grid_cap,
                                                                                                    s);
