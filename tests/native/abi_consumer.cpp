@@ -133,6 +133,23 @@ int main(int argc, char **argv) {
     CHECK(hdfs3_memcpy_h2d(ctx, static_cast<uint8_t *>(d_blk) + 12345 * bpc + 7, &x, 1) == 0, "flip h2d");
     CHECK(hdfs3_crc32c_verify_dev(ctx, d_blk, blen, bpc, d_crc, 1, &bad) == 0 && bad == 12345,
           "device flip reported %lld", (long long)bad);
+    // overlapped launches (HDFS3_LAUNCH_OVERLAP_PREVIOUS): a barriered first verify after the
+    // memset, then chained ones; every result word still holds its own launch's answer
+    void *d_res4 = nullptr;
+    CHECK(hdfs3_dev_malloc(&d_res4, 32) == 0 && hdfs3_memset_dev(ctx, d_res4, 0, 32) == 0, "res4");
+    for (int i = 0; i < 4; ++i)
+        CHECK(hdfs3_crc32c_verify_dev_async_ex(ctx, d_blk, blen, bpc, d_crc, 1, static_cast<uint64_t *>(d_res4) + i,
+                                               i ? HDFS3_LAUNCH_OVERLAP_PREVIOUS : 0) == 0,
+              "verify_dev_async_ex %d", i);
+    uint64_t words[4] = {0, 0, 0, 0};
+    CHECK(hdfs3_crc_ctx_synchronize(ctx) == 0 && hdfs3_memcpy_d2h(ctx, words, d_res4, 32) == 0, "res4 d2h");
+    for (int i = 0; i < 4; ++i)
+        CHECK(hdfs3_crc_decode_result(words[i]) == 12345, "chained launch %d decoded %lld", i,
+              (long long)hdfs3_crc_decode_result(words[i]));
+    CHECK(hdfs3_crc32c_verify_dev_async_ex(ctx, d_blk, blen, bpc, d_crc, 1, static_cast<uint64_t *>(d_res4), 8u) ==
+              -EINVAL,
+          "unknown launch flag accepted");
+    hdfs3_dev_free(d_res4);
     hdfs3_dev_free(d_blk);
     hdfs3_dev_free(d_crc);
     hdfs3_dev_free(d_res);
