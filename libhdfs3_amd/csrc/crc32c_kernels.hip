@@ -1449,7 +1449,7 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         const uint64_t units = a.len / kRoundBytes;
         const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
         const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
-        if constexpr (ANY_ORDER)  // experiment (variant 16): AQL packet without the barrier bit
+        if (ANY_ORDER || a.overlap_previous)  // AQL packet without the barrier bit (variant 16, opt-in flag)
             hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
                                   dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
         else

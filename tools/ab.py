@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--reps", type=int, default=24)
     ap.add_argument("--ref", action="store_true", help="also time coalesced-read probes")
     ap.add_argument("--streams", default="1", help="comma list: launches alternate over S streams")
+    ap.add_argument("--overlap", action="store_true",
+                    help="launches after the first of each timed batch use HDFS3_LAUNCH_OVERLAP_PREVIOUS")
     args = ap.parse_args()
 
     import torch
@@ -60,7 +62,7 @@ def main():
             c = ctxs[i % ns]
             if args.mode == "verify":
                 c.verify_dev_async(data[i % blocks].data_ptr(), bb, bpc, crc[i % blocks].data_ptr(),
-                                   res.data_ptr() + 8 * (i % 4096))
+                                   res.data_ptr() + 8 * (i % 4096), overlap_previous=args.overlap and i > 0)
             else:
                 c.compute_dev(data[i % blocks].data_ptr(), bb, bpc, crc[i % blocks].data_ptr())
 
