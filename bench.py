@@ -299,6 +299,19 @@ def cpu_baseline(work, seconds, bpc):
            "sample": f"{reps} x verify of one {data.nbytes >> 20} MiB block ({bpc} B chunks, "
                      f"RemoteBlockReader::verifyChecksum loop) split over {threads} threads, {t:.1f} s; "
                      f"engine: {engine}"}
+    # the reference's production x86 engine is IntelAsmCrc32c (crc_pcl, 3-way crc32q + pclmul;
+    # needs yasm, not buildable here): time its restatement too, the stronger CPU baseline
+    if kind == "reference":
+        bad2 = ctypes.c_int64(0)
+        fp = lambda reps: oracle().oracle_bench_verify(PCL, data.ctypes.data, data.nbytes, bpc, crc.ctypes.data,
+                                                       threads, reps, ctypes.byref(bad2))
+        r2 = max(1, int(seconds / 2 / max(fp(1), 1e-6)))
+        t2 = fp(r2)
+        if bad2.value == -1:
+            out["pcl_port"] = {"value": round(data.nbytes * r2 / t2 / 2**30, 3), "unit": "GiB/s", "cores": threads,
+                               "kind": "port",
+                               "engine": "oracle crc_pcl restatement (IntelAsmCrc32c behaviour, "
+                                         "src/common/crc_iscsi_v_pcl.asm:93-340)"}
     # BASELINE.json configs[0]: one 64 KiB packet (128 x 512 B chunks) through the reference
     # CPU path on one core, 10^4 repetitions timed inside the C loop
     if ref is not None and ref.ref_hw_available():
@@ -507,6 +520,8 @@ def main():
         line["batched"] = extra["batched"]
     if cpu:
         line["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        if "pcl_port" in cpu:
+            line["gpu_over_cpu_pcl"] = round(value / cpu["pcl_port"]["value"], 1)
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
