@@ -11,7 +11,7 @@ HOSTFLAGS:= -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
 
 LIB      := $(LIBDIR)/libhdfs3_crc.so
 LOOPBACK := $(LIBDIR)/libhdfs3_loopback.so
-OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc32c.o \
+OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/crc32c_experiments.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc32c.o \
             $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/client_block_reader.o \
             $(OBJDIR)/client_input_stream.o $(OBJDIR)/client_output_stream.o \
             $(OBJDIR)/client_local_reader.o
@@ -20,7 +20,11 @@ CONSUMER := tests/native/abi_consumer
 
 all: $(LIB) $(LOOPBACK) oracle $(CONSUMER)
 
-$(OBJDIR)/crc32c_kernels.o: $(CSRC)/crc32c_kernels.hip $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
+$(OBJDIR)/crc32c_kernels.o: $(CSRC)/crc32c_kernels.hip $(CSRC)/crc32c_device.h $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/crc32c_experiments.o: $(CSRC)/crc32c_experiments.hip $(CSRC)/crc32c_device.h $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -1,0 +1,149 @@
+// Kernel variants kept for in-process A/B and diagnostics (hdfs3x_set_variant, tools/ab.py;
+// DESIGN.md §5.0). Separate translation unit so the production kernels build in parallel.
+// Bit-exact variants are parity-tested (tests/test_gpu_parity.py); the diagnostic ones
+// (no HBM / no math / fake lookups / timestamps) give wrong results on purpose.
+#include "crc32c_device.h"
+
+namespace hdfs3crc {
+namespace {
+
+template <int BPC, bool V>
+hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
+                      hipStream_t s) {
+    switch (variant) {
+    case 1: return launch_r3<BPC, V, 1, false>(a, tab, fold, grid_cap, s);   // first round kernel
+    case 2: return launch_r3<BPC, V, 1, true>(a, tab, fold, grid_cap, s);    // + bitop3 fold
+    case 3: return launch_r3<BPC, V, 2, true>(a, tab, fold, grid_cap, s);    // + 2-deep prefetch
+    case 4: return launch_wave<BPC, V, 1>(a, tab, fold, grid_cap, s);        // nibble fold, 1 chain
+    case 5: return launch_wave<BPC, V, 2, false>(a, tab, fold, grid_cap, s); // 2 chains, default-policy loads
+    case 7: return launch_wave<BPC, V, 2, true, false>(a, tab, fold, grid_cap, s);  // nt via global_load
+    case 9: {  // diagnostic: full grid, LDS fill + barrier, no rounds (per-launch fixed cost)
+        ChunkLaunch e = a;
+        e.len = 0;
+        constexpr int G = BPC <= kRoundBytes ? BPC / 64 : 64;
+        constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
+        if constexpr (BPC <= kRoundBytes)
+            hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, 1>), dim3(grid_cap), dim3(kBlockThreads), 0, s, e,
+                               tab, fold + kFoldWords + set * kFoldNibbleWords);
+        return hipGetLastError();
+    }
+    case 10:
+        hipLaunchKernelGGL(fixed_cost_kernel<10>, dim3(grid_cap), dim3(kBlockThreads), 0, s, tab, fold, nullptr);
+        return hipGetLastError();
+    case 11:
+        hipLaunchKernelGGL(fixed_cost_kernel<11>, dim3(grid_cap), dim3(kBlockThreads), 0, s, tab, fold, nullptr);
+        return hipGetLastError();
+    case 12:
+        hipLaunchKernelGGL(fixed_cost_kernel<12>, dim3(grid_cap), dim3(kBlockThreads), 0, s, tab,
+                           fold + kFoldWords, nullptr);
+        return hipGetLastError();
+    case 13: {  // diagnostic: production kernel + per-wave timestamps (tools/wave_trace.py)
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true>(e, tab, fold, grid_cap, s);
+    }
+    case 14: return launch_wave<BPC, V, 2, true, true, false, true>(a, tab, fold, grid_cap, s);  // + s_setprio
+    case 16: return launch_wave<BPC, V, 2, true, true, false, false, true>(a, tab, fold, grid_cap, s);
+    case 15: {  // 14 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, true>(e, tab, fold, grid_cap, s);
+    }
+    case 18: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptFillFirst>(a, tab, fold, grid_cap, s);
+    case 19: {  // 18 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptFillFirst>(e, tab, fold, grid_cap, s);
+    }
+    case 20: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptFillWait>(a, tab, fold, grid_cap, s);
+    case 21: {  // 20 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptFillWait>(e, tab, fold, grid_cap, s);
+    }
+    case 22: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNoHbm>(a, tab, fold, grid_cap, s);
+    case 23: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNoFill>(a, tab, fold, grid_cap, s);
+    case 24: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNoMath>(a, tab, fold, grid_cap, s);
+    case 25:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNoMath | kOptNoFill>(a, tab, fold, grid_cap, s);
+    case 26: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNibPerm | kOptWantBuf>(a, tab, fold, grid_cap, s);
+    case 27: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptPf2 | kOptWantBuf>(a, tab, fold, grid_cap, s);
+    case 28:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptPf2 | kOptNibPerm | kOptWantBuf>(a, tab, fold,
+                                                                                                       grid_cap, s);
+    case 29: {  // 28 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptPf2 | kOptNibPerm | kOptWantBuf>(e, tab, fold,
+                                                                                                      grid_cap, s);
+    }
+    case 30: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptWantBuf>(a, tab, fold, grid_cap, s);
+    case 31:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptWantBuf | kOptLate>(a, tab, fold, grid_cap, s);
+    case 32:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptWantBuf | kOptSplit>(a, tab, fold, grid_cap, s);
+    case 33: return launch_wave<BPC, V, 2, true, true, false, true, false, kOptWantBuf | kOptLate>(a, tab, fold, grid_cap, s);
+    case 35: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptFakeLut>(a, tab, fold, grid_cap, s);
+    case 40: return launch_pool<BPC, V>(a, tab, fold, grid_cap, s);
+    case 43: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNtStore>(a, tab, fold, grid_cap, s);
+    case 42:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptVgprFold | kOptWantBuf>(a, tab, fold, grid_cap,
+                                                                                                   s);
+    case 41: {  // 40 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_pool<BPC, V, true>(e, tab, fold, grid_cap, s);
+    }
+    case 36:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptSlotRegion | kOptWantBuf>(a, tab, fold, grid_cap,
+                                                                                                    s);
+    case 37: {  // 36 with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptSlotRegion | kOptWantBuf>(e, tab, fold,
+                                                                                                   grid_cap, s);
+    }
+    case 38:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptSlotRegion | kOptWantBuf | kOptNoMath>(
+            a, tab, fold, grid_cap, s);
+    case 34: {  // 24 (no table math) with timestamps
+        if (!g_trace) return hipErrorInvalidValue;
+        ChunkLaunch e = a;
+        e.trace = g_trace;
+        return launch_wave<BPC, V, 2, true, true, true, false, false, kOptNoMath>(e, tab, fold, grid_cap, s);
+    }
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int BPC>
+hipError_t launch_exp_v(int variant, const ChunkLaunch &a, bool verify, const uint32_t *tab, const uint32_t *fold,
+                        int grid_cap, hipStream_t s) {
+    return verify ? launch_exp<BPC, true>(variant, a, tab, fold, grid_cap, s)
+                  : launch_exp<BPC, false>(variant, a, tab, fold, grid_cap, s);
+}
+
+}  // namespace
+
+hipError_t launch_experiment(int variant, const ChunkLaunch &a, bool verify, const uint32_t *tab,
+                             const uint32_t *fold, int grid_cap, hipStream_t s) {
+    switch (a.bpc) {
+    case 512: return launch_exp_v<512>(variant, a, verify, tab, fold, grid_cap, s);
+    case 1024: return launch_exp_v<1024>(variant, a, verify, tab, fold, grid_cap, s);
+    case 2048: return launch_exp_v<2048>(variant, a, verify, tab, fold, grid_cap, s);
+    case 4096: return launch_exp_v<4096>(variant, a, verify, tab, fold, grid_cap, s);
+    case 8192: return launch_exp_v<8192>(variant, a, verify, tab, fold, grid_cap, s);
+    case 16384: return launch_exp_v<16384>(variant, a, verify, tab, fold, grid_cap, s);
+    case 65536: return launch_exp_v<65536>(variant, a, verify, tab, fold, grid_cap, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace hdfs3crc

@@ -78,6 +78,11 @@ hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_
 
 // Measurement knob: selects kernel variants for in-process A/B (0 = production).
 void set_variant(int v);
+extern int g_variant;
+extern uint64_t *g_trace;
+// The A/B variants (crc32c_experiments.hip): variant != 0, bpc with a whole-round kernel.
+hipError_t launch_experiment(int variant, const ChunkLaunch &a, bool verify, const uint32_t *tab,
+                             const uint32_t *fold, int grid_cap, hipStream_t s);
 void set_trace(uint64_t *d_trace);  // buffer for variant 13 (4 x u64 per wave)
 
 // Measurement-only kernels (bench/profiling): HBM read ceiling and the CRC
