@@ -327,3 +327,30 @@ def test_overlapped_verify_chain_matches_oracle(gpu_ctx, bpc):
         for i in range(nblk):
             got = gpu_ctx.decode_result(int(words[r * nblk + i]))
             assert got == (bad_chunk if i == bad_blk else -1), (r, i, got)
+
+
+def test_overlapped_chain_at_bench_size(gpu_ctx):
+    """BASELINE configs[1] size through the bench's launch mode: 8 x 128 MiB blocks verified by
+    overlapped single-block launches, three passes; a flipped bit in the LAST chunk of block 5
+    is reported in every pass, every other block is clean."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    n, nblk, passes = 128 << 20, 8, 3
+    blocks = []
+    for i in range(nblk):
+        data = splitmix_bytes(n, 0xB16 + i)
+        blocks.append((gpu_ctx.upload(data), gpu_ctx.upload(oracle_compute(data, 512)), data))
+    last = n // 512 - 1
+    pos = last * 512 + 500
+    gpu_ctx.upload(np.array([blocks[5][2][pos] ^ 1], np.uint8), blocks[5][0], offset=pos)
+    res = DeviceBuffer(8 * nblk * passes)
+    gpu_ctx.memset(res, 0, 8 * nblk * passes)
+    k = 0
+    for p in range(passes):
+        for i, (d, c, _) in enumerate(blocks):
+            gpu_ctx.verify_dev_async(d.ptr, n, 512, c.ptr, res.ptr + 8 * k, overlap_previous=k > 0)
+            k += 1
+    gpu_ctx.synchronize()
+    words = gpu_ctx.download(res, 8 * nblk * passes).view(np.uint64)
+    got = [gpu_ctx.decode_result(int(w)) for w in words]
+    assert got == [last if i % nblk == 5 else -1 for i in range(nblk * passes)]
