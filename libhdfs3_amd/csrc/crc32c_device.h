@@ -590,6 +590,23 @@ __device__ __forceinline__ uint32_t combine(const Look &l, uint32_t next) {
     return xor3(xor3(l.v[0], l.v[1], l.v[2]), l.v[3], next);
 }
 
+constexpr int kPoolFoldOff = kLdsBytes;                 // 128 KiB
+constexpr int kPoolCtrOff = kLdsBytes + 16 * 1024;      // 144 KiB
+constexpr int kPoolLdsBytes = kPoolCtrOff + 16;
+
+__device__ __forceinline__ uint32_t fold_half(const uint8_t *lds, uint32_t x) {
+    const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
+    const uint32_t fb = kPoolFoldOff + 4 * (threadIdx.x & 31);
+    auto at = [&](uint32_t src, uint32_t byte, int off) {
+        const uint32_t addr = __builtin_amdgcn_perm(src, fb, 0x0C020000u | ((4u + byte) << 8));
+        return *reinterpret_cast<const uint32_t *>(lds + addr + off);
+    };
+    const uint32_t a0 = at(lo, 0, 0), a1 = at(hi, 0, 128), a2 = at(lo, 1, 4096), a3 = at(hi, 1, 4096 + 128);
+    const uint32_t a4 = at(lo, 2, 8192), a5 = at(hi, 2, 8192 + 128), a6 = at(lo, 3, 12288);
+    const uint32_t a7 = at(hi, 3, 12288 + 128);
+    return xor3(xor3(a0, a1, a2), xor3(a3, a4, a5), a6 ^ a7);
+}
+
 // OPT bits (experiments kept for A/B, tools/ab.py):
 //  kOptFillFirst: every wave of the workgroup issues its table/fold-image loads before any
 //    wave issues data loads (s_barrier between). The CU returns loads in order, so a table
@@ -630,6 +647,10 @@ constexpr int kOptSlotRegion = 4096;
 constexpr int kOptVgprFold = 8192;
 //  kOptNtStore: (compute) the CRC words go out as non-temporal stores.
 constexpr int kOptNtStore = 16384;
+//  kOptLeanFill (bpc <= 2048): each thread loads ONE slice-table word and writes its 32
+//    copies (8 KiB of L2 reads per CU instead of 32 KiB), and the fold image is the
+//    half-size one of the pool kernel (16 KiB, one v_perm per fold address).
+constexpr int kOptLeanFill = 32768;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -682,19 +703,40 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     };
     stamp(0);
     // table + nibble-image words, then the first round(s), then the LDS fill
-    uint32_t tv[kFillPerThread];
-    fetch_tables(tv, g_tab);
-    const u32x4 n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
-    const u32x4 n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+    constexpr bool kLean = (OPT & kOptLeanFill) != 0;
+    static_assert(!kLean || G <= 32, "the half fold image needs lanes l and l + 32 to share tables");
+    uint32_t tv[kLean ? 1 : kFillPerThread];
+    u32x4 n0, n1;
+    if constexpr (kLean) {
+        const uint32_t t = threadIdx.x;
+        tv[0] = g_tab[t];  // slice t >> 8, entry t & 255
+        const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
+        n0 = *reinterpret_cast<const u32x4 *>(g_nib + (fk * 16 + fe) * 64 + fc);
+    } else {
+        fetch_tables(tv, g_tab);
+        n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
+        n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+    }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr ((OPT & kOptFillFirst) != 0) asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     auto fill = [&]() {
         if constexpr ((OPT & kOptNoFill) != 0) return;
-        store_tables(lds, tv);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * threadIdx.x;
-        dst[0] = n0;
-        dst[1] = n1;
+        if constexpr (kLean) {
+            // 32 copies of this thread's entry: 8 x b128, rotated by thread so 8 neighbouring
+            // threads (consecutive entries, 256 B apart) hit 8 different bank groups
+            const uint32_t t = threadIdx.x, slice = t >> 8, entry = t & 255;
+            u32x4 *l4 = reinterpret_cast<u32x4 *>(lds);
+            const uint32_t slot0 = ((slice >> 1) << 16 | entry << 8 | (slice & 1) << 7) / 16;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) l4[slot0 + ((r + t) & 7)] = u32x4{tv[0], tv[0], tv[0], tv[0]};
+            reinterpret_cast<u32x4 *>(lds + kPoolFoldOff / 4)[t] = n0;
+        } else {
+            store_tables(lds, tv);
+            u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * threadIdx.x;
+            dst[0] = n0;
+            dst[1] = n1;
+        }
         lds_barrier();
     };
     if constexpr ((OPT & kOptFillWait) != 0) fill();
@@ -720,6 +762,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         for (int i = 0; i < 32; ++i) col[i] = g_fold[(kFoldOff[set] + j) * 32 + i];
     }
     auto fold = [&](uint32_t x) -> uint32_t {
+        if constexpr (kLean) return fold_half(reinterpret_cast<const uint8_t *>(lds), x);
         if constexpr ((OPT & kOptVgprFold) != 0) return gf2_apply4(col, x);
         if constexpr ((OPT & kOptNibPerm) != 0) return nf.apply_perm(x);
         return nf.apply(x);
@@ -902,23 +945,6 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
 // nibble sits in address byte 1, so ONE v_perm on the nibble-spread state builds each
 // fold address; (k >> 1) * 4096 + (k & 1) * 128 rides in the ds_read offset. Then the
 // pool counter.
-constexpr int kPoolFoldOff = kLdsBytes;                 // 128 KiB
-constexpr int kPoolCtrOff = kLdsBytes + 16 * 1024;      // 144 KiB
-constexpr int kPoolLdsBytes = kPoolCtrOff + 16;
-
-__device__ __forceinline__ uint32_t fold_half(const uint8_t *lds, uint32_t x) {
-    const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
-    const uint32_t fb = kPoolFoldOff + 4 * (threadIdx.x & 31);
-    auto at = [&](uint32_t src, uint32_t byte, int off) {
-        const uint32_t addr = __builtin_amdgcn_perm(src, fb, 0x0C020000u | ((4u + byte) << 8));
-        return *reinterpret_cast<const uint32_t *>(lds + addr + off);
-    };
-    const uint32_t a0 = at(lo, 0, 0), a1 = at(hi, 0, 128), a2 = at(lo, 1, 4096), a3 = at(hi, 1, 4096 + 128);
-    const uint32_t a4 = at(lo, 2, 8192), a5 = at(hi, 2, 8192 + 128), a6 = at(lo, 3, 12288);
-    const uint32_t a7 = at(hi, 3, 12288 + 128);
-    return xor3(xor3(a0, a1, a2), xor3(a3, a4, a5), a6 ^ a7);
-}
-
 template <int BPC, bool VERIFY, bool TRACE = false>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_pool_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
