@@ -647,9 +647,9 @@ constexpr int kOptSlotRegion = 4096;
 constexpr int kOptVgprFold = 8192;
 //  kOptNtStore: (compute) the CRC words go out as non-temporal stores.
 constexpr int kOptNtStore = 16384;
-//  kOptLeanFill (bpc <= 2048): each thread loads ONE slice-table word and writes its 32
-//    copies (8 KiB of L2 reads per CU instead of 32 KiB), and the fold image is the
-//    half-size one of the pool kernel (16 KiB, one v_perm per fold address).
+//  kOptLeanFill: each thread loads ONE slice-table word and writes its 32 copies (4 KiB of
+//    L2 reads per CU instead of 32 KiB); for bpc <= 2048 the fold image is the half-size
+//    one of the pool kernel (16 KiB, one v_perm per fold address).
 constexpr int kOptLeanFill = 32768;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
@@ -704,14 +704,20 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     stamp(0);
     // table + nibble-image words, then the first round(s), then the LDS fill
     constexpr bool kLean = (OPT & kOptLeanFill) != 0;
-    static_assert(!kLean || G <= 32, "the half fold image needs lanes l and l + 32 to share tables");
+    // the half-size fold image needs lanes l and l + 32 to share fold tables (G <= 32)
+    constexpr bool kHalfFold = kLean && G <= 32;
     uint32_t tv[kLean ? 1 : kFillPerThread];
     u32x4 n0, n1;
     if constexpr (kLean) {
         const uint32_t t = threadIdx.x;
         tv[0] = g_tab[t];  // slice t >> 8, entry t & 255
-        const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
-        n0 = *reinterpret_cast<const u32x4 *>(g_nib + (fk * 16 + fe) * 64 + fc);
+        if constexpr (kHalfFold) {
+            const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
+            n0 = *reinterpret_cast<const u32x4 *>(g_nib + (fk * 16 + fe) * 64 + fc);
+        } else {
+            n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
+            n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+        }
     } else {
         fetch_tables(tv, g_tab);
         n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
@@ -730,7 +736,13 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             const uint32_t slot0 = ((slice >> 1) << 16 | entry << 8 | (slice & 1) << 7) / 16;
 #pragma unroll
             for (int r = 0; r < 8; ++r) l4[slot0 + ((r + t) & 7)] = u32x4{tv[0], tv[0], tv[0], tv[0]};
-            reinterpret_cast<u32x4 *>(lds + kPoolFoldOff / 4)[t] = n0;
+            if constexpr (kHalfFold) {
+                reinterpret_cast<u32x4 *>(lds + kPoolFoldOff / 4)[t] = n0;
+            } else {
+                u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * t;
+                dst[0] = n0;
+                dst[1] = n1;
+            }
         } else {
             store_tables(lds, tv);
             u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * threadIdx.x;
@@ -762,7 +774,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         for (int i = 0; i < 32; ++i) col[i] = g_fold[(kFoldOff[set] + j) * 32 + i];
     }
     auto fold = [&](uint32_t x) -> uint32_t {
-        if constexpr (kLean) return fold_half(reinterpret_cast<const uint8_t *>(lds), x);
+        if constexpr (kHalfFold) return fold_half(reinterpret_cast<const uint8_t *>(lds), x);
         if constexpr ((OPT & kOptVgprFold) != 0) return gf2_apply4(col, x);
         if constexpr ((OPT & kOptNibPerm) != 0) return nf.apply_perm(x);
         return nf.apply(x);

@@ -18,10 +18,10 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
     // that); an opted-in overlapped launch (HDFS3_LAUNCH_OVERLAP_PREVIOUS) goes out as an
     // AQL packet without the barrier bit (the same kernel). Non-zero variants select the
     // designs kept for in-process A/B (crc32c_experiments.hip, tools/ab.py).
-    // For bpc <= 2048 the table fill is the lean one (one slice-table word per thread, half
-    // fold image: variant 44 in the A/B, 1-1.5 % per 128 MiB launch).
+    // The table fill is the lean one (one slice-table word per thread; for bpc <= 2048 also
+    // the half fold image): variant 44 in the A/B, 1-1.5 % per 128 MiB launch.
     if (g_variant != 0) return launch_experiment(g_variant, a, V, tab, fold, grid_cap, s);
-    constexpr int kOpt = BPC <= 2048 ? kOptLeanFill : 0;
+    constexpr int kOpt = BPC <= kRoundBytes ? kOptLeanFill : 0;
     if (a.overlap_previous)
         return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
     return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
