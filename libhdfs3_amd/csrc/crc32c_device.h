@@ -1202,10 +1202,19 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
         return v;
     };
 
-    uint32_t tv[kFillPerThread];
-    fetch_tables(tv, g_tab);
-    const u32x4 n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
-    const u32x4 n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+    // lean fill (as the production wave kernel): one slice-table word per thread, replicated
+    // in LDS; for G <= 32 the half-size fold image
+    constexpr bool kHalfFold = G <= 32;
+    const uint32_t tw = g_tab[threadIdx.x];
+    u32x4 n0, n1;
+    if constexpr (kHalfFold) {
+        const uint32_t t = threadIdx.x;
+        const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
+        n0 = *reinterpret_cast<const u32x4 *>(g_nib + (fk * 16 + fe) * 64 + fc);
+    } else {
+        n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
+        n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+    }
     // views: cv* = rounds being consumed, pv* = rounds being prefetched by this step
     RoundView cv0 = view(0), cv1 = view(1);
     __builtin_amdgcn_sched_barrier(0);
@@ -1213,15 +1222,27 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
     load_round_buf<true>(b[0], cv0.p, lane_off);
     load_round_buf<true>(b[1], cv1.p, lane_off);
     __builtin_amdgcn_sched_barrier(0);
-    store_tables(lds, tv);
     {
-        u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * threadIdx.x;
-        dst[0] = n0;
-        dst[1] = n1;
+        const uint32_t tt = threadIdx.x, slice = tt >> 8, entry = tt & 255;
+        u32x4 *l4 = reinterpret_cast<u32x4 *>(lds);
+        const uint32_t slot0 = ((slice >> 1) << 16 | entry << 8 | (slice & 1) << 7) / 16;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) l4[slot0 + ((r + tt) & 7)] = u32x4{tw, tw, tw, tw};
+        if constexpr (kHalfFold) {
+            reinterpret_cast<u32x4 *>(lds + kPoolFoldOff / 4)[tt] = n0;
+        } else {
+            u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * tt;
+            dst[0] = n0;
+            dst[1] = n1;
+        }
     }
     lds_barrier();
     const Lut t(lds);
     const NibFold nf(lds);
+    auto fold = [&](uint32_t x) -> uint32_t {
+        if constexpr (kHalfFold) return fold_half(reinterpret_cast<const uint8_t *>(lds), x);
+        return nf.apply(x);
+    };
     const uint32_t init = j == 0 ? 0xFFFFFFFFu : 0u;
     RoundView pv0 = view(2), pv1 = view(3);
 
@@ -1275,8 +1296,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
             x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
             __builtin_amdgcn_sched_barrier(0);
         }
-        finish(k, cv0, group_xor<G>(nf.apply(x0)), w0);
-        finish(k + 1, cv1, group_xor<G>(nf.apply(x1)), w1);
+        finish(k, cv0, group_xor<G>(fold(x0)), w0);
+        finish(k + 1, cv1, group_xor<G>(fold(x1)), w1);
         __builtin_amdgcn_sched_barrier(0);
         cv0 = pv0;
         cv1 = pv1;
