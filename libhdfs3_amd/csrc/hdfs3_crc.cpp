@@ -143,9 +143,9 @@ bool is_pinned_host(const void *p) {
 // Host-buffer pipeline shared by compute and verify: segments of whole chunks
 // alternate between two pinned/device slots, so the CPU copy into pinned memory
 // of segment i+1 overlaps the DMA and kernel of segment i.
-int host_pipeline(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc,
-                  const void *crc_in, void *crc_out, int check_short_tail,
-                  int64_t *first_bad) {
+int host_pipeline_impl(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc,
+                       const void *crc_in, void *crc_out, int check_short_tail,
+                       int64_t *first_bad) {
     const bool verify = crc_in != nullptr;
     const size_t seg = (kSegmentBytes / bpc > 0 ? kSegmentBytes / bpc : 1) * size_t(bpc);
     const size_t seg_crc = (seg / bpc) * 4;
@@ -198,6 +198,19 @@ int host_pipeline(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc
         if (int rc = finish_pending(s)) return rc;
     if (verify && first_bad) *first_bad = hdfs3_crc_decode_result(*ctx->h_result);
     return 0;
+}
+
+int host_pipeline(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc,
+                  const void *crc_in, void *crc_out, int check_short_tail,
+                  int64_t *first_bad) {
+    const int rc = host_pipeline_impl(ctx, data, len, bpc, crc_in, crc_out, check_short_tail, first_bad);
+    if (rc != 0) {
+        // a failed call must not leave CRC words queued for a caller buffer it no longer
+        // owns: the next call would copy them out in finish_pending
+        (void)hipStreamSynchronize(ctx->stream);
+        for (Slot &sl : ctx->slot) sl.pending_out = nullptr;
+    }
+    return rc;
 }
 
 int packets_common(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len,
