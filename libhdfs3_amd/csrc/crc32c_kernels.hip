@@ -155,12 +155,22 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    for (size_t i = 0; i < n; ++i)
-        h_stage[i] = DevSegment{d_arena + h_pk[i].data_off, const_cast<uint8_t *>(d_arena) + h_pk[i].crc_off,
-                                h_pk[i].data_len, 0, uint64_t(i) << 32};
-    if (g_variant != 17 && segments_fast(h_stage, n, bpc)) {
-        uint64_t uniform = 0;
-        const uint64_t units = plan_segments(h_stage, n, &uniform);
+    // one pass: descriptors, the alignment test of segments_fast and the unit plan of
+    // plan_segments (16K packets per GiB: the host loop is on the call's critical path)
+    bool fast = g_variant != 17 && (bpc == 512 || bpc == 1024 || bpc == 2048 || bpc == 4096);
+    uint64_t units = 0, u0 = h_pk[0].data_len / kRoundBytes;
+    bool same = true;
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t *data = d_arena + h_pk[i].data_off;
+        uint8_t *crc = const_cast<uint8_t *>(d_arena) + h_pk[i].crc_off;
+        const uint64_t u = h_pk[i].data_len / kRoundBytes;
+        fast = fast && ((reinterpret_cast<uintptr_t>(data) & 15u) | (reinterpret_cast<uintptr_t>(crc) & 3u)) == 0;
+        if (i + 1 < n && u != u0) same = false;
+        h_stage[i] = DevSegment{data, crc, h_pk[i].data_len, units, uint64_t(i) << 32};
+        units += u;
+    }
+    if (fast) {
+        const uint64_t uniform = same && u0 > 0 ? u0 : 0;
         if (n > kInlineSegments) {
             hipError_t e = hipMemcpyAsync(d_stage, h_stage, n * sizeof(DevSegment), hipMemcpyHostToDevice, stream);
             if (e != hipSuccess) return e;

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
+#include <cstddef>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -213,6 +214,11 @@ int host_pipeline(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_t bpc
     return rc;
 }
 
+static_assert(sizeof(hdfs3_pkt_desc) == sizeof(DevPacket) && offsetof(hdfs3_pkt_desc, data_off) == offsetof(DevPacket, data_off) &&
+                  offsetof(hdfs3_pkt_desc, crc_off) == offsetof(DevPacket, crc_off) &&
+                  offsetof(hdfs3_pkt_desc, data_len) == offsetof(DevPacket, data_len),
+              "the packets API hands descriptors to the kernels unconverted");
+
 int packets_common(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len,
                    const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc, bool verify,
                    int check_short_tail, int64_t *bad_packet, int64_t *bad_chunk) {
@@ -226,10 +232,10 @@ int packets_common(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len,
     if (int rc = grow_pk(ctx, n)) return rc;
     // the previous call's descriptors may still be in flight from h_pk
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    std::vector<DevPacket> hp(n);
-    for (size_t i = 0; i < n; ++i) hp[i] = DevPacket{pk[i].data_off, pk[i].crc_off, pk[i].data_len, 0};
+    // hdfs3_pkt_desc and DevPacket share one layout (asserted below): no conversion copy
+    const DevPacket *hp = reinterpret_cast<const DevPacket *>(pk);
     if (verify) HIP_TRY(hipMemsetAsync(ctx->d_result, 0, sizeof(unsigned long long), ctx->stream));
-    HIP_TRY(launch_packet_batch(d_arena, hp.data(), n, bpc, verify, check_short_tail, ctx->d_result, ctx->h_pk,
+    HIP_TRY(launch_packet_batch(d_arena, hp, n, bpc, verify, check_short_tail, ctx->d_result, ctx->h_pk,
                                 ctx->d_pk, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
     ++ctx->launches;
     if (verify) {
