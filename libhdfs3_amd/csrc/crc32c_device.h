@@ -989,8 +989,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_pool_kernel(ChunkLaunch 
         }
     };
     stamp(0);
-    uint32_t tv[kFillPerThread];
-    fetch_tables(tv, g_tab);
+    const uint32_t tw = g_tab[threadIdx.x];  // lean fill: one slice-table word per thread
     // half fold image: this thread's 4 LDS words w = 4 * tid
     const uint32_t t = threadIdx.x;
     const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
@@ -1004,7 +1003,13 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_pool_kernel(ChunkLaunch 
     __builtin_amdgcn_sched_barrier(0);
     load_round_buf<true>(b[1], round_ptr(unit_of(ic + 1)), lane_off);
     __builtin_amdgcn_sched_barrier(0);
-    store_tables(lds, tv);
+    {
+        const uint32_t slice = t >> 8, entry = t & 255;
+        u32x4 *l4 = reinterpret_cast<u32x4 *>(lds);
+        const uint32_t slot0 = ((slice >> 1) << 16 | entry << 8 | (slice & 1) << 7) / 16;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) l4[slot0 + ((r + t) & 7)] = u32x4{tw, tw, tw, tw};
+    }
     reinterpret_cast<u32x4 *>(lds + kPoolFoldOff / 4)[t] = nv;
     if (t == 0) *ctr = 64;
     lds_barrier();
@@ -1530,8 +1535,12 @@ hipError_t launch_pool(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         const uint64_t units = a.len / kRoundBytes;
         const uint64_t need = (units + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock);
         const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
-        hipLaunchKernelGGL((crc32c_pool_kernel<BPC, V, TRACE>), dim3(grid > 0 ? grid : 1), dim3(kBlockThreads), 0, s, a,
-                           tab, nib);
+        if (a.overlap_previous)
+            hipExtLaunchKernelGGL((crc32c_pool_kernel<BPC, V, TRACE>), dim3(grid > 0 ? grid : 1), dim3(kBlockThreads), 0,
+                                  s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+        else
+            hipLaunchKernelGGL((crc32c_pool_kernel<BPC, V, TRACE>), dim3(grid > 0 ? grid : 1), dim3(kBlockThreads), 0, s,
+                               a, tab, nib);
         return hipGetLastError();
     }
 }
