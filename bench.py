@@ -401,11 +401,13 @@ def main():
 
     K, W = args.steps, args.warmup
     result = torch.zeros(max(K, W, 1), dtype=torch.int64, device=device)
-    # (0) diagnostic pass, before the warmup: the same K launches eagerly, each bracketed by
-    # HIP events on the launch stream (per-launch duration including dispatch). Running it
-    # first also takes the GPU out of its idle power state (~25 ms of load)
-    events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
-    run_steps(work, ctx, args.mode, K, result, events)
+    # (0) diagnostic pass, before the warmup: max(K, 2000) launches eagerly, each bracketed
+    # by HIP events on the launch stream (per-launch duration including dispatch, averaged
+    # over the last K). Running it first also takes the GPU out of its idle power state
+    # (~25 ms of load), so short --warmup values still time a steady GPU
+    D = max(K, 2000)
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * D)]
+    run_steps(work, ctx, args.mode, D, result, events)
     torch.cuda.synchronize()
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the roofline pass")
@@ -436,8 +438,8 @@ def main():
         elapsed = max_over_ranks(dist, elapsed, coll_device)
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the timed region")
-    launch_ms = [events[2 * s].elapsed_time(events[2 * s + 1]) for s in range(K)]
-    eager_launch_s = sum(launch_ms) / K * 1e-3
+    launch_ms = [events[2 * s].elapsed_time(events[2 * s + 1]) for s in range(D)]
+    eager_launch_s = sum(launch_ms[-K:]) / K * 1e-3  # the last K of the diagnostic pass
     avg_launch_s = region_launch_s
     payload = block_bytes
     alg_bytes = work.nchunks * (args.bpc + 4)  # verify reads data + CRC; compute reads data, writes CRC
