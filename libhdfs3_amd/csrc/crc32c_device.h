@@ -651,6 +651,8 @@ constexpr int kOptNtStore = 16384;
 //    L2 reads per CU instead of 32 KiB); for bpc <= 2048 the fold image is the half-size
 //    one of the pool kernel (16 KiB, one v_perm per fold address).
 constexpr int kOptLeanFill = 32768;
+//  kOptNoStore (diagnostic only, wrong results): compute mode skips its CRC-word stores.
+constexpr int kOptNoStore = 65536;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -804,6 +806,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             const bool bad = (OPT & (kOptNoHbm | kOptNoFill | kOptNoMath | kOptFakeLut)) != 0 ? __builtin_bswap32(want) == ~c
                                                                                : __builtin_bswap32(want) != c;
             if (bad) atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
+        } else if constexpr ((OPT & kOptNoStore) != 0) {
+            if (c == 0x9E3779B9u) *reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk) = c;
         } else if constexpr ((OPT & kOptNtStore) != 0) {
             __builtin_nontemporal_store(__builtin_bswap32(c), reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk));
         } else {

@@ -91,6 +91,9 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
     case 35: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptFakeLut>(a, tab, fold, grid_cap, s);
     case 40: return launch_pool<BPC, V>(a, tab, fold, grid_cap, s);
     case 44: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill>(a, tab, fold, grid_cap, s);
+    case 45:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptNoStore>(a, tab, fold,
+                                                                                                    grid_cap, s);
     case 43: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNtStore>(a, tab, fold, grid_cap, s);
     case 42:
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptVgprFold | kOptWantBuf>(a, tab, fold, grid_cap,

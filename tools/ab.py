@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--reps", type=int, default=24)
     ap.add_argument("--ref", action="store_true", help="also time coalesced-read probes")
     ap.add_argument("--streams", default="1", help="comma list: launches alternate over S streams")
+    ap.add_argument("--block-mib", type=int, default=128)
+    ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--overlap", action="store_true",
                     help="launches after the first of each timed batch use HDFS3_LAUNCH_OVERLAP_PREVIOUS")
     args = ap.parse_args()
@@ -42,7 +44,7 @@ def main():
         c.set_stream(st.cuda_stream)
     ctx = ctxs[0]
     torch.cuda.set_stream(streams[0])
-    blocks, bb = 8, 128 << 20
+    blocks, bb = args.blocks, args.block_mib << 20
     data = torch.randint(0, 256, (blocks, bb), dtype=torch.uint8, device=dev)
     sink = torch.zeros(16, dtype=torch.int32, device=dev)
     res = torch.zeros(4096, dtype=torch.int64, device=dev)
