@@ -181,3 +181,168 @@ def test_dropped_connection_and_dead_node_fail_over(cluster):
             assert s.stats()["failovers"] == 2
     finally:
         flaky.stop()
+
+
+# --- the reference's own function-test shape (test/function/TestInputStream.cpp) -------------
+# Files hold the FillBuffer "012345678\n" pattern and are written with 1 KiB packets
+# (TestInputStream.cpp:62 output.default.packetsize=1024), so every read-path packet carries
+# two 512 B chunks; reads are checked with CheckBuffer at their file offset.
+
+def _fill_cluster(sizes, packet_bytes, base_id, bpc=BPC):
+    from loopback import LoopbackDatanode
+
+    from util import fill_buffer
+
+    node = LoopbackDatanode(packet_bytes=packet_bytes)
+    blocks, off = [], 0
+    for i, n in enumerate(sizes):
+        d = fill_buffer(n, off)
+        node.add_block(base_id + i, d, oracle_compute(d, bpc), bpc)
+        blocks.append((base_id + i, n))
+        off += n
+    return node, blocks
+
+
+@pytest.mark.parametrize("packet_bytes", [1024, 512, 1536])
+def test_reference_checksum_read_pattern_1k_packets(packet_bytes):
+    """TestInputStream.cpp:126-154 CheckSum: reads of size, size-100 and size+100 bytes at a
+    running offset, each checked against FillBuffer; 40 KiB file (largefile, :97-101) split
+    into 2 KiB blocks so reads cross block boundaries the way readOneBlock cuts them."""
+    from util import fill_buffer
+
+    total = 20 * 2048
+    node, blocks = _fill_cluster([2048] * 20, packet_bytes, 700)
+    try:
+        with _stream(blocks, [("127.0.0.1", node.port)]) as s:
+            pos = 0
+            for want in [1024, 924, 1124] * 40:
+                if pos >= total:
+                    break
+                buf = np.zeros(want, np.uint8)
+                got = 0
+                while got < want and pos + got < total:  # readFully over block cuts
+                    n = s.read_into(buf, got, want - got)
+                    assert n > 0
+                    got += n
+                assert np.array_equal(buf[:got], fill_buffer(got, pos))
+                pos += got
+            assert pos == total and s.read_into(np.zeros(8, np.uint8)) == 0
+            assert s.stats()["failovers"] == 0
+    finally:
+        node.stop()
+
+
+@pytest.mark.parametrize("size", [512, 1024, 2048])
+def test_reference_read_fully_sizes(size):
+    """TestInputStream.cpp:194-205 ReadFully(size), (size-100), (size+100) from offset 0 of a
+    file served in 1 KiB packets; the short last chunk is verified too."""
+    from util import fill_buffer
+
+    node, blocks = _fill_cluster([size + 100], 1024, 760)
+    try:
+        for n in (size, size - 100, size + 100):
+            with _stream(blocks, [("127.0.0.1", node.port)]) as s:
+                got = s.read_fully(n)
+                assert np.array_equal(got, fill_buffer(n, 0))
+    finally:
+        node.stop()
+
+
+def test_reference_checksum_corruption_1k_packets():
+    """A flipped byte inside a 1 KiB packet: the corrupt replica raises the ChecksumException
+    path (failover to the good replica, RemoteBlockReader.cpp:306-326 -> InputStreamImpl.cpp
+    :682-708); with the corrupt replica alone the read fails with EIO after the good bytes."""
+    from libhdfs3_amd.engine import HdfsIOError
+    from loopback import LoopbackDatanode
+
+    from util import fill_buffer
+
+    total = 64 << 10
+    good, blocks = _fill_cluster([total], 1024, 780)
+    bad = LoopbackDatanode(packet_bytes=1024)
+    try:
+        d = fill_buffer(total, 0)
+        c = oracle_compute(d, BPC)
+        d = d.copy()
+        d[40_000] ^= 0x01  # chunk 78, packet 39
+        bad.add_block(780, d, c, BPC)
+        with _stream(blocks, [("127.0.0.1", bad.port), ("127.0.0.1", good.port)]) as s:
+            assert np.array_equal(s.read_fully(total, chunk=3000), fill_buffer(total, 0))
+            assert s.stats()["failovers"] == 1
+        with _stream(blocks, [("127.0.0.1", bad.port)]) as s:
+            out = np.zeros(total, np.uint8)
+            pos = 0
+            with pytest.raises(HdfsIOError) as ei:
+                while True:
+                    n = s.read_into(out, pos, 3000)
+                    assert n > 0
+                    pos += n
+            assert ei.value.errno == errno.EIO
+            assert pos <= 78 * BPC and np.array_equal(out[:pos], fill_buffer(pos, 0))
+    finally:
+        good.stop()
+        bad.stop()
+
+
+def _check_file_content(blocks, port, length, errors):
+    """TestInputStream.cpp:256-273 CheckFileContent: 20 KiB + 1 reads, CheckBuffer each."""
+    from util import fill_buffer
+
+    try:
+        with _stream(blocks, [("127.0.0.1", port)]) as s:
+            buf = np.zeros(20 * 1024 + 1, np.uint8)
+            off = 0
+            while off < length:
+                n = s.read_into(buf, 0, min(buf.nbytes, length - off))
+                assert n > 0
+                if not np.array_equal(buf[:n], fill_buffer(n, off)):
+                    errors.append(f"mismatch at {off}")
+                    return
+                off += n
+    except Exception as e:  # noqa: BLE001 - collected and asserted by the caller
+        errors.append(repr(e))
+
+
+def test_reference_read_one_file_same_time():
+    """TestInputStream.cpp:299-319 TestReadOneFileSameTime (scaled: 16 threads instead of 50,
+    an 8 MiB + 234 B file instead of 1 GiB): concurrent streams, each with its own engine
+    context, read the first 1 MiB + 234 B of one file through 1 KiB packets."""
+    import threading
+
+    size = (8 << 20) + 234
+    node, blocks = _fill_cluster([4 << 20, 4 << 20, 234], 1024, 800)
+    errors: list = []
+    try:
+        ts = [threading.Thread(target=_check_file_content, args=(blocks, node.port, (1 << 20) + 234, errors))
+              for _ in range(16)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=100)
+        assert not any(t.is_alive() for t in ts), "reader thread hung"
+        assert not errors, errors[:3]
+        assert sum(n for _, n in blocks) == size
+    finally:
+        node.stop()
+
+
+def test_reference_read_many_files_same_time():
+    """TestInputStream.cpp:321-342 TestReadManyFileSameTime (scaled: 8 files of 2 MiB + 234 B
+    on separate datanodes, one thread per file)."""
+    import threading
+
+    nodes, errors = [], []
+    try:
+        for i in range(8):
+            nodes.append(_fill_cluster([1 << 20, (1 << 20) + 234], 1024, 900 + 10 * i))
+        ts = [threading.Thread(target=_check_file_content, args=(blocks, node.port, (1 << 20) + 234, errors))
+              for node, blocks in nodes]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=100)
+        assert not any(t.is_alive() for t in ts), "reader thread hung"
+        assert not errors, errors[:3]
+    finally:
+        for node, _ in nodes:
+            node.stop()

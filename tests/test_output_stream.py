@@ -63,6 +63,7 @@ def random_ops(rng, total, flush_p=0.1):
 @pytest.mark.parametrize("bpc,packet_size,block_size,batch", [
     (512, 65536, 64 << 20, 64),      # reference defaults
     (512, 65536, 1 << 20, 3),        # block boundaries every 16 packets, small batches
+    (512, 1024, 1 << 20, 64),        # function-test shape: 1 KiB packets (TestOutputStream.cpp:86)
     (4096, 65536, 2 << 20, 64),
     (2048, 4096, 256 << 10, 1),      # one chunk-ish per packet, one packet per GPU batch
     (100, 1000, 100 * 37, 5),        # odd chunk size, ragged everything
