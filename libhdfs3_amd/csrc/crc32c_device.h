@@ -653,6 +653,11 @@ constexpr int kOptNtStore = 16384;
 constexpr int kOptLeanFill = 32768;
 //  kOptNoStore (diagnostic only, wrong results): compute mode skips its CRC-word stores.
 constexpr int kOptNoStore = 65536;
+//  kOptLineStore: (compute, bpc 512) a wave takes 4 consecutive rounds (16 KiB, 32 chunks)
+//    per visit and stores their 32 CRC words as ONE full 128-B line from lanes 0..31, instead
+//    of one 32-B partial line per round. The words are transposed into lane order by one
+//    ds_bpermute per round.
+constexpr int kOptLineStore = 131072;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -675,7 +680,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                           __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // this wave's rounds: unit first + k * stride for k < K
     uint64_t first = wave, stride = nwaves, K;
-    if constexpr ((OPT & kOptSlotRegion) != 0) {
+    constexpr bool kLine = !VERIFY && (OPT & kOptLineStore) != 0 && G == 8 && PAIR == 2 && (OPT & kOptPf2) == 0;
+    // kLine: round k of the wave is unit 4 * (first + (k >> 2) * stride) + (k & 3)
+    auto unit_of = [&](uint64_t k) -> uint64_t {
+        if constexpr (kLine) return 4 * (first + (k >> 2) * stride) + (k & 3);
+        return first + k * stride;
+    };
+    if constexpr (kLine) {
+        const uint64_t nsup = (nunits + 3) / 4;
+        K = wave < nsup ? 4 * ((nsup - wave + nwaves - 1) / nwaves) : 0;
+    } else if constexpr ((OPT & kOptSlotRegion) != 0) {
         const uint64_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const uint64_t R = (nunits + kWavesPerBlock - 1) / kWavesPerBlock;
         const uint64_t lo = slot * R, hi = lo + R < nunits ? lo + R : nunits;
@@ -691,6 +705,11 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     // would, since the non-temporal stream is not kept in L2).
     auto round_ptr = [&](uint64_t k) -> const uint8_t * {
         if constexpr ((OPT & kOptNoHbm) != 0) return reinterpret_cast<const uint8_t *>(g_tab);
+        if constexpr (kLine) {
+            // the wave's last visit may hold fewer than 4 rounds
+            const uint64_t u = unit_of(k);
+            return k < K && u < nunits ? a.data + u * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
+        }
         return k < K ? a.data + (first + k * stride) * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
     };
 
@@ -798,7 +817,21 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         }
         return 0;
     };
+    uint32_t line = 0;  // kLine: lane q (< 32) collects word q of the visit's 32 chunks
     auto finish = [&](uint64_t k, uint32_t y, uint32_t want) {
+        if constexpr (kLine) {
+            // every lane of group c holds chunk c's state (group_xor is a butterfly); lane
+            // 8r + c takes chunk c of round r
+            const uint32_t r = uint32_t(k & 3);
+            const uint32_t v = uint32_t(__builtin_amdgcn_ds_bpermute(int(32 * (lane & 7)), int(y)));
+            line = (lane >> 3) == r ? v : line;
+            if (r == 3) {
+                const uint64_t u0 = unit_of(k - 3);
+                if (lane < 32 && u0 + (lane >> 3) < nunits)
+                    *reinterpret_cast<uint32_t *>(a.out_be + 4 * (u0 * kChunksPerUnit + lane)) = __builtin_bswap32(~line);
+            }
+            return;
+        }
         if (k >= K || j != 0) return;
         const uint64_t chunk = (first + k * stride) * kChunksPerUnit + lane / G;
         const uint32_t c = ~y;
