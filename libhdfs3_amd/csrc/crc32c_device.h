@@ -658,6 +658,10 @@ constexpr int kOptNoStore = 65536;
 //    of one 32-B partial line per round. The words are transposed into lane order by one
 //    ds_bpermute per round.
 constexpr int kOptLineStore = 131072;
+//  kOptHoldStore: (compute, bpc 512) batch the CRC-word stores in time: a wave transposes
+//    each 8 rounds' 64 words into one VGPR (lane 8r + c = chunk c of round r) and keeps up
+//    to 8 such VGPRs (64 rounds), storing them only when full and at the end of its stream.
+constexpr int kOptHoldStore = 262144;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -818,7 +822,38 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         return 0;
     };
     uint32_t line = 0;  // kLine: lane q (< 32) collects word q of the visit's 32 chunks
+    constexpr bool kHold = !VERIFY && !kLine && (OPT & kOptHoldStore) != 0 && G == 8 &&
+                           (OPT & kOptSlotRegion) == 0;
+    uint32_t hold[kHold ? 8 : 1];  // hold[i] = octet hold_base + nheld - 1 - i
+    uint32_t nheld = 0;
+    uint64_t hold_base = 0;
+    auto flush = [&]() {
+#pragma unroll
+        for (int i = 0; i < (kHold ? 8 : 0); ++i) {
+            if (uint32_t(i) < nheld) {
+                const uint64_t k = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
+                if (k < K)
+                    *reinterpret_cast<uint32_t *>(a.out_be + 4 * ((first + k * stride) * kChunksPerUnit + (lane & 7))) =
+                        __builtin_bswap32(~hold[i]);
+            }
+        }
+        hold_base += nheld;
+        nheld = 0;
+    };
     auto finish = [&](uint64_t k, uint32_t y, uint32_t want) {
+        if constexpr (kHold) {
+            if (k >= K) return;
+            const uint32_t r = uint32_t(k & 7);
+            const uint32_t v = uint32_t(__builtin_amdgcn_ds_bpermute(int(32 * (lane & 7)), int(y)));
+            line = (lane >> 3) == r ? v : line;
+            if (r == 7 || k + 1 == K) {
+#pragma unroll
+                for (int i = (kHold ? 7 : 0); i > 0; --i) hold[i] = hold[i - 1];
+                hold[0] = line;
+                if (++nheld == 8) flush();
+            }
+            return;
+        }
         if constexpr (kLine) {
             // every lane of group c holds chunk c's state (group_xor is a butterfly); lane
             // 8r + c takes chunk c of round r
@@ -955,6 +990,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             }
         }
     }
+    if constexpr (kHold) flush();
     stamp(3);
 
     // slow region: chunks after the last whole round, plus the short tail chunk

@@ -19,9 +19,11 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
     // AQL packet without the barrier bit (the same kernel). Non-zero variants select the
     // designs kept for in-process A/B (crc32c_experiments.hip, tools/ab.py).
     // The table fill is the lean one (one slice-table word per thread; for bpc <= 2048 also
-    // the half fold image): variant 44 in the A/B, 1-1.5 % per 128 MiB launch.
+    // the half fold image): variant 44 in the A/B, 1-1.5 % per 128 MiB launch. Compute at
+    // bpc 512 holds its CRC words in VGPRs and stores them in bursts (variant 47: -2.8 % per
+    // GiB, -0.8 % per 128 MiB; profiles/r01_kernel_study/ab_holdstore.jsonl).
     if (g_variant != 0) return launch_experiment(g_variant, a, V, tab, fold, grid_cap, s);
-    constexpr int kOpt = BPC <= kRoundBytes ? kOptLeanFill : 0;
+    constexpr int kOpt = (BPC <= kRoundBytes ? kOptLeanFill : 0) | (!V && BPC == 512 ? kOptHoldStore : 0);
     if (a.overlap_previous)
         return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
     return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
