@@ -100,6 +100,9 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
     case 47:
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptHoldStore>(a, tab, fold,
                                                                                                       grid_cap, s);
+    case 48:
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptNibPerm>(a, tab, fold, grid_cap,
+                                                                                                    s);
     case 43: return launch_wave<BPC, V, 2, true, true, false, false, false, kOptNtStore>(a, tab, fold, grid_cap, s);
     case 42:
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptVgprFold | kOptWantBuf>(a, tab, fold, grid_cap,

@@ -4,7 +4,8 @@
             the host-buffer API (H2D + kernel + result) and the packets API; the reference CPU
             timing of the same packet is bench.py's cpu_baseline.config0_packet_us
   config 2  1 GiB synthetic stream, compute (write) and verify (read) at bpc 512 / 2048 / 4096,
-            one launch each, HIP-event timed, plus the compute -> verify round trip and a flip
+            after a 200-launch ramp, HIP events around batches of 5 back-to-back launches (median
+            of 10), plus the compute -> verify round trip and a flip
 Prints one JSON line per measurement."""
 import json
 import os
@@ -35,17 +36,28 @@ def main():
         nch = n // bpc
         crc = torch.empty(4 * nch, dtype=torch.uint8, device=dev)
         times = {"compute": [], "verify": []}
-        for rep in range(6):
-            for mode in ("compute", "verify"):
+
+        def launch(mode, i):
+            if mode == "compute":
+                ctx.compute_dev(data.data_ptr(), n, bpc, crc.data_ptr())
+            else:
+                ctx.verify_dev_async(data.data_ptr(), n, bpc, crc.data_ptr(), res.data_ptr() + 8 * (i % 64))
+
+        launch("compute", 0)
+        # the GPU needs ~25 ms of sustained load to leave its idle power state:
+        # ramp with back-to-back launches, then time batches of BATCH back-to-back launches
+        BATCH = 5
+        for mode in ("compute", "verify"):
+            for i in range(200):
+                launch(mode, i)
+            for rep in range(10):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
-                if mode == "compute":
-                    ctx.compute_dev(data.data_ptr(), n, bpc, crc.data_ptr())
-                else:
-                    ctx.verify_dev_async(data.data_ptr(), n, bpc, crc.data_ptr(), res.data_ptr() + 8 * rep)
+                for i in range(BATCH):
+                    launch(mode, i)
                 e1.record(st)
-                torch.cuda.synchronize()
-                times[mode].append(e0.elapsed_time(e1) * 1e-3)
+                e1.synchronize()
+                times[mode].append(e0.elapsed_time(e1) * 1e-3 / BATCH)
         assert int(res.abs().sum()) == 0, "round trip: verify of freshly computed words failed"
         pos = n // 3 + 5
         orig = int(data[pos].item())
@@ -56,7 +68,7 @@ def main():
         torch.cuda.synchronize()
         assert first == pos // bpc, (first, pos // bpc)
         for mode in ("compute", "verify"):
-            t = statistics.median(times[mode][1:])
+            t = statistics.median(times[mode])
             alg = nch * (bpc + 4)  # verify: data + words read; compute: data read + words written
             print(json.dumps({"bench": "config2_stream", "bpc": bpc, "mode": mode, "bytes": n,
                               "us": round(t * 1e6, 1), "GiBps_payload": round(n / t / 2**30, 1),
