@@ -222,6 +222,8 @@ static_assert(sizeof(hdfs3_pkt_desc) == sizeof(DevPacket) && offsetof(hdfs3_pkt_
 int packets_common(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len,
                    const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc, bool verify,
                    int check_short_tail, int64_t *bad_packet, int64_t *bad_chunk) {
+    // the result key is (packet << 32 | chunk)
+    if (n >= (size_t(1) << 31)) return fail(-EINVAL, "too many packets in one batch");
     for (size_t i = 0; i < n; ++i) {
         const hdfs3_pkt_desc &d = pk[i];
         const uint64_t chunks = (uint64_t(d.data_len) + bpc - 1) / bpc;
