@@ -17,8 +17,9 @@ OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/crc32c_experiments.o $(OBJDIR)/
             $(OBJDIR)/client_local_reader.o
 
 CONSUMER := tests/native/abi_consumer
+CLIENT_CONSUMER := tests/native/client_consumer
 
-all: $(LIB) $(LOOPBACK) oracle $(CONSUMER)
+all: $(LIB) $(LOOPBACK) oracle $(CONSUMER) $(CLIENT_CONSUMER)
 
 $(OBJDIR)/crc32c_kernels.o: $(CSRC)/crc32c_kernels.hip $(CSRC)/crc32c_device.h $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
 	@mkdir -p $(OBJDIR)
@@ -75,12 +76,19 @@ $(CONSUMER): tests/native/abi_consumer.cpp include/hdfs3_crc.h oracle/crc32c_ora
 	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ tests/native/abi_consumer.cpp $(OBJDIR)/consumer_oracle.o \
 	    -L$(LIBDIR) -lhdfs3_crc -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath-link,/opt/rocm/lib -pthread
 
+# test infrastructure: a C++ consumer of the client drop-ins (include/hdfs3_client.h) over the
+# loopback datanode, in the reference function tests' shape
+$(CLIENT_CONSUMER): tests/native/client_consumer.cpp include/hdfs3_client.h $(CONSUMER) $(LIB) $(LOOPBACK)
+	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ tests/native/client_consumer.cpp $(OBJDIR)/consumer_oracle.o \
+	    -L$(LIBDIR) -lhdfs3_crc -lhdfs3_loopback -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath-link,/opt/rocm/lib \
+	    -pthread
+
 oracle:
 	$(MAKE) -C oracle all
 	@if [ -d /root/reference/src/common ]; then $(MAKE) -C oracle ref; fi
 
 clean:
-	rm -rf build $(LIB) $(LOOPBACK) $(CONSUMER)
+	rm -rf build $(LIB) $(LOOPBACK) $(CONSUMER) $(CLIENT_CONSUMER)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -32,3 +32,20 @@ def test_cpp_consumer_on_gpu():
     r = _run()
     assert r.returncode == 0, r.stdout + r.stderr
     assert "abi_consumer ok" in r.stdout
+
+
+CLIENT_BIN = os.path.join(REPO, "tests", "native", "client_consumer")
+
+
+@pytest.mark.gpu
+def test_cpp_client_consumer_round_trip_on_gpu():
+    """tests/native/client_consumer.cpp: hdfs3_output_* writes FillBuffer data in 1 KiB
+    packets (GPU CRCs checked against the oracle packet by packet), loopback datanodes serve
+    the blocks with those words, hdfs3_input_* reads them back (CheckBuffer in 20 KiB + 1
+    reads, pread across a block boundary, one failover off a corrupt replica, EOVERFLOW past
+    EOF, EIO when every replica is bad)."""
+    if not os.path.exists(CLIENT_BIN):
+        pytest.fail("tests/native/client_consumer not built (run `make`)")
+    r = subprocess.run([CLIENT_BIN], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "client_consumer ok" in r.stdout
