@@ -184,6 +184,23 @@ def test_full_size_stream_1gib_roundtrip(gpu_ctx, bpc):
     assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, True) == -1
 
 
+@pytest.mark.parametrize("n", [(1 << 30) + (3 << 20) + 4096 * 5 + 300, (2 << 30) + 4096 * 13 + 4096 - 1])
+def test_compute_held_stores_past_64_rounds_per_wave(gpu_ctx, n):
+    """Compute at bpc 512 holds each wave's CRC words in VGPRs (up to 64 rounds) and stores
+    them in bursts (kOptHoldStore). Sizes where waves run past one full hold (flush mid-stream),
+    end on a partial 8-round group, and leave a slow region and a short tail: every word
+    against the oracle."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    bpc = 512
+    data = splitmix_bytes(n, 0x5704E + n)
+    d = gpu_ctx.upload(data)
+    nc = (n + bpc - 1) // bpc
+    dc = DeviceBuffer(4 * nc)
+    gpu_ctx.compute_dev(d.ptr, n, bpc, dc.ptr)
+    assert np.array_equal(gpu_ctx.download(dc, 4 * nc), oracle_compute(data, bpc))
+
+
 def test_block_128mib_async_result_and_launch_count(gpu_ctx):
     """Config 2: one 128 MiB block, 512 B chunks, device-resident async verify."""
     from libhdfs3_amd.engine import DeviceBuffer
