@@ -287,6 +287,14 @@ __device__ __forceinline__ void load_round(Round &r, const uint8_t *base, uint32
     }
 }
 
+// A wave-uniform 64-bit value made provably uniform (two v_readfirstlane): downstream
+// arithmetic then stays in SGPRs/SALU instead of 64-bit VALU per use.
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(x));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(x >> 32));
+    return (uint64_t(hi) << 32) | lo;
+}
+
 // Same, through a buffer resource built from the wave-uniform round base (scalar
 // registers, made provably uniform by readfirstlane: cdna_hip_programming.md T8/T20).
 // The lane's constant byte offset is the only VGPR operand, so no 64-bit VGPR address
@@ -1238,7 +1246,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
             uint32_t lo = 0, hi = L.nseg - 1;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi + 1) >> 1;
-                const uint64_t ub = segp(mid)->unit_begin;
+                const uint64_t ub = rfl64(segp(mid)->unit_begin);
                 if (ub <= u) lo = mid;
                 else hi = mid - 1;
             }
@@ -1258,12 +1266,14 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
         if (k < K) {
             const uint64_t u = wave + k * nwaves;
             if (u < c_begin || u >= c_end) {
+                // descriptor fields come back in VGPRs (vector loads); made uniform here,
+                // every per-round view computation below is SALU
                 const DevSegment *sd = segp(seg_of(u));
-                c_begin = sd->unit_begin;
-                c_end = sd->unit_begin + sd->len / kRoundBytes;
-                c_data = sd->data;
-                c_crc = sd->crc;
-                c_key = sd->key_base;
+                c_begin = rfl64(sd->unit_begin);
+                c_end = c_begin + rfl64(sd->len) / kRoundBytes;
+                c_data = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->data)));
+                c_crc = reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->crc)));
+                c_key = rfl64(sd->key_base);
             }
             const uint64_t r = u - c_begin;
             v.p = c_data + r * kRoundBytes;

@@ -2,6 +2,7 @@
 """A/B of the segmented kernel against the contiguous wave kernel on the same 1 GiB:
   contiguous   hdfs3_crc32c_verify_dev_async over the 8 contiguous 128 MiB blocks
   blocks       hdfs3_crc32c_verify_blocks_dev_async, the same bytes as 8 independent blocks
+  one_segment  the same API with the whole 1 GiB as ONE block (segmented kernel, 1 segment)
 HIP-event timed, interleaved rounds, median us per launch."""
 import json
 import os
@@ -39,10 +40,15 @@ def main():
             lib.hdfs3x_set_variant(0)
         return f
 
-    cases = {"contiguous": contiguous, "blocks": blk(0)}
+    one = [(data.data_ptr(), crc.data_ptr(), nb * bb)]
+
+    def one_segment(i):
+        ctx.verify_blocks_dev_async(one, bpc, res.data_ptr() + 8 * (i % 1024))
+
+    cases = {"contiguous": contiguous, "blocks": blk(0), "one_segment": one_segment}
     samples = {k: [] for k in cases}
-    for f in cases.values():
-        for i in range(3):
+    for f in cases.values():  # ramp the clocks (~25 ms of load)
+        for i in range(100):
             f(i)
     torch.cuda.synchronize()
     for rnd in range(7):
