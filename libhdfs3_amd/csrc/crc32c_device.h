@@ -1220,7 +1220,8 @@ struct RoundView {
 // UNI: every segment but the last has L.uniform units -> the segment is a 32-bit divide;
 // otherwise a binary search. They are separate instantiations on purpose: a search loop in
 // the hot loop's CFG (even untaken) makes the waitcnt pass drain the prefetch each step.
-template <int BPC, bool VERIFY, bool UNI>
+// ONE (A/B variant 49): a single segment, its view fixed at kernel start (no refresh branch).
+template <int BPC, bool VERIFY, bool UNI, bool ONE = false>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, const uint32_t *__restrict__ g_tab,
                                                                    const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 64 == 0, "one-round units");
@@ -1263,9 +1264,18 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
     uint8_t *c_crc = nullptr;
     auto view = [&](uint64_t k) -> RoundView {
         RoundView v;
+        if constexpr (ONE) {  // diagnostic: the wave kernel's round_ptr arithmetic, branch-free
+            const uint64_t u = wave + k * nwaves;
+            const bool in = k < K;
+            v.p = in ? c_data + u * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
+            v.crc = in ? c_crc : const_cast<uint8_t *>(reinterpret_cast<const uint8_t *>(g_tab));
+            v.chunk0 = in ? u * kChunksPerUnit : 0;
+            v.key0 = v.chunk0;
+            return v;
+        }
         if (k < K) {
             const uint64_t u = wave + k * nwaves;
-            if (u < c_begin || u >= c_end) {
+            if (!ONE && (u < c_begin || u >= c_end)) {
                 // descriptor fields come back in VGPRs (vector loads); made uniform here,
                 // every per-round view computation below is SALU
                 const DevSegment *sd = segp(seg_of(u));
@@ -1290,6 +1300,14 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
         return v;
     };
 
+    if constexpr (ONE) {
+        const DevSegment *sd = segp(0);
+        c_begin = rfl64(sd->unit_begin);
+        c_end = c_begin + rfl64(sd->len) / kRoundBytes;
+        c_data = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->data)));
+        c_crc = reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->crc)));
+        c_key = rfl64(sd->key_base);
+    }
     // lean fill (as the production wave kernel): one slice-table word per thread, replicated
     // in LDS; for G <= 32 the half-size fold image
     constexpr bool kHalfFold = G <= 32;

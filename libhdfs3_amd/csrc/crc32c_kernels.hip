@@ -102,13 +102,15 @@ bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc) {
     return true;
 }
 
-template <int BPC, bool UNI>
+template <int BPC, bool UNI, bool ONE = false>
 hipError_t launch_seg_k(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *nib, int grid,
                         hipStream_t s) {
     if (verify)
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, true, UNI>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
+        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, true, UNI, ONE>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab,
+                           nib);
     else
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false, UNI>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
+        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false, UNI, ONE>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab,
+                           nib);
     return hipGetLastError();
 }
 
@@ -117,6 +119,7 @@ hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, co
                         hipStream_t s) {
     constexpr int set = BPC == 512 ? 0 : BPC == 1024 ? 1 : BPC == 2048 ? 2 : 3;
     const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
+    if (g_variant == 49 && L.nseg == 1) return launch_seg_k<BPC, true, true>(L, verify, tab, nib, grid, s);
     return L.uniform ? launch_seg_k<BPC, true>(L, verify, tab, nib, grid, s)
                      : launch_seg_k<BPC, false>(L, verify, tab, nib, grid, s);
 }

@@ -145,3 +145,28 @@ def test_packet_fast_path_agrees_with_packet_kernel(gpu_ctx, bpc):
         assert np.array_equal(gpu_ctx.download(d, arena.nbytes), arena)
     finally:
         lib.hdfs3x_set_variant(0)
+
+
+@pytest.mark.parametrize("bpc", [512, 2048, 4096])
+@pytest.mark.parametrize("variant", [0, 49])
+def test_single_segment_batch(gpu_ctx, bpc, variant):
+    """One block through the batch API (segmented kernel with one segment); variant 49 fixes
+    the segment view at kernel start (A/B, tools/seg_ab.py). Words and first bad chunk."""
+    from libhdfs3_amd import _native
+
+    lib = _native.lib()
+    n = 4096 * 1000 + 3 * bpc + 77
+    try:
+        lib.hdfs3x_set_variant(variant)
+        blocks, keep, datas = make_blocks(gpu_ctx, [n], bpc, 4900 + bpc)
+        gpu_ctx.compute_blocks_dev(blocks, bpc)
+        d, c, _ = blocks[0]
+        want = oracle_compute(datas[0], bpc)
+        assert np.array_equal(gpu_ctx.download(c, want.nbytes), want)
+        assert gpu_ctx.verify_blocks_dev(blocks, bpc, True) == (-1, -1)
+        k = (n // bpc) // 2
+        pos = k * bpc + 5
+        gpu_ctx.upload(np.array([datas[0][pos] ^ 8], np.uint8), keep[0], offset=pos)
+        assert gpu_ctx.verify_blocks_dev(blocks, bpc, False) == (0, k)
+    finally:
+        lib.hdfs3x_set_variant(0)

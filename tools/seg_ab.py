@@ -3,6 +3,8 @@
   contiguous   hdfs3_crc32c_verify_dev_async over the 8 contiguous 128 MiB blocks
   blocks       hdfs3_crc32c_verify_blocks_dev_async, the same bytes as 8 independent blocks
   one_segment  the same API with the whole 1 GiB as ONE block (segmented kernel, 1 segment)
+  one_segment_fixed_view_v49  the same with the segment view fixed at kernel start (no
+               per-step refresh branch; A/B variant 49)
 HIP-event timed, interleaved rounds, median us per launch."""
 import json
 import os
@@ -45,7 +47,15 @@ def main():
     def one_segment(i):
         ctx.verify_blocks_dev_async(one, bpc, res.data_ptr() + 8 * (i % 1024))
 
-    cases = {"contiguous": contiguous, "blocks": blk(0), "one_segment": one_segment}
+    def one_segment_v(v):
+        def f(i):
+            lib.hdfs3x_set_variant(v)
+            ctx.verify_blocks_dev_async(one, bpc, res.data_ptr() + 8 * (i % 1024))
+            lib.hdfs3x_set_variant(0)
+        return f
+
+    cases = {"contiguous": contiguous, "blocks": blk(0), "one_segment": one_segment,
+             "one_segment_fixed_view_v49": one_segment_v(49)}
     samples = {k: [] for k in cases}
     for f in cases.values():  # ramp the clocks (~25 ms of load)
         for i in range(100):
