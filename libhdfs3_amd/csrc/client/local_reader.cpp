@@ -27,6 +27,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "../ctx.h"
 #include "hdfs3_client.h"
@@ -66,6 +67,47 @@ int pread_fully(int fd, void *buf, size_t n, int64_t off) {
         off += r;
     }
     return 0;
+}
+
+// Reader resources — a ctx (stream, table images) and kSlots pinned + device windows —
+// are pooled per process. The reference opens one LocalBlockReader per block
+// (InputStreamImpl::setupBlockReader), and creating a ctx and pinning the windows costs
+// more than reading a 128 MiB block from the page cache.
+struct LocalResources {
+    hdfs3_crc_ctx *ctx = nullptr;
+    PacketArena a[kSlots];
+};
+std::mutex g_pool_mu;
+std::vector<LocalResources> g_pool;
+constexpr size_t kPoolMax = 16;
+
+bool take_pooled(int device, size_t cap, LocalResources *out) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size(); ++i) {
+        if (g_pool[i].ctx->device == device && g_pool[i].a[0].cap >= cap) {
+            *out = g_pool[i];
+            g_pool.erase(g_pool.begin() + long(i));
+            return true;
+        }
+    }
+    return false;
+}
+
+void free_resources(LocalResources &r) {
+    for (PacketArena &a : r.a) a.release();
+    hdfs3_crc_ctx_destroy(r.ctx);
+    r.ctx = nullptr;
+}
+
+void give_back(LocalResources r) {
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (g_pool.size() < kPoolMax) {
+            g_pool.push_back(r);
+            return;
+        }
+    }
+    free_resources(r);
 }
 
 struct Window {
@@ -290,9 +332,14 @@ struct hdfs3_local_reader {
             loader.join();
         }
         if (ctx) {
-            (void)hipStreamSynchronize(ctx->stream);
-            for (Window &w : slot) w.a.release();
-            hdfs3_crc_ctx_destroy(ctx);
+            LocalResources res;
+            res.ctx = ctx;
+            for (int i = 0; i < kSlots; ++i) res.a[i] = slot[i].a;
+            // a ctx whose stream completes cleanly goes back to the pool for the next reader
+            if (hipStreamSynchronize(ctx->stream) == hipSuccess && res.a[kSlots - 1].done)
+                give_back(res);
+            else
+                free_resources(res);
         }
         if (data_fd >= 0) ::close(data_fd);
         if (meta_fd >= 0) ::close(meta_fd);
@@ -333,20 +380,28 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
     r->cursor = offset;
     r->window = uint32_t(std::min<int64_t>(int64_t(r->buffer_size) * wbuf, 1ll << 30) / r->buffer_size * r->buffer_size);
     r->cap_data = (size_t(r->window) + 255) & ~size_t(255);
-    if (int rc = hdfs3_crc_ctx_create(device, &r->ctx)) return bail(rc);
-    if (r->checksum_type == wire::kChecksumCrc32)
-        if (int rc = hdfs3_crc_ctx_set_checksum_type(r->ctx, HDFS3_CHECKSUM_TYPE_CRC32)) return bail(rc);
     const size_t crc_bytes = r->verify ? 4 * ((size_t(r->window) + r->chunk_size - 1) / r->chunk_size) : 0;
-    for (Window &w : r->slot) {
-        PacketArena &a = w.a;
-        if (hipHostMalloc(reinterpret_cast<void **>(&a.h), r->cap_data + crc_bytes, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.d), r->cap_data + crc_bytes) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.d_res), sizeof(unsigned long long)) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
-            hipEventCreateWithFlags(&a.done, hipEventDisableTiming) != hipSuccess)
-            return bail(fail(-ENOMEM, "LocalBlockReader: window allocation failed"));
-        a.cap = r->cap_data + crc_bytes;
+    LocalResources pooled;
+    if (take_pooled(device, r->cap_data + crc_bytes, &pooled)) {
+        r->ctx = pooled.ctx;
+        for (int i = 0; i < kSlots; ++i) r->slot[i].a = pooled.a[i];
+    } else {
+        if (int rc = hdfs3_crc_ctx_create(device, &r->ctx)) return bail(rc);
+        for (Window &w : r->slot) {
+            PacketArena &a = w.a;
+            if (hipHostMalloc(reinterpret_cast<void **>(&a.h), r->cap_data + crc_bytes, hipHostMallocDefault) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&a.d), r->cap_data + crc_bytes) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&a.d_res), sizeof(unsigned long long)) != hipSuccess ||
+                hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
+                hipEventCreateWithFlags(&a.done, hipEventDisableTiming) != hipSuccess)
+                return bail(fail(-ENOMEM, "LocalBlockReader: window allocation failed"));
+            a.cap = r->cap_data + crc_bytes;
+        }
     }
+    if (int rc = hdfs3_crc_ctx_set_checksum_type(r->ctx, r->checksum_type == wire::kChecksumCrc32
+                                                             ? HDFS3_CHECKSUM_TYPE_CRC32
+                                                             : HDFS3_CHECKSUM_TYPE_CRC32C))
+        return bail(rc);
     for (int i = 0; i < kSlots; ++i) r->free_slots.push_back(i);
     if (r->first < r->length) {
         r->loader = std::thread([r] { r->run_loader(); });

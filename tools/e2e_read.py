@@ -6,6 +6,9 @@
                 hdfs3_block_reader: socket -> pinned arena -> H2D -> packet-kernel verify ->
                 caller buffer), verify on vs off
   parallel      8 concurrent streams, one hdfsPread of one whole block each
+  local         short-circuit read (hdfs3_local_reader, LocalBlockReader): 8 block files of
+                128 MiB + .meta in a temp dir (page-cache resident after writing), 4 MiB reads,
+                verify on vs off; 1 stream, and 8 concurrent readers (one block each)
 
 The datanode thread and the reader share the host's cores, so the loopback numbers bound
 the client from below; the verify-off line is the same transport without the GPU work.
@@ -82,6 +85,82 @@ def diag(dn, blocks, out, data, args):
               flush=True)
 
 
+def local_reads(data, crc, args, line):
+    """hdfs3_local_reader over block files + .meta (BE16 version 1 | u8 type 2 | BE32 bpc | words)."""
+    import shutil
+    import struct
+    import tempfile
+
+    from libhdfs3_amd.engine import LocalBlockReader
+
+    bsz = args.block_mib << 20
+    tmp = tempfile.mkdtemp(prefix="hdfs3_local_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        files = []
+        for i in range(args.blocks):
+            d, m = os.path.join(tmp, f"blk_{i}"), os.path.join(tmp, f"blk_{i}.meta")
+            with open(d, "wb") as f:
+                f.write(data[i * bsz:(i + 1) * bsz].tobytes())
+            with open(m, "wb") as f:
+                f.write(struct.pack(">hBI", 1, 2, args.bpc))
+                f.write(crc[4 * (i * bsz // args.bpc): 4 * ((i + 1) * bsz // args.bpc)].tobytes())
+            files.append((d, m))
+        out = np.empty(args.blocks * bsz, dtype=np.uint8)
+
+        def one(i, verify, errors):
+            try:
+                with LocalBlockReader(*files[i], verify=verify) as r:
+                    pos = 0
+                    while pos < bsz:
+                        got = r.read_into(out, i * bsz + pos, min(args.read_mib << 20, bsz - pos))
+                        if got <= 0:
+                            errors.append(f"block {i}: read returned {got} at {pos}")
+                            return
+                        pos += got
+            except Exception as e:  # noqa: BLE001 - reported
+                errors.append(f"block {i}: {e}")
+
+        # transport floor: plain buffered reads of the same files into the same buffer
+        best = 0.0
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            for i, (d, _m) in enumerate(files):
+                with open(d, "rb", buffering=0) as f:
+                    pos = 0
+                    while pos < bsz:
+                        n = min(args.read_mib << 20, bsz - pos)
+                        got = f.readinto(memoryview(out[i * bsz + pos: i * bsz + pos + n]))
+                        assert got and got > 0
+                        pos += got
+            best = max(best, out.nbytes / (time.perf_counter() - t0) / GIB)
+        print(json.dumps({**line, "mode": "plain_file_read", "streams": 1, "read_mib": args.read_mib,
+                          "gib_s": round(best, 2), "fs": tmp}), flush=True)
+        for verify in (True, False):
+            for streams in (1, args.blocks):
+                best = 0.0
+                for _ in range(args.reps):
+                    errors: list[str] = []
+                    t0 = time.perf_counter()
+                    if streams == 1:
+                        for i in range(args.blocks):
+                            one(i, verify, errors)
+                    else:
+                        th = [threading.Thread(target=one, args=(i, verify, errors)) for i in range(args.blocks)]
+                        for t in th:
+                            t.start()
+                        for t in th:
+                            t.join()
+                    dt = time.perf_counter() - t0
+                    assert not errors, errors
+                    best = max(best, out.nbytes / dt / GIB)
+                assert np.array_equal(out, data[:out.nbytes])
+                out[:] = 0
+                print(json.dumps({**line, "mode": "local_read", "verify": verify, "streams": streams,
+                                  "read_mib": args.read_mib, "gib_s": round(best, 2)}), flush=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=8)
@@ -92,6 +171,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--read-mib", type=int, default=4, help="hdfsRead request size")
     ap.add_argument("--diag", action="store_true", help="per-phase timing of the block reader only")
+    ap.add_argument("--local-only", action="store_true", help="only the short-circuit reader lines")
     args = ap.parse_args()
 
     from libhdfs3_amd import _native
@@ -105,6 +185,10 @@ def main():
     data = rng.integers(0, 256, size=total, dtype=np.uint8)
     crc = ctx.compute(data, args.bpc)
     line = {"bench": "e2e", "bytes": total, "bpc": args.bpc}
+    if args.local_only:
+        local_reads(data, crc, args, line)
+        ctx.close()
+        return
 
     # (the words' parity with the reference is the -m gpu suite's job; this tool only times)
     print(json.dumps({**line, "mode": "host_verify_pageable",
@@ -169,6 +253,7 @@ def main():
                                   "gib_s": round(best, 2)}), flush=True)
     finally:
         dn.stop()
+    local_reads(data, crc, args, line)
     ctx.close()
 
 
