@@ -464,7 +464,7 @@ struct hdfs3_block_reader {
             if (!cached) b.a.release();
             b.a = PacketArena();
         }
-        if (ctx && own_ctx) hdfs3_crc_ctx_destroy(ctx);
+        if (ctx && own_ctx) ctx_release(ctx);
         net::close_fd(fd);
     }
 };
@@ -491,7 +491,7 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
     if (shared_ctx) {
         r->ctx = shared_ctx;
         r->own_ctx = false;
-    } else if (int rc = hdfs3_crc_ctx_create(device, &r->ctx)) {
+    } else if (int rc = ctx_acquire(device, &r->ctx)) {
         delete r;
         return rc;
     }

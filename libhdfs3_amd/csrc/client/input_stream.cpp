@@ -58,7 +58,7 @@ struct hdfs3_input_stream {
 
     ~hdfs3_input_stream() {
         drop_reader();
-        if (ctx) hdfs3_crc_ctx_destroy(ctx);
+        if (ctx) ctx_release(ctx);
     }
 
     void drop_reader() {
@@ -249,7 +249,7 @@ int hdfs3_input_open(const hdfs3_located_block *blocks, int n_blocks, const char
         return fail(-EINVAL, "the first block must start at file offset 0");
     }
     s->file_length = expect;
-    if (int rc = hdfs3_crc_ctx_create(s->opts.device, &s->ctx)) {
+    if (int rc = ctx_acquire(s->opts.device, &s->ctx)) {
         delete s;
         return rc;
     }

@@ -95,7 +95,7 @@ bool take_pooled(int device, size_t cap, LocalResources *out) {
 
 void free_resources(LocalResources &r) {
     for (PacketArena &a : r.a) a.release();
-    hdfs3_crc_ctx_destroy(r.ctx);
+    ctx_release(r.ctx);
     r.ctx = nullptr;
 }
 
@@ -386,7 +386,7 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
         r->ctx = pooled.ctx;
         for (int i = 0; i < kSlots; ++i) r->slot[i].a = pooled.a[i];
     } else {
-        if (int rc = hdfs3_crc_ctx_create(device, &r->ctx)) return bail(rc);
+        if (int rc = ctx_acquire(device, &r->ctx)) return bail(rc);
         for (Window &w : r->slot) {
             PacketArena &a = w.a;
             if (hipHostMalloc(reinterpret_cast<void **>(&a.h), r->cap_data + crc_bytes, hipHostMallocDefault) != hipSuccess ||

@@ -100,7 +100,7 @@ struct hdfs3_output_stream {
         if (ctx) {
             (void)hipStreamSynchronize(ctx->stream);
             for (WBatch &b : batch) b.a.release();
-            hdfs3_crc_ctx_destroy(ctx);
+            ctx_release(ctx);
         }
     }
 
@@ -330,7 +330,7 @@ int hdfs3_output_open(const hdfs3_writer_opts *opts, hdfs3_packet_sink sink, voi
         delete s;
         return fail(-EINVAL, "invalid packet size / chunk size / block size combination");
     }
-    if (int rc = hdfs3_crc_ctx_create(device, &s->ctx)) {
+    if (int rc = ctx_acquire(device, &s->ctx)) {
         delete s;
         return rc;
     }

@@ -55,6 +55,18 @@ struct PacketArena {
 
 }  // namespace hdfs3crc
 
+struct hdfs3_crc_ctx;
+namespace hdfs3crc {
+// Process-wide pool of contexts for the client drop-ins (input/output streams, block and
+// local readers). libhdfs3 opens a stream per file and a reader per block; creating a ctx
+// (stream, table uploads, device query) and its pinned arenas costs milliseconds, more than
+// reading a small file. A released ctx keeps its arena cache and goes back to the pool.
+// acquire: a pooled ctx of `device` (stream reset to its own, type CRC32C) or a new one.
+int ctx_acquire(int device, hdfs3_crc_ctx **out);
+// release: synchronizes the ctx's stream; pooled when that succeeds and the pool has room.
+void ctx_release(hdfs3_crc_ctx *ctx);
+}  // namespace hdfs3crc
+
 struct hdfs3_crc_ctx {
     int device = 0;
     int grid_cap = 256;            // one 1024-thread workgroup per CU (128 KiB LDS image)

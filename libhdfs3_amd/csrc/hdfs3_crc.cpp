@@ -458,6 +458,56 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx) {
     delete ctx;
 }
 
+}  // extern "C"
+
+namespace hdfs3crc {
+namespace {
+std::mutex g_ctx_pool_mu;
+std::vector<hdfs3_crc_ctx *> g_ctx_pool;
+constexpr size_t kCtxPoolMax = 32;
+}  // namespace
+
+int ctx_acquire(int device, hdfs3_crc_ctx **out) {
+    if (!out) return fail(-EINVAL, "null out");
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_pool_mu);
+        for (size_t i = 0; i < g_ctx_pool.size(); ++i) {
+            hdfs3_crc_ctx *ctx = g_ctx_pool[i];
+            if (ctx->device != device) continue;
+            g_ctx_pool.erase(g_ctx_pool.begin() + long(i));
+            ctx->stream = ctx->own_stream;
+            ctx->checksum_type = HDFS3_CHECKSUM_TYPE_CRC32C;
+            ctx->d_tables = ctx->d_tables_by[0];
+            ctx->d_fold = ctx->d_fold_by[0];
+            *out = ctx;
+            return 0;
+        }
+    }
+    return hdfs3_crc_ctx_create(device, out);
+}
+
+void ctx_release(hdfs3_crc_ctx *ctx) {
+    if (!ctx) return;
+    bool ok;
+    {
+        DeviceGuard g(ctx->device);
+        ok = hipStreamSynchronize(ctx->stream) == hipSuccess;
+    }
+    for (Slot &s : ctx->slot) s.pending_out = nullptr;
+    if (ok) {
+        std::lock_guard<std::mutex> lk(g_ctx_pool_mu);
+        if (g_ctx_pool.size() < kCtxPoolMax) {
+            g_ctx_pool.push_back(ctx);
+            return;
+        }
+    }
+    hdfs3_crc_ctx_destroy(ctx);
+}
+
+}  // namespace hdfs3crc
+
+extern "C" {
+
 int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream) {
     if (!ctx) return fail(-EINVAL, "null ctx");
     DeviceGuard g(ctx->device);
