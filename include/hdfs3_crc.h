@@ -67,6 +67,15 @@ const char *hdfs3_crc_last_error(void);
  * RemoteBlockReader.cpp:169-184, LocalBlockReader.cpp:86-98, OutputStreamImpl.cpp:55-66. */
 int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out);
 void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx);
+/* Pooled create/destroy for callers that make a context per reader or per file, as libhdfs3
+ * does (one Checksum per RemoteBlockReader/LocalBlockReader/OutputStreamImpl). create costs
+ * milliseconds (stream, table upload, device query); acquire returns a pooled context of
+ * `device` (own stream, CRC32C) when one is free, else creates one. release synchronizes the
+ * context's stream and returns it to the process-wide pool (thread-safe), or destroys it when
+ * the pool is full or the stream reports an error. Never release a context twice, and never
+ * mix release with destroy for the same context. */
+int hdfs3_crc_ctx_acquire(int device, hdfs3_crc_ctx **out);
+void hdfs3_crc_ctx_release(hdfs3_crc_ctx *ctx);
 /* Attach an external hipStream_t (e.g. a framework's current stream); NULL
  * restores the ctx-owned stream. */
 int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream);

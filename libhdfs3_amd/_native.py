@@ -39,6 +39,8 @@ PUBLIC_API = {
     "hdfs3_crc_abi_version": (c_int, []),
     "hdfs3_crc_last_error": (ctypes.c_char_p, []),
     "hdfs3_crc_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "hdfs3_crc_ctx_acquire": (c_int, [c_int, POINTER(c_void_p)]),
+    "hdfs3_crc_ctx_release": (None, [c_void_p]),
     "hdfs3_crc_ctx_destroy": (None, [c_void_p]),
     "hdfs3_crc_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
     "hdfs3_crc_ctx_get_stream": (c_void_p, [c_void_p]),

@@ -508,6 +508,9 @@ void ctx_release(hdfs3_crc_ctx *ctx) {
 
 extern "C" {
 
+int hdfs3_crc_ctx_acquire(int device, hdfs3_crc_ctx **out) { return hdfs3crc::ctx_acquire(device, out); }
+void hdfs3_crc_ctx_release(hdfs3_crc_ctx *ctx) { hdfs3crc::ctx_release(ctx); }
+
 int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream) {
     if (!ctx) return fail(-EINVAL, "null ctx");
     DeviceGuard g(ctx->device);

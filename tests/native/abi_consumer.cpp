@@ -48,6 +48,9 @@ int main(int argc, char **argv) {
     if (argc > 1 && std::strcmp(argv[1], "nodevice") == 0) {
         // no silent CPU fallback: the engine refuses to exist without a gfx950 device
         CHECK(rc == -ENODEV && ctx == nullptr, "ctx_create without a device returned %d", rc);
+        hdfs3_crc_ctx *pooled = nullptr;
+        const int rc2 = hdfs3_crc_ctx_acquire(0, &pooled);
+        CHECK(rc2 == -ENODEV && pooled == nullptr, "ctx_acquire without a device returned %d", rc2);
         CHECK(std::strlen(hdfs3_crc_last_error()) > 0, "no error message");
         std::printf(g_fail ? "abi_consumer nodevice FAILED\n" : "abi_consumer nodevice ok\n");
         return g_fail ? 1 : 0;
@@ -162,6 +165,14 @@ int main(int argc, char **argv) {
           "null ctx accepted");
     CHECK(hdfs3_crc_ctx_get_checksum_type(ctx) == HDFS3_CHECKSUM_TYPE_CRC32C, "default type");
     CHECK(hdfs3_crc_ctx_kernel_launches(ctx) > 0, "no kernel launched");
+
+    // pooled contexts: a released context comes back on the next acquire, and works
+    hdfs3_crc_ctx *p1 = nullptr, *p2 = nullptr;
+    CHECK(hdfs3_crc_ctx_acquire(0, &p1) == 0 && p1, "acquire");
+    hdfs3_crc_ctx_release(p1);
+    CHECK(hdfs3_crc_ctx_acquire(0, &p2) == 0 && p2 == p1, "released context not reused");
+    CHECK(hdfs3_crc32c_compute(p2, pkt.data(), pkt.size(), bpc, got.data()) == 0 && got == want, "pooled compute");
+    hdfs3_crc_ctx_release(p2);
 
     hdfs3_crc_ctx_destroy(ctx);
     std::printf(g_fail ? "abi_consumer FAILED (%d)\n" : "abi_consumer ok\n", g_fail);
