@@ -92,7 +92,8 @@ typedef struct hdfs3_located_block {  /* LocatedBlockProto (hdfs.proto) */
 } hdfs3_located_block;
 
 /* Blocks must be in file order and contiguous (offset[i+1] = offset[i] + num_bytes[i]);
- * the table and host strings are copied. One GPU context per stream. 0 or -errno. */
+ * the table and host strings are copied. One GPU context per stream, taken from the process-wide
+ * pool (hdfs3_crc_ctx_acquire) and returned on close. 0 or -errno. */
 int hdfs3_input_open(const hdfs3_located_block *blocks, int n_blocks, const char *client_name,
                      const hdfs3_reader_opts *opts, hdfs3_input_stream **out);
 /* hdfsRead: up to len bytes from the cursor, never crossing a block boundary (readOneBlock) */
