@@ -126,7 +126,7 @@ typedef struct hdfs3_local_opts {
     int device;
     int verify;               /* 0: no verification                                     */
     int32_t buffer_size;      /* input.localread.default.buffersize (1 MiB), chunk-rounded */
-    int window_buffers;       /* buffers per GPU window (16)                            */
+    int window_buffers;       /* buffers per GPU window (4)                             */
 } hdfs3_local_opts;
 
 /* num_bytes <= 0 takes the block file's size; offset skips like LocalBlockReader::skip.

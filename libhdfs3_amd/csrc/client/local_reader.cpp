@@ -41,7 +41,7 @@ namespace {
 constexpr int kMetaHeader = 7;             // HEADER_SIZE: version 2 + type 1 + bpc 4
 constexpr int kSlots = 3;
 constexpr int32_t kDefaultBuffer = 1 << 20;  // input.localread.default.buffersize
-constexpr int kDefaultWindowBuffers = 16;
+constexpr int kDefaultWindowBuffers = 4;  // 4 MiB windows: first delivery sooner
 
 int hip_err(hipError_t e, const char *what) {
     return fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));

@@ -457,7 +457,7 @@ class LocalBlockReader:
     its .meta file with GPU verification of every chunk."""
 
     def __init__(self, data_path: str, meta_path: str, *, num_bytes: int = 0, offset: int = 0, device: int = 0,
-                 verify: bool = True, buffer_size: int = 1 << 20, window_buffers: int = 16):
+                 verify: bool = True, buffer_size: int = 1 << 20, window_buffers: int = 4):
         self._lib = _native.lib()
         opts = _native.LocalOpts(device, int(verify), buffer_size, window_buffers)
         p = c_void_p()
