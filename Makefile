@@ -14,7 +14,7 @@ LOOPBACK := $(LIBDIR)/libhdfs3_loopback.so
 OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/crc32c_experiments.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc32c.o \
             $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/client_block_reader.o \
             $(OBJDIR)/client_input_stream.o $(OBJDIR)/client_output_stream.o \
-            $(OBJDIR)/client_local_reader.o
+            $(OBJDIR)/client_local_reader.o $(OBJDIR)/client_block_checksum.o $(OBJDIR)/md5.o
 
 CONSUMER := tests/native/abi_consumer
 CLIENT_CONSUMER := tests/native/client_consumer
@@ -61,10 +61,18 @@ $(OBJDIR)/client_local_reader.o: $(CSRC)/client/local_reader.cpp include/hdfs3_c
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
+$(OBJDIR)/client_block_checksum.o: $(CSRC)/client/block_checksum.cpp include/hdfs3_client.h $(CSRC)/ctx.h $(CSRC)/client/wire.h $(CSRC)/client/net.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(OBJDIR)/md5.o: $(CSRC)/md5.cpp $(CSRC)/md5.h
+	@mkdir -p $(OBJDIR)
+	g++ $(HOSTFLAGS) -c $< -o $@
+
 # test/bench infrastructure: loopback datanode (tools/loopback)
-$(LOOPBACK): tools/loopback/loopback_datanode.cpp $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o
+$(LOOPBACK): tools/loopback/loopback_datanode.cpp $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/md5.o
 	@mkdir -p $(LIBDIR)
-	g++ $(HOSTFLAGS) -shared -pthread -o $@ tools/loopback/loopback_datanode.cpp $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o
+	g++ $(HOSTFLAGS) -shared -pthread -o $@ tools/loopback/loopback_datanode.cpp $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/md5.o
 
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)

@@ -189,6 +189,25 @@ int hdfs3_output_stats(hdfs3_output_stream *s, uint64_t *packets, uint64_t *gpu_
 /* hdfsCloseFile: the remaining packets and the block's last packet reach the sink; frees s */
 int hdfs3_output_close(hdfs3_output_stream *s);
 
+/* ------------------------------------------------------------------------------------
+ * OP_BLOCK_CHECKSUM client (DataTransferProtocolSender::blockChecksum, a TODO in the
+ * reference, DataTransferProtocolSender.cpp:169-180): sends version | 85 | varint len |
+ * OpBlockChecksumProto to host:port and parses BlockOpResponseProto.checksumResponse
+ * (datatransfer.proto:189-227). A non-SUCCESS status or a reply without the checksum
+ * response fails with -EIO (message in hdfs3_crc_last_error), a malformed reply with
+ * -EPROTO. Compare md5 with hdfs3_block_checksum_dev over the same block to check a
+ * replica end to end.
+ * ---------------------------------------------------------------------------------- */
+typedef struct hdfs3_block_checksum_info {
+    uint32_t bytes_per_crc;
+    uint64_t crc_per_block;
+    uint8_t md5[16];
+    int crc_type;                 /* ChecksumTypeProto, or -1 when the reply omits it */
+} hdfs3_block_checksum_info;
+
+int hdfs3_block_checksum_remote(const char *host, int port, const hdfs3_block_id *block, int timeout_ms,
+                                hdfs3_block_checksum_info *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -184,6 +184,23 @@ int hdfs3_crc32c_compute_packets_dev(hdfs3_crc_ctx *ctx, void *d_arena, size_t a
  * calls (OutputStreamImpl.cpp:309-314). Host code; never used by the batch API. */
 uint32_t hdfs3_crc32c_update_host(uint32_t state, const void *p, size_t len);
 
+/* ---- block checksum ("MD5 of CRC32", OP_BLOCK_CHECKSUM) --------------------
+ * DataTransferProtocolSender::blockChecksum (DataTransferProtocolSender.h:112-120) is a
+ * TODO in the reference (DataTransferProtocolSender.cpp:169-180). The datanode answers it
+ * with OpBlockChecksumResponseProto {bytesPerCrc, crcPerBlock, md5} (datatransfer.proto:
+ * 222-227), md5 being the MD5 digest of the block's stored CRC words: ceil(len/bpc)
+ * big-endian words, exactly the .meta file after its 7-byte header (LocalBlockReader.cpp:
+ * 64-121). hdfs3_block_checksum_dev computes those words on the GPU (the ctx's checksum
+ * type, one compute launch per 4 Mi chunks) and digests them on the host (MD5 is a serial
+ * chain); crc_per_block may be NULL. _crcs digests words the caller already holds (a
+ * .meta file). The file checksum (MD5MD5CRC32FileChecksum) is the MD5 of the blocks'
+ * 16-byte digests, concatenated in block order. All return 0 or -errno. */
+int hdfs3_block_checksum_dev(hdfs3_crc_ctx *ctx, const void *d_data, size_t len, uint32_t bpc,
+                             uint8_t *md5_out /* 16 B */, uint64_t *crc_per_block);
+int hdfs3_block_checksum_crcs(const void *crc_be, uint64_t n_crcs, uint8_t *md5_out /* 16 B */);
+int hdfs3_file_checksum_md5md5crc(const uint8_t *block_md5s /* n_blocks x 16 B */, size_t n_blocks,
+                                  uint8_t *md5_out /* 16 B */);
+
 /* ---- device memory helpers for FFI callers without a HIP binding ---------- */
 int hdfs3_dev_malloc(void **d_ptr, size_t bytes);
 int hdfs3_dev_free(void *d_ptr);

@@ -81,6 +81,9 @@ PUBLIC_API = {
                                                      c_void_p]),
     "hdfs3_crc32c_compute_blocks_dev": (c_int, [c_void_p, POINTER(DevBlock), c_size_t, c_uint32]),
     "hdfs3_crc_ctx_get_checksum_type": (c_int, [c_void_p]),
+    "hdfs3_block_checksum_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p, POINTER(c_uint64)]),
+    "hdfs3_block_checksum_crcs": (c_int, [c_void_p, c_uint64, c_void_p]),
+    "hdfs3_file_checksum_md5md5crc": (c_int, [c_void_p, c_size_t, c_void_p]),
 }
 
 class BlockId(ctypes.Structure):
@@ -133,8 +136,17 @@ class WriterOpts(ctypes.Structure):
                 ("block_size", c_int64), ("batch_packets", c_int)]
 
 
+class BlockChecksumInfo(ctypes.Structure):
+    """hdfs3_block_checksum_info (include/hdfs3_client.h)."""
+
+    _fields_ = [("bytes_per_crc", c_uint32), ("crc_per_block", c_uint64), ("md5", ctypes.c_uint8 * 16),
+                ("crc_type", c_int)]
+
+
 # every symbol include/hdfs3_client.h declares
 CLIENT_API = {
+    "hdfs3_block_checksum_remote": (c_int, [ctypes.c_char_p, c_int, POINTER(BlockId), c_int,
+                                            POINTER(BlockChecksumInfo)]),
     "hdfs3_block_reader_open": (c_int, [ctypes.c_char_p, c_int, POINTER(BlockId), c_int64, c_int64,
                                         ctypes.c_char_p, POINTER(ReaderOpts), POINTER(c_void_p)]),
     "hdfs3_block_reader_read": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),

@@ -150,16 +150,32 @@ static std::string encode_extended_block(const ExtendedBlock &b) {
     return s;
 }
 
-std::string encode_read_block(const ReadBlockRequest &r) {
-    // TokenProto with empty fields (all four are required; security is out of scope)
+// BaseHeaderProto {1: block, 2: TokenProto} (datatransfer.proto:40-43); the token's four
+// required fields are empty (security is out of scope)
+static std::string encode_base_header(const ExtendedBlock &b) {
     std::string token;
     put_bytes(token, 1, "");
     put_bytes(token, 2, "");
     put_bytes(token, 3, "");
     put_bytes(token, 4, "");
     std::string base;
-    put_bytes(base, 1, encode_extended_block(r.block));
+    put_bytes(base, 1, encode_extended_block(b));
     put_bytes(base, 2, token);
+    return base;
+}
+
+static std::string frame_op(int op, const std::string &proto) {
+    std::string out;
+    out.push_back(char(kDataTransferVersion >> 8));
+    out.push_back(char(kDataTransferVersion & 0xFF));
+    out.push_back(char(op));
+    put_varint(out, proto.size());
+    out += proto;
+    return out;
+}
+
+std::string encode_read_block(const ReadBlockRequest &r) {
+    const std::string base = encode_base_header(r.block);
     std::string client_header;
     put_bytes(client_header, 1, base);
     put_bytes(client_header, 2, r.client_name);
@@ -168,14 +184,13 @@ std::string encode_read_block(const ReadBlockRequest &r) {
     put_uint(op, 2, r.offset);
     put_uint(op, 3, r.len);
     if (!r.send_checksums) put_uint(op, 4, 0);
+    return frame_op(kOpReadBlock, op);
+}
 
-    std::string out;
-    out.push_back(char(kDataTransferVersion >> 8));
-    out.push_back(char(kDataTransferVersion & 0xFF));
-    out.push_back(char(kOpReadBlock));
-    put_varint(out, op.size());
-    out += op;
-    return out;
+std::string encode_block_checksum(const ExtendedBlock &block) {
+    std::string op;
+    put_bytes(op, 1, encode_base_header(block));
+    return frame_op(kOpBlockChecksum, op);
 }
 
 static bool decode_extended_block(const std::string &s, ExtendedBlock &b) {
@@ -190,6 +205,33 @@ static bool decode_extended_block(const std::string &s, ExtendedBlock &b) {
         else r.skip(wt);
     }
     return r.ok;
+}
+
+bool decode_block_checksum(const void *proto, size_t n, ExtendedBlock &out) {
+    Reader r(proto, n);
+    bool have_block = false;
+    while (r.more()) {
+        const uint64_t key = r.varint();
+        const int field = int(key >> 3), wt = int(key & 7);
+        if (field == 1 && wt == 2) {
+            const std::string base = r.bytes();
+            Reader b(base.data(), base.size());
+            while (b.more()) {
+                const uint64_t k2 = b.varint();
+                const int f2 = int(k2 >> 3), w2 = int(k2 & 7);
+                if (f2 == 1 && w2 == 2) {
+                    if (!decode_extended_block(b.bytes(), out)) return false;
+                    have_block = true;
+                } else {
+                    b.skip(w2);
+                }
+            }
+            if (!b.ok) return false;
+        } else {
+            r.skip(wt);
+        }
+    }
+    return r.ok && have_block;
 }
 
 bool decode_read_block(const void *proto, size_t n, ReadBlockRequest &out) {
@@ -239,6 +281,15 @@ bool decode_read_block(const void *proto, size_t n, ReadBlockRequest &out) {
 std::string encode_block_op_response(const BlockOpResponse &r) {
     std::string out;
     put_uint(out, 1, uint64_t(r.status));
+    if (r.has_checksum_response) {
+        const BlockChecksumResponse &c = r.checksum_response;
+        std::string cr;
+        put_uint(cr, 1, c.bytes_per_crc);
+        put_uint(cr, 2, c.crc_per_block);
+        put_bytes(cr, 3, c.md5);
+        if (c.crc_type >= 0) put_uint(cr, 4, uint64_t(c.crc_type));
+        put_bytes(out, 3, cr);
+    }
     if (r.has_checksum_info) {
         std::string cs;
         put_uint(cs, 1, uint64_t(r.checksum_type));
@@ -261,6 +312,22 @@ bool decode_block_op_response(const void *proto, size_t n, BlockOpResponse &out)
         if (field == 1 && wt == 0) {
             out.status = int(r.varint());
             have_status = true;
+        } else if (field == 3 && wt == 2) {
+            const std::string cr = r.bytes();
+            Reader c(cr.data(), cr.size());
+            BlockChecksumResponse &o = out.checksum_response;
+            int seen = 0;
+            while (c.more()) {
+                const uint64_t k2 = c.varint();
+                const int f2 = int(k2 >> 3), w2 = int(k2 & 7);
+                if (f2 == 1 && w2 == 0) o.bytes_per_crc = uint32_t(c.varint()), seen |= 1;
+                else if (f2 == 2 && w2 == 0) o.crc_per_block = c.varint(), seen |= 2;
+                else if (f2 == 3 && w2 == 2) o.md5 = c.bytes(), seen |= 4;
+                else if (f2 == 4 && w2 == 0) o.crc_type = int(c.varint());
+                else c.skip(w2);
+            }
+            if (!c.ok || seen != 7) return false;   // the three fields are required
+            out.has_checksum_response = true;
         } else if (field == 4 && wt == 2) {
             const std::string info = r.bytes();
             Reader i(info.data(), info.size());

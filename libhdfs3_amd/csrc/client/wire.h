@@ -22,6 +22,7 @@ namespace wire {
 constexpr int kDataTransferVersion = 28;   // DataTransferProtocolSender.h:38
 constexpr int kOpWriteBlock = 80;          // DataTransferProtocolSender.h:44
 constexpr int kOpReadBlock = 81;           // DataTransferProtocolSender.h:45
+constexpr int kOpBlockChecksum = 85;       // DataTransferProtocolSender.h:49
 constexpr int kPacketHeaderSize = 31;      // PacketHeader::CalcPkgHeaderSize with all fields set
 
 enum Status : int {                        // datatransfer.proto:152-166
@@ -91,8 +92,23 @@ std::string encode_read_block(const ReadBlockRequest &r);
 // parse the proto part of a READ_BLOCK request (datanode side)
 bool decode_read_block(const void *proto, size_t n, ReadBlockRequest &out);
 
+struct BlockChecksumResponse {     // OpBlockChecksumResponseProto, datatransfer.proto:222-227
+    uint32_t bytes_per_crc = 0;
+    uint64_t crc_per_block = 0;
+    std::string md5;               // 16 bytes: MD5 of the block's BE CRC words
+    int crc_type = -1;             // optional ChecksumTypeProto; -1 when absent
+};
+
+// OP_BLOCK_CHECKSUM request (DataTransferProtocolSender::blockChecksum, a TODO in the
+// reference at DataTransferProtocolSender.cpp:169-180): version | op 85 | varint len |
+// OpBlockChecksumProto {1: BaseHeaderProto {1: block, 2: token}} (datatransfer.proto:128-130)
+std::string encode_block_checksum(const ExtendedBlock &block);
+bool decode_block_checksum(const void *proto, size_t n, ExtendedBlock &out);
+
 struct BlockOpResponse {           // BlockOpResponseProto, datatransfer.proto:189-209
     int status = kSuccess;
+    bool has_checksum_response = false;   // field 3 (OP_BLOCK_CHECKSUM replies)
+    BlockChecksumResponse checksum_response;
     bool has_checksum_info = false;
     int checksum_type = kChecksumCrc32c;
     uint32_t bytes_per_checksum = 512;

@@ -5,9 +5,11 @@
 // leave a thread-local message (hdfs3_crc_last_error, cf. hdfsGetLastError at
 // Hdfs.cpp:59,329).
 #include "hdfs3_crc.h"
+#include "md5.h"
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstddef>
 #include <cstdarg>
@@ -665,6 +667,72 @@ int hdfs3_crc32c_compute_packets_dev(hdfs3_crc_ctx *ctx, void *d_arena, size_t a
 
 uint32_t hdfs3_crc32c_update_host(uint32_t state, const void *p, size_t len) {
     return len ? host_update(state, p, len) : state;
+}
+
+// Block checksum (include/hdfs3_crc.h): the CRC words come from the compute kernel in
+// pieces of up to kMd5PieceChunks chunks, alternating between the two slots, so the host
+// digests piece i while the GPU computes and copies out piece i+1.
+namespace {
+constexpr uint64_t kMd5PieceChunks = 1ull << 20;  // 4 MiB of CRC words per piece
+}
+
+int hdfs3_block_checksum_dev(hdfs3_crc_ctx *ctx, const void *d_data, size_t len, uint32_t bpc,
+                             uint8_t *md5_out, uint64_t *crc_per_block) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (!md5_out || (len && !d_data)) return fail(-EINVAL, "null buffer");
+    const uint64_t n = (uint64_t(len) + bpc - 1) / bpc;
+    if (crc_per_block) *crc_per_block = n;
+    Md5 md5;
+    if (n) {
+        DeviceGuard g(ctx->device);
+        const uint64_t per = kMd5PieceChunks;
+        const uint64_t pieces = (n + per - 1) / per;
+        for (Slot &s : ctx->slot) {
+            if (int rc = finish_pending(s)) return rc;
+            if (int rc = grow_slot(s, 0, size_t(std::min(n, per)) * 4)) return rc;
+            if (!s.done) HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        }
+        auto issue = [&](uint64_t i) -> int {
+            Slot &s = ctx->slot[i & 1];
+            const uint64_t c0 = i * per, cn = std::min(per, n - c0);
+            const uint64_t off = c0 * bpc;
+            ChunkLaunch a{};
+            a.data = static_cast<const uint8_t *>(d_data) + off;
+            a.len = std::min<uint64_t>(cn * bpc, uint64_t(len) - off);
+            a.bpc = bpc;
+            a.out_be = s.d_crc;
+            if (int rc = launch(ctx, a, false)) return rc;
+            HIP_TRY(hipMemcpyAsync(s.h_crc, s.d_crc, size_t(cn) * 4, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipEventRecord(s.done, ctx->stream));
+            return 0;
+        };
+        if (int rc = issue(0)) return rc;
+        for (uint64_t i = 0; i < pieces; ++i) {
+            if (i + 1 < pieces)
+                if (int rc = issue(i + 1)) return rc;
+            Slot &s = ctx->slot[i & 1];
+            HIP_TRY(hipEventSynchronize(s.done));
+            md5.update(s.h_crc, size_t(std::min(per, n - i * per)) * 4);
+        }
+    }
+    md5.finish(md5_out);
+    return 0;
+}
+
+int hdfs3_block_checksum_crcs(const void *crc_be, uint64_t n_crcs, uint8_t *md5_out) {
+    if (!md5_out || (n_crcs && !crc_be)) return fail(-EINVAL, "null buffer");
+    Md5 md5;
+    md5.update(crc_be, size_t(n_crcs) * 4);
+    md5.finish(md5_out);
+    return 0;
+}
+
+int hdfs3_file_checksum_md5md5crc(const uint8_t *block_md5s, size_t n_blocks, uint8_t *md5_out) {
+    if (!md5_out || (n_blocks && !block_md5s)) return fail(-EINVAL, "null buffer");
+    Md5 md5;
+    md5.update(block_md5s, n_blocks * 16);
+    md5.finish(md5_out);
+    return 0;
 }
 
 int hdfs3_dev_malloc(void **d_ptr, size_t bytes) {

@@ -193,6 +193,15 @@ class CrcContext:
         check("hdfs3_crc32c_compute_blocks_dev",
               self._lib.hdfs3_crc32c_compute_blocks_dev(self.ctx, self._blocks(blocks), len(blocks), bpc))
 
+    # -- block checksum (OP_BLOCK_CHECKSUM's "MD5 of CRC32") ----------------------------
+    def block_checksum_dev(self, d_data: int, nbytes: int, bpc: int) -> tuple[bytes, int]:
+        """MD5 of the block's BE CRC words (GPU CRCs, host MD5) and crcPerBlock."""
+        out = np.zeros(16, dtype=np.uint8)
+        n = ctypes.c_uint64(0)
+        check("hdfs3_block_checksum_dev",
+              self._lib.hdfs3_block_checksum_dev(self.ctx, d_data, nbytes, bpc, _ptr(out), byref(n)))
+        return out.tobytes(), n.value
+
     # -- packet-stream API ------------------------------------------------------------
     @staticmethod
     def _descs(pk) -> ctypes.Array:
@@ -222,6 +231,35 @@ class CrcContext:
         d = self._descs(pk)
         check("hdfs3_crc32c_compute_packets_dev",
               self._lib.hdfs3_crc32c_compute_packets_dev(self.ctx, d_arena, arena_len, d, len(pk), bpc))
+
+
+def block_checksum_crcs(crc_be: bytes | np.ndarray) -> bytes:
+    """hdfs3_block_checksum_crcs: MD5 of stored BE CRC words (a .meta file's body)."""
+    buf = np.frombuffer(bytes(crc_be), dtype=np.uint8)
+    out = np.zeros(16, dtype=np.uint8)
+    check("hdfs3_block_checksum_crcs",
+          _native.lib().hdfs3_block_checksum_crcs(_ptr(buf) if buf.nbytes else None, buf.nbytes // 4, _ptr(out)))
+    return out.tobytes()
+
+
+def file_checksum_md5md5crc(block_md5s) -> bytes:
+    """hdfs3_file_checksum_md5md5crc: MD5 over the blocks' 16-byte digests in order."""
+    buf = np.frombuffer(b"".join(block_md5s), dtype=np.uint8)
+    out = np.zeros(16, dtype=np.uint8)
+    check("hdfs3_file_checksum_md5md5crc",
+          _native.lib().hdfs3_file_checksum_md5md5crc(_ptr(buf) if buf.nbytes else None, buf.nbytes // 16,
+                                                      _ptr(out)))
+    return out.tobytes()
+
+
+def block_checksum_remote(host: str, port: int, block_id: int, *, pool_id: bytes = b"BP-loopback",
+                          generation_stamp: int = 1, num_bytes: int = 0, timeout_ms: int = 60000):
+    """hdfs3_block_checksum_remote: (bytes_per_crc, crc_per_block, md5, crc_type) from a datanode."""
+    blk = _native.BlockId(pool_id, block_id, generation_stamp, num_bytes)
+    info = _native.BlockChecksumInfo()
+    check("hdfs3_block_checksum_remote",
+          _native.lib().hdfs3_block_checksum_remote(host.encode(), port, byref(blk), timeout_ms, byref(info)))
+    return info.bytes_per_crc, info.crc_per_block, bytes(info.md5), info.crc_type
 
 
 def update_host(state: int, data: bytes | np.ndarray) -> int:

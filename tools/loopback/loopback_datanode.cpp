@@ -22,6 +22,7 @@
 
 #include "../../libhdfs3_amd/csrc/client/net.h"
 #include "../../libhdfs3_amd/csrc/client/wire.h"
+#include "../../libhdfs3_amd/csrc/md5.h"
 
 using namespace hdfs3crc;
 
@@ -87,13 +88,54 @@ int send_all_iov(int fd, iovec *iov, int n) {
     return 0;
 }
 
+// OP_BLOCK_CHECKSUM: the datanode's answer is the MD5 of the block's stored CRC words
+// (the .meta file after its header), with bytesPerCrc and crcPerBlock beside it
+void serve_block_checksum(Server *sv, int fd, const std::string &proto, int version, int to) {
+    wire::ExtendedBlock eb;
+    wire::BlockOpResponse resp;
+    Block b{};
+    bool found = false;
+    const bool ok = version == wire::kDataTransferVersion && wire::decode_block_checksum(proto.data(), proto.size(), eb);
+    if (ok) {
+        std::lock_guard<std::mutex> lk(sv->mu);
+        auto it = sv->blocks.find(eb.block_id);
+        if (it != sv->blocks.end()) b = it->second, found = true;
+    }
+    if (!ok || !found || b.type == wire::kChecksumNull) {
+        resp.status = wire::kErrorInvalid;
+        resp.message = !ok ? "bad request" : !found ? "block not found" : "block has no checksums";
+    } else {
+        const uint64_t n = (b.len + b.bpc - 1) / b.bpc;
+        Md5 md5;
+        md5.update(b.crc_be, size_t(n) * 4);
+        uint8_t d[16];
+        md5.finish(d);
+        resp.status = wire::kSuccess;
+        resp.has_checksum_response = true;
+        resp.checksum_response.bytes_per_crc = b.bpc;
+        resp.checksum_response.crc_per_block = n;
+        resp.checksum_response.md5.assign(reinterpret_cast<const char *>(d), 16);
+        resp.checksum_response.crc_type = b.type;
+    }
+    (void)net::write_delimited(fd, wire::encode_block_op_response(resp), to);
+    net::close_fd(fd);
+}
+
 void serve(Server *sv, int fd) {
     const int to = 60000;
     uint8_t head[3];
     std::string proto;
     wire::ReadBlockRequest req;
-    if (net::read_fully(fd, head, 3, to) || net::read_delimited(fd, proto, 1 << 20, to) ||
-        !wire::decode_read_block(proto.data(), proto.size(), req)) {
+    if (net::read_fully(fd, head, 3, to) || net::read_delimited(fd, proto, 1 << 20, to)) {
+        net::close_fd(fd);
+        return;
+    }
+    if (head[2] == wire::kOpBlockChecksum) {
+        ++sv->requests;
+        serve_block_checksum(sv, fd, proto, (head[0] << 8) | head[1], to);
+        return;
+    }
+    if (!wire::decode_read_block(proto.data(), proto.size(), req)) {
         net::close_fd(fd);
         return;
     }
