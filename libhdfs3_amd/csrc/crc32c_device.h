@@ -138,6 +138,33 @@ __device__ uint32_t crc_run_any(const Lut &t, uint32_t c, const uint8_t *p, uint
     return c;
 }
 
+// crc_run_any for a 16-byte aligned run: 128-byte lines whose 8 loads are issued
+// together, then the remaining 16-byte pieces (again issued together), then words and
+// bytes. One load latency per line instead of one per 16 bytes: the segmented kernel's
+// slow pass runs it on one lane per chunk while the rest of the wave waits.
+__device__ uint32_t crc_run_lines(const Lut &t, uint32_t c, const uint8_t *p, uint32_t n) {
+    for (; n >= 128; n -= 128, p += 128) {
+        u32x4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = ld16(p + 16 * i);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c = t.vec_state(c, v[i]);
+    }
+    const uint32_t k = n / 16;
+    u32x4 v[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+        if (uint32_t(i) < k) v[i] = ld16(p + 16 * i);
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+        if (uint32_t(i) < k) c = t.vec_state(c, v[i]);
+    p += 16 * k;
+    n -= 16 * k;
+    for (; n >= 4; n -= 4, p += 4) c = t.word_state(c, *reinterpret_cast<const uint32_t *>(p));
+    for (; n; --n) c = t.byte(c, *p++);
+    return c;
+}
+
 __device__ __forceinline__ uint32_t load_be32(const uint8_t *p, bool aligned4) {
     if (aligned4) return __builtin_bswap32(*reinterpret_cast<const uint32_t *>(p));
     return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3];
@@ -514,7 +541,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_rounds_kernel(ChunkLaunc
     if (gtid < nslow) {
         const uint64_t chunk = first_slow + gtid;
         const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(a.len % BPC);
-        const uint32_t c = ~crc_run_any(t, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
+        const uint32_t c = ~crc_run_lines(t, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
         if constexpr (VERIFY) {
             if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(a.crc_be + 4 * chunk, crc_al4) != c)
                 atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
@@ -1010,7 +1037,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     if (gtid < nslow) {
         const uint64_t chunk = first_slow + gtid;
         const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(a.len % BPC);
-        const uint32_t c = ~crc_run_any(t, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
+        const uint32_t c = ~crc_run_lines(t, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
         if constexpr (VERIFY) {
             if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(a.crc_be + 4 * chunk, crc_al4) != c)
                 atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
@@ -1180,7 +1207,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_pool_kernel(ChunkLaunch 
     if (gtid < nslow) {
         const uint64_t chunk = first_slow + gtid;
         const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(a.len % BPC);
-        const uint32_t c = ~crc_run_any(tb, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
+        const uint32_t c = ~crc_run_lines(tb, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
         if constexpr (VERIFY) {
             if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(a.crc_be + 4 * chunk, crc_al4) != c)
                 atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
@@ -1221,7 +1248,12 @@ struct RoundView {
 // otherwise a binary search. They are separate instantiations on purpose: a search loop in
 // the hot loop's CFG (even untaken) makes the waitcnt pass drain the prefetch each step.
 // ONE (A/B variant 49): a single segment, its view fixed at kernel start (no refresh branch).
-template <int BPC, bool VERIFY, bool UNI, bool ONE = false>
+// HOLD (compute at bpc 512): the wave kernel's held stores (kOptHoldStore). Each lane keeps
+// the word it collects per 8 rounds together with its target address (rounds of one wave
+// may belong to different segments), up to 8 octets, and stores them in bursts.
+// USEARCH (A/B variant 51): the non-uniform segment lookup as a fixed-depth unrolled search
+// (32 guarded levels, no loop), so the hot loop's CFG stays loop-free.
+template <int BPC, bool VERIFY, bool UNI, bool ONE = false, bool HOLD = false, bool USEARCH = false>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, const uint32_t *__restrict__ g_tab,
                                                                    const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 64 == 0, "one-round units");
@@ -1243,6 +1275,15 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
         if constexpr (UNI) {  // unit counts stay < 2^32 (16 TiB per launch): 32-bit divide
             const uint32_t s = uint32_t(u) / uint32_t(L.uniform);
             return s < L.nseg ? s : L.nseg - 1;
+        } else if constexpr (USEARCH) {
+            // the last segment whose unit_begin <= u (begins are non-decreasing)
+            uint32_t lo = 0;
+#pragma unroll
+            for (int sh = 31; sh >= 0; --sh) {
+                const uint32_t m = lo + (1u << sh);
+                if (m < L.nseg && m > lo && rfl64(segp(m)->unit_begin) <= u) lo = m;
+            }
+            return lo;
         } else {
             uint32_t lo = 0, hi = L.nseg - 1;
             while (lo < hi) {
@@ -1363,7 +1404,40 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
         if constexpr (VERIFY) return *(gcu32 *)(v.crc + 4 * (v.chunk0 + lane / G));
         return 0;
     };
+    constexpr bool kHold = HOLD && !VERIFY && G == 8;
+    uint32_t line = 0;                 // kHold: lane 8r + c collects chunk c of the octet's round r
+    gu32 *laddr = nullptr;             //        and that word's destination (null: none this octet)
+    uint32_t hold[kHold ? 8 : 1];      // hold[i] = the octet closed i octets ago
+    gu32 *hold_addr[kHold ? 8 : 1];
+    uint32_t nheld = 0;
+    auto flush = [&]() {
+#pragma unroll
+        for (int i = 0; i < (kHold ? 8 : 0); ++i)
+            if (uint32_t(i) < nheld && hold_addr[i]) *hold_addr[i] = __builtin_bswap32(~hold[i]);
+        nheld = 0;
+    };
     auto finish = [&](uint64_t k, const RoundView &v, uint32_t y, uint32_t want) {
+        if constexpr (kHold) {
+            if (k >= K) return;
+            const uint32_t r = uint32_t(k & 7);
+            // group c's lanes all hold chunk c's state (group_xor is a butterfly)
+            const uint32_t got = uint32_t(__builtin_amdgcn_ds_bpermute(int(32 * (lane & 7)), int(y)));
+            const bool mine = (lane >> 3) == r;
+            line = mine ? got : line;
+            laddr = mine ? (gu32 *)(v.crc + 4 * (v.chunk0 + (lane & 7))) : laddr;
+            if (r == 7 || k + 1 == K) {
+#pragma unroll
+                for (int i = (kHold ? 7 : 0); i > 0; --i) {
+                    hold[i] = hold[i - 1];
+                    hold_addr[i] = hold_addr[i - 1];
+                }
+                hold[0] = line;
+                hold_addr[0] = laddr;
+                laddr = nullptr;
+                if (++nheld == 8) flush();
+            }
+            return;
+        }
         if (k >= K || j != 0) return;
         const uint32_t c = ~y;
         if constexpr (VERIFY) {
@@ -1415,18 +1489,25 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
         if (k + 2 >= K) break;
         step(b[2], b[3], b[0], b[1], k + 2);
     }
+    if constexpr (kHold) flush();
 
     // slow pass: per segment, the chunks after its last whole round and its short tail
-    const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
-    const uint64_t nthreads = uint64_t(gridDim.x) * kBlockThreads;
-    for (uint64_t si = gtid; si < L.nseg; si += nthreads) {
-        const DevSegment sd = *segp(uint32_t(si));
+    // (at most kChunksPerUnit of them). One chunk per thread, item i = segment
+    // i / kChunksPerUnit, spread over the workgroups (item i -> block i % grid): a
+    // segment's leftovers no longer run one after another on one lane, which made every
+    // ragged batch wait for up to 7 serial chunks (~30 us at 1 GiB, tools/seg_search_ab.py).
+    const uint64_t items = uint64_t(L.nseg) * kChunksPerUnit;
+    for (uint64_t it = uint64_t(threadIdx.x) * gridDim.x + blockIdx.x; it < items;
+         it += uint64_t(gridDim.x) * kBlockThreads) {
+        const uint32_t si = uint32_t(it / kChunksPerUnit);
+        const DevSegment sd = *segp(si);
         const uint64_t nfull = sd.len / BPC;
         const uint64_t first = (sd.len / kRoundBytes) * kChunksPerUnit;
         const uint64_t last = nfull + (sd.len % BPC ? 1 : 0);
-        for (uint64_t c = first; c < last; ++c) {
+        const uint64_t c = first + it % kChunksPerUnit;
+        if (c < last) {
             const uint32_t sz = c < nfull ? uint32_t(BPC) : uint32_t(sd.len % BPC);
-            const uint32_t v = ~crc_run_any(t, 0xFFFFFFFFu, sd.data + c * BPC, sz);
+            const uint32_t v = ~crc_run_lines(t, 0xFFFFFFFFu, sd.data + c * BPC, sz);
             if constexpr (VERIFY) {
                 if ((sz == uint32_t(BPC) || L.check_short_tail) && load_be32(sd.crc + 4 * c, true) != v)
                     atomicMax(L.result, ~(unsigned long long)(sd.key_base + c));
