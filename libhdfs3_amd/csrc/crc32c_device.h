@@ -1234,6 +1234,10 @@ struct SegLaunch {
     uint64_t uniform;
     unsigned long long *result;
     int check_short_tail;
+    // stride != 0: packet i is {inl[0].data + i*stride, inl[0].crc + i*stride, inl[0].len,
+    // key i << 32}, the last one with inl[1].len (uniform view only). Packets laid out at a
+    // constant pitch in one arena need no descriptor array at all.
+    uint64_t stride;
     DevSegment inl[kInlineSegments];
 };
 
@@ -1319,12 +1323,21 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
             if (!ONE && (u < c_begin || u >= c_end)) {
                 // descriptor fields come back in VGPRs (vector loads); made uniform here,
                 // every per-round view computation below is SALU
+                if (L.stride) {  // kernel-argument arithmetic only: no descriptor loads
+                    const uint32_t si = seg_of(u);
+                    c_begin = uint64_t(si) * L.uniform;
+                    c_end = c_begin + (si + 1 < L.nseg ? L.uniform : L.inl[1].len / kRoundBytes);
+                    c_data = L.inl[0].data + uint64_t(si) * L.stride;
+                    c_crc = L.inl[0].crc + uint64_t(si) * L.stride;
+                    c_key = uint64_t(si) << 32;
+                } else {
                 const DevSegment *sd = segp(seg_of(u));
                 c_begin = rfl64(sd->unit_begin);
                 c_end = c_begin + rfl64(sd->len) / kRoundBytes;
                 c_data = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->data)));
                 c_crc = reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->crc)));
                 c_key = rfl64(sd->key_base);
+                }
             }
             const uint64_t r = u - c_begin;
             v.p = c_data + r * kRoundBytes;
@@ -1500,7 +1513,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
     for (uint64_t it = uint64_t(threadIdx.x) * gridDim.x + blockIdx.x; it < items;
          it += uint64_t(gridDim.x) * kBlockThreads) {
         const uint32_t si = uint32_t(it / kChunksPerUnit);
-        const DevSegment sd = *segp(si);
+        DevSegment sd;
+        if (L.stride) {
+            sd = L.inl[0];
+            sd.data += uint64_t(si) * L.stride;
+            sd.crc += uint64_t(si) * L.stride;
+            sd.len = si + 1 < L.nseg ? L.inl[0].len : L.inl[1].len;
+            sd.key_base = uint64_t(si) << 32;
+        } else {
+            sd = *segp(si);
+        }
         const uint64_t nfull = sd.len / BPC;
         const uint64_t first = (sd.len / kRoundBytes) * kChunksPerUnit;
         const uint64_t last = nfull + (sd.len % BPC ? 1 : 0);

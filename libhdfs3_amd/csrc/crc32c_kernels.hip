@@ -131,7 +131,7 @@ hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, co
 hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,
                            uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
                            const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream,
-                           const DevSegment *h_inline) {
+                           const DevSegment *h_inline, uint64_t stride) {
     if (nseg == 0) return hipSuccess;
     SegLaunch L{};
     L.seg = d_seg;
@@ -140,7 +140,13 @@ hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t unit
     L.uniform = uniform;
     L.result = result;
     L.check_short_tail = check_short_tail;
-    if (h_inline) {
+    if (stride) {  // h_inline = {first packet, last packet}; the rest follow by pitch
+        if (!h_inline || !uniform) return hipErrorInvalidValue;
+        L.seg = nullptr;
+        L.stride = stride;
+        L.inl[0] = h_inline[0];
+        L.inl[1] = h_inline[1];
+    } else if (h_inline) {
         if (nseg > kInlineSegments) return hipErrorInvalidValue;
         L.seg = nullptr;
         for (uint32_t i = 0; i < nseg; ++i) L.inl[i] = h_inline[i];
@@ -169,14 +175,35 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
     bool fast = g_variant != 17 && (bpc == 512 || bpc == 1024 || bpc == 2048 || bpc == 4096);
     uint64_t units = 0, u0 = h_pk[0].data_len / kRoundBytes;
     bool same = true;
+    // constant pitch: packet i at data_off[0] + i*S, crc_off[0] + i*S, one data length
+    // (the last may be shorter) -> the kernel derives every descriptor (SegLaunch::stride)
+    const uint64_t pitch = n > 1 ? h_pk[1].data_off - h_pk[0].data_off : 0;
+    bool strided = n > kInlineSegments && g_variant != 52 && pitch > 0 && pitch == h_pk[1].crc_off - h_pk[0].crc_off;
     for (size_t i = 0; i < n; ++i) {
         const uint8_t *data = d_arena + h_pk[i].data_off;
-        uint8_t *crc = const_cast<uint8_t *>(d_arena) + h_pk[i].crc_off;
+        const uint8_t *crc = d_arena + h_pk[i].crc_off;
         const uint64_t u = h_pk[i].data_len / kRoundBytes;
         fast = fast && ((reinterpret_cast<uintptr_t>(data) & 15u) | (reinterpret_cast<uintptr_t>(crc) & 3u)) == 0;
         if (i + 1 < n && u != u0) same = false;
-        h_stage[i] = DevSegment{data, crc, h_pk[i].data_len, units, uint64_t(i) << 32};
+        strided = strided && h_pk[i].data_off == h_pk[0].data_off + i * pitch &&
+                  h_pk[i].crc_off == h_pk[0].crc_off + i * pitch &&
+                  (i + 1 == n || h_pk[i].data_len == h_pk[0].data_len);
         units += u;
+    }
+    if (fast && strided && same && u0 > 0) {
+        const DevSegment ends[2] = {
+            DevSegment{d_arena + h_pk[0].data_off, const_cast<uint8_t *>(d_arena) + h_pk[0].crc_off,
+                       h_pk[0].data_len, 0, 0},
+            DevSegment{d_arena + h_pk[n - 1].data_off, const_cast<uint8_t *>(d_arena) + h_pk[n - 1].crc_off,
+                       h_pk[n - 1].data_len, (n - 1) * u0, uint64_t(n - 1) << 32}};
+        return launch_segments(nullptr, uint32_t(n), units, u0, bpc, verify, check_short_tail, result, d_tables,
+                               d_fold, grid_cap, stream, ends, pitch);
+    }
+    units = 0;
+    for (size_t i = 0; i < n; ++i) {
+        h_stage[i] = DevSegment{d_arena + h_pk[i].data_off, const_cast<uint8_t *>(d_arena) + h_pk[i].crc_off,
+                                h_pk[i].data_len, units, uint64_t(i) << 32};
+        units += h_pk[i].data_len / kRoundBytes;
     }
     if (fast) {
         const uint64_t uniform = same && u0 > 0 ? u0 : 0;

@@ -170,3 +170,57 @@ def test_single_segment_batch(gpu_ctx, bpc, variant):
         assert gpu_ctx.verify_blocks_dev(blocks, bpc, False) == (0, k)
     finally:
         lib.hdfs3x_set_variant(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bpc", [512, 4096])
+@pytest.mark.parametrize("last_len", [65536, 65536 - 300, 100])
+def test_constant_pitch_packets_without_descriptors(gpu_ctx, bpc, last_len):
+    """Packets at one pitch in one arena (the reader's and writer's layout) go to the
+    segmented kernel with no descriptor array (SegLaunch::stride). Same keys and words as
+    with descriptors (A/B variant 52) and as the packet kernel (variant 17)."""
+    from libhdfs3_amd import _native
+
+    lib = _native.lib()
+    rng = np.random.default_rng(bpc + last_len)
+    n, plen = 40, 65536
+    crc_bytes = 4 * (plen // bpc)
+    pitch = 31 + 1 + crc_bytes + plen  # header-sized gap keeps data 16 B aligned below
+    pitch += (-pitch) % 16
+    arena = np.zeros(n * pitch, np.uint8)
+    pk = []
+    for i in range(n):
+        dl = plen if i + 1 < n else last_len
+        data = splitmix_bytes(dl, 7000 + i)
+        crc = oracle_compute(data, bpc)
+        crc_off = i * pitch + 32
+        data_off = crc_off + crc_bytes
+        arena[crc_off:crc_off + crc.nbytes] = crc
+        arena[data_off:data_off + dl] = data
+        pk.append((data_off, crc_off, dl))
+    d = gpu_ctx.upload(arena)
+    try:
+        for v in (0, 52, 17):
+            lib.hdfs3x_set_variant(v)
+            assert gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True) == (-1, -1), v
+        for _ in range(3):
+            p = int(rng.integers(0, n))
+            q = int(rng.integers(0, pk[p][2]))
+            bad = arena.copy()
+            bad[pk[p][0] + q] ^= 0x20
+            gpu_ctx.upload(bad, d)
+            got = set()
+            for v in (0, 52, 17):
+                lib.hdfs3x_set_variant(v)
+                got.add(gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True))
+            assert got == {(p, q // bpc)}, (p, q, got)
+        blank = arena.copy()
+        for data_off, crc_off, dl in pk:
+            blank[crc_off:data_off] = 0
+        for v in (0, 52):
+            lib.hdfs3x_set_variant(v)
+            gpu_ctx.upload(blank, d)
+            gpu_ctx.compute_packets_dev(d.ptr, arena.nbytes, pk, bpc)
+            assert np.array_equal(gpu_ctx.download(d, arena.nbytes), arena), v
+    finally:
+        lib.hdfs3x_set_variant(0)

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Device-resident packet-stream verify/compute rate (hdfs3_crc32c_{verify,compute}_packets_dev):
 1 GiB arena of 64 KiB packets in the wire layout [CRCs][data] (data 16 B aligned), the
-segmented wave kernel (variant 0) vs the chunk-per-lane packet kernel (variant 17). Each
-call includes the host-side descriptor build and a stream sync (the API is synchronous)."""
+segmented wave kernel (variant 0: constant-pitch packets take the descriptor-free strided
+launch; variant 52: the same kernel with a descriptor array) vs the chunk-per-lane packet
+kernel (variant 17). Each call includes the host-side descriptor pass and a stream sync
+(the API is synchronous)."""
 import ctypes
 import json
 import os
@@ -30,7 +32,7 @@ def main():
         desc[i].data_off, desc[i].crc_off, desc[i].data_len, desc[i].reserved = i * stride + 512, i * stride, pkt, 0
     bp, bc = ctypes.c_int64(), ctypes.c_int64()
     out = []
-    for v in (0, 17, 0, 17):
+    for v in (0, 52, 17, 0, 52):
         lib.hdfs3x_set_variant(v)
         _native.check("compute", lib.hdfs3_crc32c_compute_packets_dev(ctx.ctx, arena.data_ptr(), arena.numel(), desc, n, bpc))
         _native.check("verify", lib.hdfs3_crc32c_verify_packets_dev(ctx.ctx, arena.data_ptr(), arena.numel(), desc, n,
