@@ -1255,9 +1255,9 @@ struct RoundView {
 // HOLD (compute at bpc 512): the wave kernel's held stores (kOptHoldStore). Each lane keeps
 // the word it collects per 8 rounds together with its target address (rounds of one wave
 // may belong to different segments), up to 8 octets, and stores them in bursts.
-// USEARCH (A/B variant 51): the non-uniform segment lookup as a fixed-depth unrolled search
-// (32 guarded levels, no loop), so the hot loop's CFG stays loop-free.
-template <int BPC, bool VERIFY, bool UNI, bool ONE = false, bool HOLD = false, bool USEARCH = false>
+// (A fixed-depth unrolled search in place of the binary-search loop was 47 % slower on
+// ragged batches: profiles/r01_kernel_study/seg_search_ab.jsonl, former variant 51.)
+template <int BPC, bool VERIFY, bool UNI, bool ONE = false, bool HOLD = false>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, const uint32_t *__restrict__ g_tab,
                                                                    const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 64 == 0, "one-round units");
@@ -1279,15 +1279,6 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_seg_kernel(SegLaunch L, 
         if constexpr (UNI) {  // unit counts stay < 2^32 (16 TiB per launch): 32-bit divide
             const uint32_t s = uint32_t(u) / uint32_t(L.uniform);
             return s < L.nseg ? s : L.nseg - 1;
-        } else if constexpr (USEARCH) {
-            // the last segment whose unit_begin <= u (begins are non-decreasing)
-            uint32_t lo = 0;
-#pragma unroll
-            for (int sh = 31; sh >= 0; --sh) {
-                const uint32_t m = lo + (1u << sh);
-                if (m < L.nseg && m > lo && rfl64(segp(m)->unit_begin) <= u) lo = m;
-            }
-            return lo;
         } else {
             uint32_t lo = 0, hi = L.nseg - 1;
             while (lo < hi) {

@@ -102,17 +102,17 @@ bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc) {
     return true;
 }
 
-template <int BPC, bool UNI, bool ONE = false, bool US = false>
+template <int BPC, bool UNI, bool ONE = false>
 hipError_t launch_seg_k(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *nib, int grid,
                         hipStream_t s) {
     if (verify)
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, true, UNI, ONE, false, US>), dim3(grid), dim3(kBlockThreads), 0,
+        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, true, UNI, ONE>), dim3(grid), dim3(kBlockThreads), 0,
                            s, L, tab, nib);
     else if (BPC != 512 || g_variant == 50)  // A/B variant 50: per-round CRC-word stores (before held stores)
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false, UNI, ONE, false, US>), dim3(grid), dim3(kBlockThreads), 0,
+        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false, UNI, ONE>), dim3(grid), dim3(kBlockThreads), 0,
                            s, L, tab, nib);
     else  // compute at bpc 512: held stores (-2.4 % per GiB of blocks, -4.3 % for packet streams)
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false, UNI, ONE, true, US>), dim3(grid), dim3(kBlockThreads), 0,
+        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false, UNI, ONE, true>), dim3(grid), dim3(kBlockThreads), 0,
                            s, L, tab, nib);
     return hipGetLastError();
 }
@@ -124,7 +124,6 @@ hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, co
     const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
     if (g_variant == 49 && L.nseg == 1) return launch_seg_k<BPC, true, true>(L, verify, tab, nib, grid, s);
     if (L.uniform) return launch_seg_k<BPC, true>(L, verify, tab, nib, grid, s);
-    if (g_variant == 51) return launch_seg_k<BPC, false, false, true>(L, verify, tab, nib, grid, s);
     return launch_seg_k<BPC, false>(L, verify, tab, nib, grid, s);
 }
 
