@@ -8,6 +8,8 @@
 // checked against the oracle (test infrastructure, oracle/crc32c_oracle.c) and reassembled
 // into blocks; loopback datanodes (tools/loopback, test infrastructure) then serve those
 // blocks WITH the GPU-written CRC words, and hdfs3_input_* verifies them on the GPU again.
+// Last, each block's OP_BLOCK_CHECKSUM digest from both replicas is compared with the
+// digest of the held words and with a GPU recomputation from each replica's bytes.
 //
 //   client_consumer   -> exit 0 = every check passed (needs a gfx950 device)
 #include <cerrno>
@@ -218,6 +220,49 @@ int main() {
         CHECK(got == -1 && errno == EIO, "all replicas bad: read %d errno %d", got, errno);
         CHECK(pos >= kBlock && pos <= kBlock + kBlock / 2 + 17, "error surfaced at %lld", (long long)pos);
         if (in) hdfs3_input_close(in);
+    }
+
+    // ---- block checksums (OP_BLOCK_CHECKSUM, "MD5 of CRC32") and the file checksum -------
+    // Both replicas hold the same stored CRC words, so both datanodes answer the same
+    // digest; recomputing the words from each replica's bytes on the GPU tells the corrupt
+    // replica of block 1 apart.
+    {
+        hdfs3_crc_ctx *ctx = nullptr;
+        CHECK(hdfs3_crc_ctx_create(0, &ctx) == 0, "ctx_create: %s", hdfs3_crc_last_error());
+        std::vector<uint8_t> digests;
+        for (auto &kv : c.data) {
+            const uint64_t id = 9000 + uint64_t(kv.first);
+            const uint64_t words = c.crc[kv.first].size() / 4;
+            hdfs3_block_id b{"BP-loopback", id, 1, kv.second.size()};
+            hdfs3_block_checksum_info gi{}, bi{};
+            CHECK(hdfs3_block_checksum_remote("127.0.0.1", good, &b, 10000, &gi) == 0, "block checksum: %s",
+                  hdfs3_crc_last_error());
+            CHECK(hdfs3_block_checksum_remote("127.0.0.1", bad, &b, 10000, &bi) == 0, "block checksum (bad)");
+            uint8_t held[16];
+            CHECK(hdfs3_block_checksum_crcs(c.crc[kv.first].data(), words, held) == 0, "checksum of held words");
+            CHECK(std::memcmp(gi.md5, held, 16) == 0 && std::memcmp(bi.md5, held, 16) == 0, "block %lld md5",
+                  (long long)kv.first);
+            CHECK(gi.bytes_per_crc == kBpc && gi.crc_per_block == words && gi.crc_type == 2, "block %lld fields",
+                  (long long)kv.first);
+            for (int replica = 0; replica < 2 && ctx; ++replica) {
+                const std::vector<uint8_t> &d = replica == 1 && kv.first == 1 ? corrupt : kv.second;
+                void *dd = nullptr;
+                uint8_t md5[16];
+                uint64_t n = 0;
+                CHECK(hdfs3_dev_malloc(&dd, d.size()) == 0 && hdfs3_memcpy_h2d(ctx, dd, d.data(), d.size()) == 0,
+                      "upload");
+                CHECK(hdfs3_block_checksum_dev(ctx, dd, d.size(), kBpc, md5, &n) == 0 && n == words,
+                      "block_checksum_dev: %s", hdfs3_crc_last_error());
+                const bool differs = std::memcmp(md5, gi.md5, 16) != 0;
+                CHECK(differs == (replica == 1 && kv.first == 1), "block %lld replica %d: GPU digest %s",
+                      (long long)kv.first, replica, differs ? "differs" : "matches");
+                hdfs3_dev_free(dd);
+            }
+            digests.insert(digests.end(), gi.md5, gi.md5 + 16);
+        }
+        uint8_t file_md5[16];
+        CHECK(hdfs3_file_checksum_md5md5crc(digests.data(), digests.size() / 16, file_md5) == 0, "file checksum");
+        if (ctx) hdfs3_crc_ctx_destroy(ctx);
     }
 
     hdfs3_loopback_stop(good);
