@@ -1,93 +1,93 @@
 # Builds the MI355X (gfx950) CRC32C engine and its C-ABI:
-#   libhdfs3_amd/lib/libhdfs3_crc.so   (include/hdfs3_crc.h)
-# and the test-only oracle (oracle/Makefile).
+#   libhdfs3_amd/lib/libhdfs3_crc.so      product (include/hdfs3_crc.h, hdfs3_client.h, hdfs3_hdfs.h);
+#                                         exports only the C API (libhdfs3_crc.map)
+#   libhdfs3_amd/lib/libhdfs3_crc_lab.so  measurement library for tools/ and the A/B tests: the
+#                                         same sources with HDFS3_LAB=1 (kernel-variant knob,
+#                                         experiment kernels, read-ceiling kernels, hdfs3x_*)
+# plus test infrastructure (loopback datanode, native consumers) and the oracle (oracle/Makefile).
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 CSRC     := libhdfs3_amd/csrc
 LIBDIR   := libhdfs3_amd/lib
 OBJDIR   := build/obj
+LABDIR   := build/obj_lab
 HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Iinclude -I$(CSRC)
 HOSTFLAGS:= -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
 
 LIB      := $(LIBDIR)/libhdfs3_crc.so
+LABLIB   := $(LIBDIR)/libhdfs3_crc_lab.so
 LOOPBACK := $(LIBDIR)/libhdfs3_loopback.so
-OBJS     := $(OBJDIR)/crc32c_kernels.o $(OBJDIR)/crc32c_experiments.o $(OBJDIR)/hdfs3_crc.o $(OBJDIR)/host_crc32c.o \
-            $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/client_block_reader.o \
-            $(OBJDIR)/client_input_stream.o $(OBJDIR)/client_output_stream.o \
-            $(OBJDIR)/client_local_reader.o $(OBJDIR)/client_block_checksum.o $(OBJDIR)/md5.o
+
+# device/HIP translation units (built twice: product and lab), host-only ones (shared)
+HIP_SRCS := crc32c_kernels.hip hdfs3_crc.cpp multi_device.cpp client/block_reader.cpp client/input_stream.cpp \
+            client/output_stream.cpp client/local_reader.cpp client/block_checksum.cpp
+HOST_SRCS:= host_crc32c.cpp client/wire.cpp client/net.cpp md5.cpp client/hdfs_shim.cpp
+objname   = $(subst /,_,$(basename $(1))).o
+HIP_OBJS := $(foreach s,$(HIP_SRCS),$(OBJDIR)/$(call objname,$(s)))
+LAB_OBJS := $(foreach s,$(HIP_SRCS),$(LABDIR)/$(call objname,$(s))) $(LABDIR)/crc32c_experiments.o
+HOST_OBJS:= $(foreach s,$(HOST_SRCS),$(OBJDIR)/$(call objname,$(s)))
+HDRS     := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h) $(wildcard $(CSRC)/client/*.h)
 
 CONSUMER := tests/native/abi_consumer
 CLIENT_CONSUMER := tests/native/client_consumer
+HDFS_CONSUMER := tests/native/hdfs_consumer
 
-all: $(LIB) $(LOOPBACK) oracle $(CONSUMER) $(CLIENT_CONSUMER)
+all: $(LIB) $(LABLIB) $(LOOPBACK) oracle $(CONSUMER) $(CLIENT_CONSUMER) $(HDFS_CONSUMER)
 
-$(OBJDIR)/crc32c_kernels.o: $(CSRC)/crc32c_kernels.hip $(CSRC)/crc32c_device.h $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
+define hip_rule
+$(OBJDIR)/$(call objname,$(1)): $(CSRC)/$(1) $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -x hip -c $$< -o $$@
+$(LABDIR)/$(call objname,$(1)): $(CSRC)/$(1) $(HDRS)
+	@mkdir -p $(LABDIR)
+	$(HIPCC) $(HIPFLAGS) -DHDFS3_LAB=1 -x hip -c $$< -o $$@
+endef
+$(foreach s,$(HIP_SRCS),$(eval $(call hip_rule,$(s))))
 
-$(OBJDIR)/crc32c_experiments.o: $(CSRC)/crc32c_experiments.hip $(CSRC)/crc32c_device.h $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(LABDIR)/crc32c_experiments.o: $(CSRC)/crc32c_experiments.hip $(HDRS)
+	@mkdir -p $(LABDIR)
+	$(HIPCC) $(HIPFLAGS) -DHDFS3_LAB=1 -c $< -o $@
 
-$(OBJDIR)/hdfs3_crc.o: $(CSRC)/hdfs3_crc.cpp include/hdfs3_crc.h $(CSRC)/crc32c_kernels.h $(CSRC)/crc32c_tables.h
+define host_rule
+$(OBJDIR)/$(call objname,$(1)): $(CSRC)/$(1) $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+	g++ $(HOSTFLAGS) -c $$< -o $$@
+endef
+$(foreach s,$(HOST_SRCS),$(eval $(call host_rule,$(s))))
 
-$(OBJDIR)/host_crc32c.o: $(CSRC)/host_crc32c.cpp $(CSRC)/crc32c_tables.h
-	@mkdir -p $(OBJDIR)
-	g++ $(HOSTFLAGS) -c $< -o $@
+$(LIB): $(HIP_OBJS) $(HOST_OBJS) $(CSRC)/libhdfs3_crc.map
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -Wl,--version-script=$(CSRC)/libhdfs3_crc.map -o $@ $(HIP_OBJS) $(HOST_OBJS)
 
-$(OBJDIR)/client_wire.o: $(CSRC)/client/wire.cpp $(CSRC)/client/wire.h
-	@mkdir -p $(OBJDIR)
-	g++ $(HOSTFLAGS) -c $< -o $@
-
-$(OBJDIR)/client_net.o: $(CSRC)/client/net.cpp $(CSRC)/client/net.h
-	@mkdir -p $(OBJDIR)
-	g++ $(HOSTFLAGS) -c $< -o $@
-
-$(OBJDIR)/client_block_reader.o: $(CSRC)/client/block_reader.cpp $(CSRC)/client/block_reader.h include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h $(CSRC)/client/wire.h $(CSRC)/client/net.h
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
-
-$(OBJDIR)/client_input_stream.o: $(CSRC)/client/input_stream.cpp $(CSRC)/client/block_reader.h include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
-
-$(OBJDIR)/client_output_stream.o: $(CSRC)/client/output_stream.cpp include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h $(CSRC)/client/wire.h
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
-
-$(OBJDIR)/client_local_reader.o: $(CSRC)/client/local_reader.cpp include/hdfs3_client.h include/hdfs3_crc.h $(CSRC)/ctx.h $(CSRC)/client/wire.h
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
-
-$(OBJDIR)/client_block_checksum.o: $(CSRC)/client/block_checksum.cpp include/hdfs3_client.h $(CSRC)/ctx.h $(CSRC)/client/wire.h $(CSRC)/client/net.h
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
-
-$(OBJDIR)/md5.o: $(CSRC)/md5.cpp $(CSRC)/md5.h
-	@mkdir -p $(OBJDIR)
-	g++ $(HOSTFLAGS) -c $< -o $@
+$(LABLIB): $(LAB_OBJS) $(HOST_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(LAB_OBJS) $(HOST_OBJS)
 
 # test/bench infrastructure: loopback datanode (tools/loopback)
 $(LOOPBACK): tools/loopback/loopback_datanode.cpp $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/md5.o
 	@mkdir -p $(LIBDIR)
 	g++ $(HOSTFLAGS) -shared -pthread -o $@ tools/loopback/loopback_datanode.cpp $(OBJDIR)/client_wire.o $(OBJDIR)/client_net.o $(OBJDIR)/md5.o
 
-$(LIB): $(OBJS)
-	@mkdir -p $(LIBDIR)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS)
-
 # test infrastructure: a C++ consumer of the C-ABI, checked against the oracle
-$(CONSUMER): tests/native/abi_consumer.cpp include/hdfs3_crc.h oracle/crc32c_oracle.c oracle/crc32c_oracle.h $(LIB)
-	gcc -O2 -msse4.2 -mpclmul -c oracle/crc32c_oracle.c -o $(OBJDIR)/consumer_oracle.o
+$(OBJDIR)/consumer_oracle.o: oracle/crc32c_oracle.c oracle/crc32c_oracle.h
+	@mkdir -p $(OBJDIR)
+	gcc -O2 -msse4.2 -mpclmul -c $< -o $@
+
+$(CONSUMER): tests/native/abi_consumer.cpp include/hdfs3_crc.h $(OBJDIR)/consumer_oracle.o $(LIB)
 	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ tests/native/abi_consumer.cpp $(OBJDIR)/consumer_oracle.o \
 	    -L$(LIBDIR) -lhdfs3_crc -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath-link,/opt/rocm/lib -pthread
 
 # test infrastructure: a C++ consumer of the client drop-ins (include/hdfs3_client.h) over the
 # loopback datanode, in the reference function tests' shape
-$(CLIENT_CONSUMER): tests/native/client_consumer.cpp include/hdfs3_client.h $(CONSUMER) $(LIB) $(LOOPBACK)
+$(CLIENT_CONSUMER): tests/native/client_consumer.cpp include/hdfs3_client.h $(OBJDIR)/consumer_oracle.o $(LIB) $(LOOPBACK)
 	g++ -O2 -std=c++17 -Wall -Iinclude -Ioracle -o $@ tests/native/client_consumer.cpp $(OBJDIR)/consumer_oracle.o \
+	    -L$(LIBDIR) -lhdfs3_crc -lhdfs3_loopback -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath-link,/opt/rocm/lib \
+	    -pthread
+
+# test infrastructure: a plain C program on the hdfs.h surface (include/hdfs3_hdfs.h) over the
+# loopback datanode: hdfsRead / hdfsPread / hdfsWrite exactly as a libhdfs3 caller writes them
+$(HDFS_CONSUMER): tests/native/hdfs_consumer.c include/hdfs3_hdfs.h $(OBJDIR)/consumer_oracle.o $(LIB) $(LOOPBACK)
+	gcc -O2 -std=c11 -Wall -Iinclude -Ioracle -o $@ tests/native/hdfs_consumer.c $(OBJDIR)/consumer_oracle.o \
 	    -L$(LIBDIR) -lhdfs3_crc -lhdfs3_loopback -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath-link,/opt/rocm/lib \
 	    -pthread
 
@@ -96,7 +96,7 @@ oracle:
 	@if [ -d /root/reference/src/common ]; then $(MAKE) -C oracle ref; fi
 
 clean:
-	rm -rf build $(LIB) $(LOOPBACK) $(CONSUMER) $(CLIENT_CONSUMER)
+	rm -rf build $(LIB) $(LABLIB) $(LOOPBACK) $(CONSUMER) $(CLIENT_CONSUMER) $(HDFS_CONSUMER)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -19,6 +19,15 @@ Also reported, in the same run:
                 this host on a bounded sample (rank 0, N=1 only).
 
     python bench.py [--gpus N --steps K --warmup W --bpc 512 --mode verify]
+
+--gpus N > 1 without a launcher (no WORLD_SIZE in the environment) starts N rank processes
+itself, before anything touches a GPU, exactly as `torch.distributed.run --nproc-per-node N`
+would: rank r drives cuda:r (r mod the visible GPUs), the ranks meet over RCCL (or gloo with
+HDFS3_BENCH_BACKEND=gloo) and rank 0 prints the one JSON line.
+
+Clock: `value`, `ms_per_step` and `roofline.achieved` all come from ONE clock, HIP events on
+the launch stream around the K timed steps (max over ranks); the host wall clock of the same
+barrier + synchronize bracket is reported beside it (`host_ms_per_step`).
 """
 from __future__ import annotations
 
@@ -62,6 +71,9 @@ def parse():
                    help="barrier every timed launch (no HDFS3_LAUNCH_OVERLAP_PREVIOUS); the overlapped "
                         "run is the default and the barriered one is reported beside it")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--plumbing-check", action="store_true",
+                   help="CPU-only rehearsal of the N-rank entry (tests/test_multigpu.py): rank spawn, "
+                        "rendezvous, per-rank block sets, barrier and max-over-ranks; no GPU work")
     return p.parse_args()
 
 
@@ -89,6 +101,76 @@ def max_over_ranks(dist, value: float, device) -> float:
 def aggregate_rate(bytes_per_rank: int, world: int, elapsed_max: float) -> float:
     """value = all ranks' payload bytes / max-over-ranks time, in GiB/s (weak scaling)."""
     return bytes_per_rank * world / elapsed_max / 2**30
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """--gpus N outside a launcher: N rank processes of this same command, started before any
+    GPU call in this process (the parent only waits), with the environment torch.distributed.run
+    would give them. If a rank fails the others are stopped (their exact PIDs); the exit code is
+    the first failure's."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def gather_per_rank(dist, world, rank, row, device):
+    """Every rank's row of floats, on rank 0 (all ranks take part)."""
+    import torch
+    t = torch.zeros((world, len(row)), dtype=torch.float64, device=device)
+    t[rank] = torch.tensor(row, dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().tolist()
+
+
+def plumbing_check(args):
+    """The N-rank entry without GPU work (CPU, gloo): every rank derives its own block set,
+    then barrier -> a rank-dependent elapsed -> max over ranks -> per-rank rows on rank 0."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    dist_ok = world > 1
+    if dist_ok:
+        dist.barrier()
+    elapsed = 1e-3 * (1 + rank)
+    emax = max_over_ranks(dist, elapsed, torch.device("cpu")) if dist_ok else elapsed
+    rows = gather_per_rank(dist, world, rank, [rank, int(os.environ.get("LOCAL_RANK", "0")), rank_seed(rank),
+                                               elapsed, os.getpid()], torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"plumbing_check": True, "n_gpus": world, "requested_gpus": args.gpus,
+                          "elapsed_max": emax,
+                          "per_rank": [{"rank": int(r[0]), "local_rank": int(r[1]), "seed": int(r[2]),
+                                        "elapsed": r[3], "pid": int(r[4])} for r in rows]}), flush=True)
+    if dist_ok:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 class Workload:
@@ -224,24 +306,34 @@ class StepGraphs:
             self.graphs[1].replay()
 
 
-def stream_read_ceiling(torch, work, ctx, reps=10, overlap=False):
+def lab_context(work, stream):
+    """A context of the measurement library (libhdfs3_crc_lab.so) on the bench's device and
+    stream: the plain-read ceiling kernels live there, not in the product library."""
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import CrcContext
+    lab = CrcContext(work.data.device.index or 0, lib=_native.lab())
+    lab.set_stream(stream.cuda_stream)
+    return lab
+
+
+def stream_read_ceiling(torch, work, lab, reps=10, overlap=False):
     """Achievable HBM read on the same arena with a plain coalesced 16 B/lane read kernel
     (no CRC): best of grid 256/512 x default/non-temporal loads.
     Returns (1 GiB-per-launch GB/s, per-launch GB/s at the bench's own shape: one block per
     launch rotating over the blocks, back to back, i.e. including the per-launch head and
     dependent-launch overhead the CRC launches pay too)."""
     from libhdfs3_amd import _native
-    lib = _native.lib()
+    lib = _native.lab()
     sink = torch.zeros(4, dtype=torch.int32, device=work.data.device)
     total = work.blocks * work.block_bytes
 
     def rate(grid, nbytes, n, ptr_of, overlap=False):
         for i in range(3):
-            lib.hdfs3x_stream_read(ctx.ctx, ptr_of(i), nbytes, grid, sink.data_ptr())
+            lib.hdfs3x_stream_read(lab.ctx, ptr_of(i), nbytes, grid, sink.data_ptr())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for i in range(n):
-            lib.hdfs3x_stream_read_ex(ctx.ctx, ptr_of(i), nbytes, grid, sink.data_ptr(), int(overlap and i > 0))
+            lib.hdfs3x_stream_read_ex(lab.ctx, ptr_of(i), nbytes, grid, sink.data_ptr(), int(overlap and i > 0))
         e1.record()
         torch.cuda.synchronize()
         return nbytes * n / (e0.elapsed_time(e1) * 1e-3) / 1e9
@@ -255,22 +347,33 @@ def stream_read_ceiling(torch, work, ctx, reps=10, overlap=False):
     return best, per_block
 
 
-def lane_read_rate(torch, work, ctx, reps=10):
+def lane_read_rate(torch, work, lab, reps=10):
     from libhdfs3_amd import _native
-    lib = _native.lib()
+    lib = _native.lab()
     sink = torch.zeros(4, dtype=torch.int32, device=work.data.device)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for r in range(reps):
         b = r % work.blocks
-        lib.hdfs3x_lane_read(ctx.ctx, work.data_ptr(b), work.block_bytes, work.bpc, sink.data_ptr())
+        lib.hdfs3x_lane_read(lab.ctx, work.data_ptr(b), work.block_bytes, work.bpc, sink.data_ptr())
     e1.record()
     torch.cuda.synchronize()
     return work.block_bytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
 
 
+def cpu_quota_cores():
+    """cgroup v2 CPU quota of this process in cores (None when unlimited or unknown)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        return None
+
+
 def cpu_baseline(work, seconds, bpc):
-    """Reference CPU path on this host, bounded sample of the same workload (one block)."""
+    """Reference CPU path on this host, bounded sample of the same workload (one block): on
+    every CPU this process may run on (os.sched_getaffinity, one block range per thread) and on
+    one core."""
     import ctypes
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -278,40 +381,51 @@ def cpu_baseline(work, seconds, bpc):
 
     data = np.ascontiguousarray(work.data[0].cpu().numpy())
     crc = np.ascontiguousarray(work.crc[0].cpu().numpy())
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = max(1, len(os.sched_getaffinity(0)))
     ref = ref_lib()
     bad = ctypes.c_int64(0)
     if ref is not None and ref.ref_hw_available():
         kind, engine = "reference", "HWCrc32c (reference src/common/HWCrc32c.cpp, built by oracle/Makefile)"
-        fn = lambda reps: ref.ref_hw_bench_verify(data.ctypes.data, data.nbytes, bpc, crc.ctypes.data,
-                                                  threads, reps, ctypes.byref(bad))
+        run = lambda nthreads, reps: ref.ref_hw_bench_verify(data.ctypes.data, data.nbytes, bpc, crc.ctypes.data,
+                                                            nthreads, reps, ctypes.byref(bad))
     else:
         kind, engine = "port", "oracle crc_pcl restatement (3-way crc32q + pclmul, IntelAsmCrc32c behaviour)"
-        fn = lambda reps: oracle().oracle_bench_verify(PCL, data.ctypes.data, data.nbytes, bpc, crc.ctypes.data,
-                                                       threads, reps, ctypes.byref(bad))
-    t1 = fn(1)
-    reps = max(1, int(seconds / max(t1, 1e-6)))
-    t = fn(reps)
-    if bad.value != -1:
-        raise SystemExit(f"cpu baseline reported a bad chunk {bad.value} on a clean block")
-    gib = data.nbytes * reps / t / 2**30
+        run = lambda nthreads, reps: oracle().oracle_bench_verify(PCL, data.ctypes.data, data.nbytes, bpc,
+                                                                 crc.ctypes.data, nthreads, reps, ctypes.byref(bad))
+
+    def timed(nthreads, budget):
+        t1 = run(nthreads, 1)
+        reps = max(1, int(budget / max(t1, 1e-6)))
+        t = run(nthreads, reps)
+        if bad.value != -1:
+            raise SystemExit(f"cpu baseline reported a bad chunk {bad.value} on a clean block")
+        return data.nbytes * reps / t / 2**30, reps, t
+
+    gib, reps, t = timed(threads, seconds)
+    quota = cpu_quota_cores()
     out = {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
            "sample": f"{reps} x verify of one {data.nbytes >> 20} MiB block ({bpc} B chunks, "
-                     f"RemoteBlockReader::verifyChecksum loop) split over {threads} threads, {t:.1f} s; "
-                     f"engine: {engine}"}
+                     f"RemoteBlockReader::verifyChecksum loop) split over {threads} threads "
+                     f"(= len(os.sched_getaffinity(0))), {t:.1f} s; engine: {engine}",
+           "nproc": os.cpu_count(), "cgroup_cpu_quota_cores": quota}
+    g1, r1, t1 = timed(1, seconds / 3)
+    out["one_core"] = {"value": round(g1, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
+                       "sample": f"{r1} x verify of the same block on 1 thread, {t1:.1f} s"}
     # the reference's production x86 engine is IntelAsmCrc32c (crc_pcl, 3-way crc32q + pclmul;
     # needs yasm, not buildable here): time its restatement too, the stronger CPU baseline
     if kind == "reference":
         bad2 = ctypes.c_int64(0)
-        fp = lambda reps: oracle().oracle_bench_verify(PCL, data.ctypes.data, data.nbytes, bpc, crc.ctypes.data,
-                                                       threads, reps, ctypes.byref(bad2))
-        r2 = max(1, int(seconds / 2 / max(fp(1), 1e-6)))
-        t2 = fp(r2)
-        if bad2.value == -1:
-            out["pcl_port"] = {"value": round(data.nbytes * r2 / t2 / 2**30, 3), "unit": "GiB/s", "cores": threads,
-                               "kind": "port",
-                               "engine": "oracle crc_pcl restatement (IntelAsmCrc32c behaviour, "
-                                         "src/common/crc_iscsi_v_pcl.asm:93-340)"}
+        fp = lambda n, reps: oracle().oracle_bench_verify(PCL, data.ctypes.data, data.nbytes, bpc, crc.ctypes.data,
+                                                          n, reps, ctypes.byref(bad2))
+        pcl = {}
+        for name, n in (("all_cores", threads), ("one_core", 1)):
+            r2 = max(1, int(seconds / 4 / max(fp(n, 1), 1e-6)))
+            t2 = fp(n, r2)
+            if bad2.value == -1:
+                pcl[name] = {"value": round(data.nbytes * r2 / t2 / 2**30, 3), "unit": "GiB/s", "cores": n}
+        out["pcl_port"] = dict(pcl, kind="port",
+                               engine="oracle crc_pcl restatement (IntelAsmCrc32c behaviour, "
+                                      "src/common/crc_iscsi_v_pcl.asm:93-340)")
     # BASELINE.json configs[0]: one 64 KiB packet (128 x 512 B chunks) through the reference
     # CPU path on one core, 10^4 repetitions timed inside the C loop
     if ref is not None and ref.ref_hw_available():
@@ -364,20 +478,27 @@ def pmc_traffic(args):
 
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        sys.exit(spawn_ranks(args.gpus))  # nothing in this process has touched a GPU
+    if args.plumbing_check:
+        return plumbing_check(args)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and rank == 0:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; the launcher's world size is used")
     # RCCL for the timing barrier/all-reduce on a GPU node; HDFS3_BENCH_BACKEND=gloo lets
     # a 1-GPU box rehearse N ranks (device = LOCAL_RANK mod visible GPUs, identity on 8)
     backend = os.environ.get("HDFS3_BENCH_BACKEND", "nccl")
-    if world > 1:
-        dist.init_process_group(backend, init_method="env://")
     ndev = max(1, torch.cuda.device_count())
     torch.cuda.set_device(local % ndev)
     device = torch.device("cuda", local % ndev)
+    if world > 1:
+        dist.init_process_group(backend, init_method="env://")
     coll_device = device if backend == "nccl" else torch.device("cpu")
 
     from libhdfs3_amd.engine import CrcContext
@@ -412,10 +533,12 @@ def main():
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the roofline pass")
     overlap = args.mode == "verify" and not args.no_overlap
-    # (0b) barriered pass (reported beside the overlapped `value`): max(D - K, 1000) untimed
-    # then K timed launches, every one with the AQL barrier bit (plain
-    # hdfs3_crc32c_verify_dev_async). It runs before the warmup: together with (0) it keeps the GPU under
-    # sustained load for ~100 ms before the timed region, whatever W is
+    alg_bytes = work.nchunks * (args.bpc + 4)  # verify reads data + CRC; compute reads data, writes CRC
+    # (0b) barriered pass (reported beside the overlapped `value`, first-class: it is what a
+    # caller issuing one plain hdfs3_crc32c_verify_dev_async per block gets): max(D - K, 1000)
+    # untimed then K timed launches, every one with the AQL barrier bit. It runs before the
+    # warmup: together with (0) it keeps the GPU under sustained load for ~100 ms before the
+    # timed region, whatever W is
     barriered = None
     if overlap:
         result.zero_()
@@ -428,17 +551,19 @@ def main():
         if bool((result != 0).any().item()):
             raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the barriered pass")
         bl = b0.elapsed_time(b1) * 1e-3 / K
-        nb = work.nchunks * (args.bpc + 4)
         barriered = {"api": "hdfs3_crc32c_verify_dev_async (AQL barrier bit on every launch)",
-                     "value": round(block_bytes / bl / 2**30, 2), "unit": "GiB/s", "avg_launch_us": round(bl * 1e6, 2),
-                     "achieved_GBps": round(nb / bl / 1e9, 1), "frac": round(nb / bl / 1e9 / HBM_PEAK_GBPS, 4)}
+                     "value": round(block_bytes / bl / 2**30, 2), "unit": "GiB/s", "ms_per_step": round(bl * 1e3, 4),
+                     "avg_launch_us": round(bl * 1e6, 2), "achieved_GBps": round(alg_bytes / bl / 1e9, 1),
+                     "frac": round(alg_bytes / bl / 1e9 / HBM_PEAK_GBPS, 4),
+                     "timing": "HIP events on the launch stream around K barriered launches"}
     result.zero_()
     run_steps(work, ctx, args.mode, W, result, overlap=overlap)
     graphs = StepGraphs(torch, work, ctx, args.mode, K, result, stream) if args.graph else None
     result.zero_()
     torch.cuda.synchronize()
-    # (1) timed region for `value`: W warmup steps done, now exactly K steps (graph replays, or K eager launches), nothing
-    # else on the stream; HIP events on the launch stream bracket the same region
+    # (1) timed region: W warmup steps done, now exactly K steps (graph replays, or K eager
+    # launches), nothing else on the stream, bracketed by barrier + synchronize on both sides.
+    # The clock of `value`: HIP events on the launch stream around the K steps (max over ranks).
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
@@ -451,19 +576,18 @@ def main():
         run_steps(work, ctx, args.mode, K, result, overlap=overlap)
     ev1.record(stream)
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    region_launch_s = ev0.elapsed_time(ev1) * 1e-3 / K
+    host_elapsed = time.perf_counter() - t0
+    elapsed = ev0.elapsed_time(ev1) * 1e-3
     if world > 1:
         dist.barrier()
-        elapsed = max_over_ranks(dist, elapsed, coll_device)
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the timed region")
-    launch_ms = [events[2 * s].elapsed_time(events[2 * s + 1]) for s in range(D)]
-    eager_launch_s = sum(launch_ms[-K:]) / K * 1e-3  # the last K of the diagnostic pass
-    avg_launch_s = region_launch_s
-    payload = block_bytes
-    alg_bytes = work.nchunks * (args.bpc + 4)  # verify reads data + CRC; compute reads data, writes CRC
-    value = aggregate_rate(payload * K, world, elapsed)
+    my_rate = block_bytes * K / elapsed / 2**30
+    rows = gather_per_rank(dist, world, rank, [rank, local % ndev, rank_seed(rank), elapsed, host_elapsed, my_rate],
+                           coll_device)
+    elapsed_max = max(r[3] for r in rows)
+    host_max = max(r[4] for r in rows)
+    value = aggregate_rate(block_bytes * K, world, elapsed_max)
 
     if rank != 0:
         if world > 1:
@@ -471,21 +595,31 @@ def main():
             dist.destroy_process_group()
         return
 
+    launch_ms = [events[2 * s].elapsed_time(events[2 * s + 1]) for s in range(D)]
+    eager_launch_s = sum(launch_ms[-K:]) / K * 1e-3  # the last K of the diagnostic pass
+    avg_launch_s = elapsed / K  # rank 0's own launches, same clock as value
     achieved = alg_bytes / avg_launch_s / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
                 "alg_bytes_per_launch": alg_bytes, "avg_launch_us": round(avg_launch_s * 1e6, 2),
-                "timing": "HIP events on the launch stream over the timed region / K",
+                "timing": "HIP events on the launch stream around the K timed steps / K (the clock of value)",
                 "eager_per_launch_us": round(eager_launch_s * 1e6, 2)}
     extra = {}
+    lab = None
     if world == 1:
         try:
-            whole, per_block = stream_read_ceiling(torch, work, ctx, overlap=overlap)
+            lab = lab_context(work, stream)
+            whole, per_block = stream_read_ceiling(torch, work, lab, overlap=overlap)
             roofline["achievable_read_GBps"] = round(whole, 1)
             # the same shape as the timed steps: a plain read of one block per launch, with
             # the same launch mode (overlapped or barriered)
             roofline["achievable_read_per_block_launch_GBps"] = round(per_block, 1)
-            roofline["frac_of_achievable_per_block"] = round(achieved / (per_block * alg_bytes / payload), 4)
+            roofline["frac_of_achievable_per_block"] = round(achieved / (per_block * alg_bytes / block_bytes), 4)
+            if barriered is not None:
+                _, per_block_b = stream_read_ceiling(torch, work, lab, overlap=False)
+                barriered["achievable_read_per_block_launch_GBps"] = round(per_block_b, 1)
+                barriered["frac_of_achievable_per_block"] = round(
+                    barriered["achieved_GBps"] / (per_block_b * alg_bytes / block_bytes), 4)
         except Exception as e:
             log("stream ceiling failed:", e)
         if barriered is not None:
@@ -499,8 +633,8 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(work, args.cpu_seconds, args.bpc)
-    if args.sweep and world == 1:
-        log(json.dumps({"lane_read_GBps": round(lane_read_rate(torch, work, ctx), 1)}))
+    if args.sweep and world == 1 and lab is not None:
+        log(json.dumps({"lane_read_GBps": round(lane_read_rate(torch, work, lab), 1)}))
     if world == 1 and not args.no_pmc:
         traffic, note = pmc_traffic(args)
         roofline["traffic"] = int(traffic) if traffic else None
@@ -508,17 +642,23 @@ def main():
 
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": K,
-        "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True,
+        "warmup": W, "ms_per_step": round(elapsed_max / K * 1e3, 4), "higher_is_better": True,
+        "host_ms_per_step": round(host_max / K * 1e3, 4),
+        "clock": "value, ms_per_step and roofline: HIP events on each rank's launch stream around its K timed "
+                 "steps (max over ranks); host_ms_per_step: host wall clock of the same barrier+synchronize bracket",
         "launch": (f"HIP graph replay, {graphs.per} single-block launches per graph" if graphs is not None
                    else "eager, one launch per step; launches after the first overlap their predecessor "
                         "(HDFS3_LAUNCH_OVERLAP_PREVIOUS)" if overlap else "eager, one barriered launch per step"),
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (torch.randint bytes)",
         "config": {"workload": f"{args.mode} of one {args.block_mib} MiB HDFS block per step, "
-                               f"{args.bpc} B chunks, device-resident (BASELINE.json configs[1])",
+                               f"{args.bpc} B chunks, device-resident (BASELINE.json configs[1]"
+                               f"{'; configs[3] sharding: one block set per GPU' if world > 1 else ''})",
                    "bpc": args.bpc, "block_bytes": block_bytes, "chunks_per_block": work.nchunks,
                    "blocks_rotated_per_gpu": args.blocks, "mode": args.mode,
                    "parallelism": f"{world} GPU(s), independent blocks one set per GPU, no collectives"},
         "roofline": roofline, "cpu_baseline": cpu,
+        "per_rank": [{"rank": int(r[0]), "device": int(r[1]), "seed": int(r[2]), "ms_per_step": round(r[3] / K * 1e3, 4),
+                      "value": round(r[5], 2)} for r in rows],
     }
     if "barriered" in extra:
         line["barriered"] = extra["barriered"]
@@ -526,8 +666,8 @@ def main():
         line["batched"] = extra["batched"]
     if cpu:
         line["gpu_over_cpu"] = round(value / cpu["value"], 1)
-        if "pcl_port" in cpu:
-            line["gpu_over_cpu_pcl"] = round(value / cpu["pcl_port"]["value"], 1)
+        if "pcl_port" in cpu and "all_cores" in cpu["pcl_port"]:
+            line["gpu_over_cpu_pcl"] = round(value / cpu["pcl_port"]["all_cores"]["value"], 1)
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

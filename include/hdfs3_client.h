@@ -125,13 +125,20 @@ typedef struct hdfs3_local_reader hdfs3_local_reader;
 typedef struct hdfs3_local_opts {
     int device;
     int verify;               /* 0: no verification                                     */
-    int32_t buffer_size;      /* input.localread.default.buffersize (1 MiB), chunk-rounded */
+    int32_t buffer_size;      /* input.localread.default.buffersize (1 MiB), chunk-rounded;
+                                 at most 1 GiB (-EINVAL above)                           */
     int window_buffers;       /* buffers per GPU window (4)                             */
+    uint32_t flags;           /* 0, or HDFS3_LOCAL_CRC32_AS_ZLIB                        */
 } hdfs3_local_opts;
 
+/* By default a .meta of type CHECKSUM_CRC32 is verified with CRC32C, exactly as the
+ * reference does (both types select its CRC32C engine, LocalBlockReader.cpp:85-98), so such
+ * a block fails with ChecksumException (-EIO) in both. With this flag it is verified with
+ * the zlib polynomial the meta declares instead (an opt-in departure from the reference). */
+#define HDFS3_LOCAL_CRC32_AS_ZLIB 1u
+
 /* num_bytes <= 0 takes the block file's size; offset skips like LocalBlockReader::skip.
- * -EIO on a bad version or unknown type. CHECKSUM_CRC32 meta is verified with the zlib
- * polynomial (the reference uses its CRC32C engine there, LocalBlockReader.cpp:82-96). */
+ * -EIO on a bad version or unknown type; -EINVAL on unknown flags. */
 int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_t num_bytes, int64_t offset,
                             const hdfs3_local_opts *opts, hdfs3_local_reader **out);
 int32_t hdfs3_local_reader_read(hdfs3_local_reader *r, void *buf, int32_t len);

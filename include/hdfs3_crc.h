@@ -20,9 +20,11 @@
  *
  * Checksum words are CRC32C (reflected poly 0x82F63B78, init/xorout 0xFFFFFFFF)
  * stored BIG-ENDIAN, one per bytesPerChecksum chunk (src/common/BigEndian.h:43-59).
- * bpc must be a positive multiple of 4 (the reference requires a multiple of 512
- * for writes, SessionConfig.cpp:112; readers accept any bpc > 0 from the
- * datanode, so bpc % 4 != 0 is rejected with -EINVAL rather than mis-verified).
+ * bpc is any positive byte count, as readers accept any bytesPerChecksum > 0 from a
+ * datanode (RemoteBlockReader.cpp:150-156) or a .meta header (LocalBlockReader.cpp:110-115);
+ * the reference requires a multiple of 512 only for writes (SessionConfig.cpp:112).
+ * bpc in {512, 1024, 2048, 4096} on 16-byte aligned data takes the coalesced round kernels;
+ * every other size is verified byte-exactly by the chunk-per-lane kernel.
  *
  * Threading: one ctx per stream/thread, like one Checksum instance per reader or
  * writer in the reference. Distinct contexts share nothing but the device.
@@ -158,6 +160,39 @@ int hdfs3_crc32c_verify_blocks_dev(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *bl
 int hdfs3_crc32c_verify_blocks_dev_async(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n,
                                          uint32_t bpc, int check_short_tail, uint64_t *d_result);
 int hdfs3_crc32c_compute_blocks_dev(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, uint32_t bpc);
+
+/* ---- independent blocks over several GPUs (BASELINE.json configs[3]) ----------
+ * An HDFS block is independent of every other block, so a multi-block job shards with no
+ * exchange step: block b goes to device devices[b % n_devices], each device
+ * has its own context, HIP stream and host worker thread, and nothing crosses devices (no
+ * RCCL, no peer access). The reference has no multi-GPU analogue; it verifies blocks one
+ * packet at a time on the reading thread.
+ * hdfs3_multi_create: one context and worker per entry of devices[] (normally distinct; a
+ * device listed twice gets two workers with their own streams); 0 or -errno.
+ * Like a ctx, a hdfs3_multi serves one caller at a time. */
+typedef struct hdfs3_multi hdfs3_multi;
+int hdfs3_multi_create(const int *devices, int n_devices, hdfs3_multi **out);
+void hdfs3_multi_destroy(hdfs3_multi *m);
+int hdfs3_multi_device_count(hdfs3_multi *m);
+/* Device-resident blocks: blocks[b] must live on devices[b % n_devices] (checked: -EINVAL).
+ * Every device verifies its blocks back to back on its own stream (after the first, each
+ * launch overlaps its predecessor, HDFS3_LAUNCH_OVERLAP_PREVIOUS), all devices at once;
+ * returns when every device is done. first_bad[b] = first mismatching chunk of block b, or
+ * -1 (each block checked exactly as hdfs3_crc32c_verify_dev would check it alone). */
+int hdfs3_crc32c_verify_blocks_multi(hdfs3_multi *m, const hdfs3_dev_block *blocks, size_t n, uint32_t bpc,
+                                     int check_short_tail, int64_t *first_bad);
+int hdfs3_crc32c_compute_blocks_multi(hdfs3_multi *m, const hdfs3_dev_block *blocks, size_t n, uint32_t bpc);
+/* Host-memory blocks (data and stored words in host memory, pinned or pageable): block b is
+ * staged to devices[b % n_devices] through that device's context (hdfs3_crc32c_verify), so
+ * the H2D copies of different devices run over their own PCIe links at once. */
+typedef struct hdfs3_host_block {
+    const void *data;
+    const void *crc_be;  /* verify: stored BE32 words; compute: written (cast away const) */
+    uint64_t len;
+} hdfs3_host_block;
+int hdfs3_crc32c_verify_host_multi(hdfs3_multi *m, const hdfs3_host_block *blocks, size_t n, uint32_t bpc,
+                                   int check_short_tail, int64_t *first_bad);
+int hdfs3_crc32c_compute_host_multi(hdfs3_multi *m, const hdfs3_host_block *blocks, size_t n, uint32_t bpc);
 
 /* ---- packet-stream API -----------------------------------------------------
  * n packets of one block in one arena (wire layout of a5/a6 in SURVEY.md §8a).

@@ -1,0 +1,84 @@
+/*
+ * hdfs3_hdfs.h — libhdfs3's C file-I/O surface (src/client/hdfs.h) over the GPU-verified
+ * streams of hdfs3_client.h.
+ *
+ * Every function below has exactly the prototype of the reference's hdfs.h (cited per
+ * line), with the same argument checks, return values and errno convention as
+ * src/client/Hdfs.cpp: a caller written against hdfs.h links against libhdfs3_crc.so and
+ * runs unchanged. tests/test_reference_headers.py compiles the implementation
+ * (csrc/client/hdfs_shim.cpp) with the reference's own hdfs.h force-included, so the
+ * compiler checks that every definition matches the reference's declaration.
+ *
+ * What stays outside the checksum path is the namenode: hdfsConnect/hdfsOpenFile resolve
+ * a path through ClientProtocol RPC (getBlockLocations, create/addBlock) and a write
+ * pipeline to datanodes (Pipeline.cpp). Here an hdfsFS is an in-process table that holds,
+ * per path, what the namenode and the pipeline would provide:
+ *   - for reading: the file's LocatedBlocks (hdfs3_fs_add_file), read through
+ *     hdfs3_input_* (datanode OP_READ_BLOCK, GPU verify, replica failover);
+ *   - for writing: a packet sink (hdfs3_fs_set_sink), fed by hdfs3_output_* with
+ *     packets byte-identical to Packet::getBuffer whose CRCs the GPU computed.
+ */
+#ifndef HDFS3_HDFS_H
+#define HDFS3_HDFS_H
+
+#include <fcntl.h>
+#include <stdint.h>
+#include <time.h>
+
+#include "hdfs3_client.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* hdfs.h:56-69 */
+typedef int32_t tSize;
+typedef time_t tTime;
+typedef int64_t tOffset;
+typedef uint16_t tPort;
+struct HdfsFileSystemInternalWrapper;
+typedef struct HdfsFileSystemInternalWrapper *hdfsFS;
+struct HdfsFileInternalWrapper;
+typedef struct HdfsFileInternalWrapper *hdfsFile;
+
+/* ---- the hdfs.h functions (reference prototypes, Hdfs.cpp semantics) ---------------- */
+const char *hdfsGetLastError();                                         /* hdfs.h:80  */
+int hdfsFileIsOpenForRead(hdfsFile file);                               /* hdfs.h:88  */
+int hdfsFileIsOpenForWrite(hdfsFile file);                              /* hdfs.h:96  */
+int hdfsDisconnect(hdfsFS fs);                                          /* hdfs.h:303 */
+/* O_RDONLY: the registered LocatedBlocks (ENOENT if none); O_WRONLY [| O_CREAT | O_SYNC]:
+ * the registered sink (ENOENT if none), blocksize 0 = the fs's writer default, which must
+ * be a multiple of the chunk size (EINVAL); O_RDWR, O_EXCL|O_CREAT: ENOTSUP (Hdfs.cpp:653);
+ * O_APPEND (append to a partial last block, Pipeline recovery): ENOTSUP. */
+hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, short replication,
+                      tOffset blocksize);                                /* hdfs.h:319 */
+int hdfsCloseFile(hdfsFS fs, hdfsFile file);                            /* hdfs.h:332 */
+int hdfsExists(hdfsFS fs, const char *path);                            /* hdfs.h:340 */
+int hdfsSeek(hdfsFS fs, hdfsFile file, tOffset desiredPos);             /* hdfs.h:350 */
+tOffset hdfsTell(hdfsFS fs, hdfsFile file);                             /* hdfs.h:358 */
+tSize hdfsRead(hdfsFS fs, hdfsFile file, void *buffer, tSize length);   /* hdfs.h:374 */
+tSize hdfsPread(hdfsFS fs, hdfsFile file, void *buffer, tSize length, tOffset position); /* :391 */
+tSize hdfsWrite(hdfsFS fs, hdfsFile file, const void *buffer, tSize length); /* hdfs.h:401 */
+int hdfsFlush(hdfsFS fs, hdfsFile file);                                /* hdfs.h:409 */
+int hdfsHFlush(hdfsFS fs, hdfsFile file);                               /* hdfs.h:418 */
+int hdfsSync(hdfsFS fs, hdfsFile file);                                 /* hdfs.h:427 */
+int hdfsAvailable(hdfsFS fs, hdfsFile file);                            /* hdfs.h:436 */
+
+/* ---- the namenode/pipeline stand-in (not in hdfs.h) ---------------------------------
+ * hdfs3_fs_new: an empty path table; read_opts/write_opts are the session's defaults
+ * (NULL: device 0, verify on, batch 64 / bpc 512, packet 64 KiB, block 128 MiB, batch 64);
+ * client_name is the DFSClient name sent in OP_READ_BLOCK. NULL with errno on failure.
+ * Release with hdfsDisconnect. */
+hdfsFS hdfs3_fs_new(const char *client_name, const hdfs3_reader_opts *read_opts,
+                    const hdfs3_writer_opts *write_opts);
+/* what getBlockLocations returns for `path` (blocks in file order, contiguous; copied).
+ * 0, or -1 with errno (EINVAL). Replaces an existing entry. */
+int hdfs3_fs_add_file(hdfsFS fs, const char *path, const hdfs3_located_block *blocks, int n_blocks);
+/* where the write pipeline of `path` starts: every packet of a file opened O_WRONLY goes to
+ * sink(user, ...) (hdfs3_client.h), in seqno order. 0, or -1 with errno (EINVAL). */
+int hdfs3_fs_set_sink(hdfsFS fs, const char *path, hdfs3_packet_sink sink, void *user);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HDFS3_HDFS_H */

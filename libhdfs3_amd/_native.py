@@ -11,6 +11,9 @@ import os
 from ctypes import POINTER, c_int, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libhdfs3_crc.so")
+# measurement library (tools/, the A/B tests, bench.py's read ceiling): the same sources built
+# with HDFS3_LAB=1 — the kernel-variant knob and the hdfs3x_* hooks live only there
+LAB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libhdfs3_crc_lab.so")
 
 
 class Hdfs3CrcError(RuntimeError):
@@ -84,6 +87,15 @@ PUBLIC_API = {
     "hdfs3_block_checksum_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p, POINTER(c_uint64)]),
     "hdfs3_block_checksum_crcs": (c_int, [c_void_p, c_uint64, c_void_p]),
     "hdfs3_file_checksum_md5md5crc": (c_int, [c_void_p, c_size_t, c_void_p]),
+    "hdfs3_multi_create": (c_int, [POINTER(c_int), c_int, POINTER(c_void_p)]),
+    "hdfs3_multi_destroy": (None, [c_void_p]),
+    "hdfs3_multi_device_count": (c_int, [c_void_p]),
+    "hdfs3_crc32c_verify_blocks_multi": (c_int, [c_void_p, POINTER(DevBlock), c_size_t, c_uint32, c_int,
+                                                 POINTER(c_int64)]),
+    "hdfs3_crc32c_compute_blocks_multi": (c_int, [c_void_p, POINTER(DevBlock), c_size_t, c_uint32]),
+    "hdfs3_crc32c_verify_host_multi": (c_int, [c_void_p, POINTER(DevBlock), c_size_t, c_uint32, c_int,
+                                               POINTER(c_int64)]),
+    "hdfs3_crc32c_compute_host_multi": (c_int, [c_void_p, POINTER(DevBlock), c_size_t, c_uint32]),
 }
 
 class BlockId(ctypes.Structure):
@@ -115,7 +127,8 @@ class LocatedBlock(ctypes.Structure):
 class LocalOpts(ctypes.Structure):
     """hdfs3_local_opts (include/hdfs3_client.h)."""
 
-    _fields_ = [("device", c_int), ("verify", c_int), ("buffer_size", ctypes.c_int32), ("window_buffers", c_int)]
+    _fields_ = [("device", c_int), ("verify", c_int), ("buffer_size", ctypes.c_int32), ("window_buffers", c_int),
+                ("flags", c_uint32)]
 
 
 class PacketInfo(ctypes.Structure):
@@ -178,7 +191,30 @@ CLIENT_API = {
     "hdfs3_output_close": (c_int, [c_void_p]),
 }
 
-# measurement hooks (bench.py only; not in the public header)
+# every symbol include/hdfs3_hdfs.h declares (hdfs.h prototypes + the namenode stand-in)
+HDFS_API = {
+    "hdfsGetLastError": (ctypes.c_char_p, []),
+    "hdfsFileIsOpenForRead": (c_int, [c_void_p]),
+    "hdfsFileIsOpenForWrite": (c_int, [c_void_p]),
+    "hdfsDisconnect": (c_int, [c_void_p]),
+    "hdfsOpenFile": (c_void_p, [c_void_p, ctypes.c_char_p, c_int, c_int, ctypes.c_short, c_int64]),
+    "hdfsCloseFile": (c_int, [c_void_p, c_void_p]),
+    "hdfsExists": (c_int, [c_void_p, ctypes.c_char_p]),
+    "hdfsSeek": (c_int, [c_void_p, c_void_p, c_int64]),
+    "hdfsTell": (c_int64, [c_void_p, c_void_p]),
+    "hdfsRead": (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, ctypes.c_int32]),
+    "hdfsPread": (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, ctypes.c_int32, c_int64]),
+    "hdfsWrite": (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, ctypes.c_int32]),
+    "hdfsFlush": (c_int, [c_void_p, c_void_p]),
+    "hdfsHFlush": (c_int, [c_void_p, c_void_p]),
+    "hdfsSync": (c_int, [c_void_p, c_void_p]),
+    "hdfsAvailable": (c_int, [c_void_p, c_void_p]),
+    "hdfs3_fs_new": (c_void_p, [ctypes.c_char_p, c_void_p, c_void_p]),
+    "hdfs3_fs_add_file": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_int]),
+    "hdfs3_fs_set_sink": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_void_p]),
+}
+
+# measurement hooks (libhdfs3_crc_lab.so only; not in any public header)
 BENCH_API = {
     "hdfs3x_stream_read": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     "hdfs3x_stream_read_ex": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_uint32]),
@@ -190,12 +226,12 @@ BENCH_API = {
 }
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
+def load(path: str = LIB_PATH, lab: bool = False) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise ImportError(f"{path} is missing: run `make` (or __graft_entry__.build()) first; "
                           "libhdfs3_amd has no CPU fallback")
     lib = ctypes.CDLL(path, use_errno=True)  # the hdfs.h-style calls report through errno
-    for table in (PUBLIC_API, CLIENT_API, BENCH_API):
+    for table in (PUBLIC_API, CLIENT_API, HDFS_API) + ((BENCH_API,) if lab else ()):
         for name, (res, args) in table.items():
             fn = getattr(lib, name)
             fn.restype = res
@@ -204,13 +240,25 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
 
 
 _LIB: ctypes.CDLL | None = None
+_LAB: ctypes.CDLL | None = None
 
 
 def lib() -> ctypes.CDLL:
+    """The product library (libhdfs3_crc.so): what every product caller loads."""
     global _LIB
     if _LIB is None:
         _LIB = load()
     return _LIB
+
+
+def lab() -> ctypes.CDLL:
+    """The measurement library (libhdfs3_crc_lab.so): production code plus the A/B variant
+    knob (hdfs3x_set_variant) and measurement kernels. A context belongs to the library that
+    created it: never pass a lab ctx to lib() calls or the reverse."""
+    global _LAB
+    if _LAB is None:
+        _LAB = load(LAB_PATH, lab=True)
+    return _LAB
 
 
 LOOPBACK_PATH = os.path.join(os.path.dirname(LIB_PATH), "libhdfs3_loopback.so")
@@ -238,7 +286,7 @@ def loopback() -> ctypes.CDLL:
     return _LOOPBACK
 
 
-def check(fn: str, rc: int) -> int:
+def check(fn: str, rc: int, library: ctypes.CDLL | None = None) -> int:
     if rc < 0:
-        raise Hdfs3CrcError(fn, rc, lib().hdfs3_crc_last_error().decode(errors="replace"))
+        raise Hdfs3CrcError(fn, rc, (library or lib()).hdfs3_crc_last_error().decode(errors="replace"))
     return rc

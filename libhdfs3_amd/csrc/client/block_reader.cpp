@@ -138,6 +138,7 @@ struct hdfs3_block_reader {
     int64_t recv_cursor = 0;   // "cursor" as seen by readNextPacket for the next packet
     int64_t last_seqno = -1;
     bool range_done = false;   // every packet of the range (and the trailer) received
+    bool trailer_ok = false;   // the trailer was the empty last packet (readTrailingEmptyPacket)
     bool have_pending_hdr = false;
     wire::PacketHeader pending_hdr;
 
@@ -188,7 +189,9 @@ struct hdfs3_block_reader {
         case wire::kChecksumCrc32: checksum_size = 4; tables = ctx->d_tables_by[1]; break;
         default: return sticky(-EPROTO, "RemoteBlockReader cannot recognize checksum type");
         }
-        if (chunk_size == 0 || (checksum_size && (chunk_size & 3u)))
+        // any bytesPerChecksum > 0 (:150-156; the reference's int chunkSize rejects >= 2^31, and
+        // a zero size would divide by zero in its readNextPacket, :239)
+        if (chunk_size == 0 || chunk_size > 0x7FFFFFFFu)
             return sticky(-EPROTO, "RemoteBlockReader invalid chunk size");
         const int64_t first = int64_t(r.chunk_offset);
         if (first < 0 || first > start || first <= start - int64_t(chunk_size))
@@ -264,7 +267,10 @@ struct hdfs3_block_reader {
                 // readTrailingEmptyPacket (:279-287): the datanode follows with an empty last packet
                 wire::PacketHeader t;
                 if (int rc = read_header(t)) return rc;
-                if (t.last_packet_in_block && t.data_len == 0) last_seqno = t.seqno;
+                if (t.last_packet_in_block && t.data_len == 0) {
+                    last_seqno = t.seqno;
+                    trailer_ok = true;
+                }
                 range_done = true;
             }
         }
@@ -354,9 +360,11 @@ struct hdfs3_block_reader {
         return 0;
     }
 
-    // sendStatus (:289-304), once every packet of the range verified and was handed out
+    // sendStatus (:289-304), once every packet of the range verified and was handed out —
+    // and only when the packet after the range was the empty last packet (:274-286): a
+    // datanode that keeps streaming gets no status, as from the reference
     void maybe_send_status() {
-        if (sent_status || error) return;
+        if (sent_status || error || !trailer_ok) return;
         {
             std::lock_guard<std::mutex> lk(mu);
             if (!recv_done || recv_error || !ready.empty()) return;
@@ -545,12 +553,14 @@ int hdfs3_block_reader_stats(hdfs3_block_reader *r, uint32_t *bpc, uint64_t *pac
     return 0;
 }
 
-// measurement hook (not in the public header): nanoseconds spent per phase so far
+#if HDFS3_LAB
+// measurement hook (libhdfs3_crc_lab.so only): nanoseconds spent per phase so far
 int hdfs3x_block_reader_timing(hdfs3_block_reader *r, uint64_t *out5) {
     if (!r || !out5) return fail(-EINVAL, "invalid argument");
     for (int i = 0; i < 5; ++i) out5[i] = r->t_ns[i].load();
     return 0;
 }
+#endif
 
 int hdfs3_block_reader_close(hdfs3_block_reader *r) {
     delete r;

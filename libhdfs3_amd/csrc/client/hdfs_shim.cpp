@@ -1,0 +1,282 @@
+// hdfs.h file-I/O surface (include/hdfs3_hdfs.h) over hdfs3_input_* / hdfs3_output_*.
+//
+// Mirrors src/client/Hdfs.cpp function by function: the PARAMETER_ASSERT checks and their
+// errno (Hdfs.cpp:75-80), hdfsRead/hdfsPread returning 0 at end of file and -1 + errno on
+// error (:826-862), hdfsWrite returning `length` (:864-881), hdfsFlush = hdfsHFlush
+// (:883-904), a thread-local last-error string initialised to "Success" (:59, :329).
+// Host code only: the GPU work happens inside the streams.
+#include "hdfs3_hdfs.h"
+
+#include "hdfs3_crc.h"
+
+#include <cerrno>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local char g_msg[4096] = "Success";
+
+void set_msg(const char *m) {
+    std::strncpy(g_msg, m ? m : "", sizeof(g_msg) - 1);
+    g_msg[sizeof(g_msg) - 1] = 0;
+}
+
+// PARAMETER_ASSERT (Hdfs.cpp:75-80): message = strerror(eno), errno = eno
+#define PARAMETER_ASSERT(para, retval, eno) \
+    if (!(para)) {                          \
+        set_msg(std::strerror(eno));        \
+        errno = eno;                        \
+        return retval;                      \
+    }
+
+// a failed stream call already set errno; keep its message for hdfsGetLastError
+template <typename T>
+T stream_failed(T rv) {
+    const int e = errno;
+    set_msg(hdfs3_crc_last_error());
+    errno = e;
+    return rv;
+}
+
+struct FileEntry {
+    std::vector<hdfs3_located_block> blocks;
+    std::vector<std::vector<hdfs3_datanode>> replicas;
+    std::vector<std::string> strings;  // pool ids and host names the tables point into
+    bool located = false;  // registered by hdfs3_fs_add_file (a file of 0 blocks is empty)
+    hdfs3_packet_sink sink = nullptr;
+    void *user = nullptr;
+};
+
+}  // namespace
+
+struct HdfsFileSystemInternalWrapper {
+    std::string client_name;
+    hdfs3_reader_opts ropts{0, 1, 64, 0};
+    hdfs3_writer_opts wopts{0, 512, 65536, int64_t(128) << 20, 64};
+    std::mutex mu;
+    std::map<std::string, FileEntry> files;
+};
+
+struct HdfsFileInternalWrapper {
+    bool input = true;
+    hdfs3_input_stream *in = nullptr;
+    hdfs3_output_stream *out = nullptr;
+};
+
+extern "C" {
+
+const char *hdfsGetLastError() { return g_msg; }
+
+int hdfsFileIsOpenForRead(hdfsFile file) {
+    PARAMETER_ASSERT(file, 0, EINVAL);
+    return file->input ? 1 : 0;
+}
+
+int hdfsFileIsOpenForWrite(hdfsFile file) {
+    PARAMETER_ASSERT(file, 0, EINVAL);
+    return !file->input ? 1 : 0;
+}
+
+hdfsFS hdfs3_fs_new(const char *client_name, const hdfs3_reader_opts *read_opts,
+                    const hdfs3_writer_opts *write_opts) {
+    hdfsFS fs = new (std::nothrow) HdfsFileSystemInternalWrapper();
+    if (!fs) {
+        set_msg("Out of memory");
+        errno = ENOMEM;
+        return nullptr;
+    }
+    fs->client_name = client_name && *client_name ? client_name : "libhdfs3_amd";
+    if (read_opts) fs->ropts = *read_opts;
+    if (write_opts) fs->wopts = *write_opts;
+    return fs;
+}
+
+int hdfs3_fs_add_file(hdfsFS fs, const char *path, const hdfs3_located_block *blocks, int n_blocks) {
+    PARAMETER_ASSERT(fs && path && std::strlen(path) > 0 && n_blocks >= 0 && (n_blocks == 0 || blocks), -1,
+                     EINVAL);
+    FileEntry e;
+    e.located = true;
+    e.blocks.assign(blocks, blocks + n_blocks);
+    e.replicas.resize(size_t(n_blocks));
+    // deep copy: the caller's strings and replica tables may go away after this call
+    size_t nstr = 0;
+    for (int i = 0; i < n_blocks; ++i) nstr += 1 + size_t(blocks[i].n_replicas > 0 ? blocks[i].n_replicas : 0);
+    e.strings.reserve(nstr);  // no reallocation: the c_str() pointers below stay valid
+    for (int i = 0; i < n_blocks; ++i) {
+        PARAMETER_ASSERT(blocks[i].n_replicas >= 0 && (blocks[i].n_replicas == 0 || blocks[i].replicas), -1, EINVAL);
+        e.strings.emplace_back(blocks[i].block.pool_id ? blocks[i].block.pool_id : "");
+        e.blocks[size_t(i)].block.pool_id = e.strings.back().c_str();
+        for (int k = 0; k < blocks[i].n_replicas; ++k) {
+            PARAMETER_ASSERT(blocks[i].replicas[k].host, -1, EINVAL);
+            e.strings.emplace_back(blocks[i].replicas[k].host);
+            e.replicas[size_t(i)].push_back(hdfs3_datanode{e.strings.back().c_str(), blocks[i].replicas[k].port});
+        }
+        e.blocks[size_t(i)].replicas = e.replicas[size_t(i)].data();
+    }
+    std::lock_guard<std::mutex> lk(fs->mu);
+    FileEntry &slot = fs->files[path];
+    e.sink = slot.sink;
+    e.user = slot.user;
+    slot = std::move(e);
+    return 0;
+}
+
+int hdfs3_fs_set_sink(hdfsFS fs, const char *path, hdfs3_packet_sink sink, void *user) {
+    PARAMETER_ASSERT(fs && path && std::strlen(path) > 0 && sink, -1, EINVAL);
+    std::lock_guard<std::mutex> lk(fs->mu);
+    FileEntry &e = fs->files[path];
+    e.sink = sink;
+    e.user = user;
+    return 0;
+}
+
+int hdfsDisconnect(hdfsFS fs) {
+    delete fs;  // Hdfs.cpp:629-636: a null fs is not an error
+    return 0;
+}
+
+hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, short replication,
+                      tOffset blocksize) {
+    PARAMETER_ASSERT(fs && path && std::strlen(path) > 0, nullptr, EINVAL);
+    PARAMETER_ASSERT(bufferSize >= 0 && replication >= 0 && blocksize >= 0, nullptr, EINVAL);
+    PARAMETER_ASSERT(!(flags & O_RDWR) && !((flags & O_EXCL) && (flags & O_CREAT)), nullptr, ENOTSUP);
+    // appending to a block's partial last chunk needs the pipeline's recovery path
+    PARAMETER_ASSERT(!(flags & O_APPEND), nullptr, ENOTSUP);
+    const bool write = (flags & O_CREAT) || (flags & O_WRONLY);
+    hdfsFile file = new (std::nothrow) HdfsFileInternalWrapper();
+    if (!file) {
+        set_msg("Out of memory");
+        errno = ENOMEM;
+        return nullptr;
+    }
+    file->input = !write;
+    int rc;
+    {
+        // held across the open: hdfs3_input_open copies the located blocks out of the table
+        std::lock_guard<std::mutex> lk(fs->mu);
+        auto it = fs->files.find(path);
+        if (it == fs->files.end() || (write ? !it->second.sink : !it->second.located)) {
+            delete file;
+            set_msg((std::string(write ? "no write pipeline registered for " : "file does not exist: ") + path).c_str());
+            errno = ENOENT;  // FileNotFoundException -> ENOENT (Hdfs.cpp:243-327)
+            return nullptr;
+        }
+        const FileEntry &e = it->second;
+        if (write) {
+            hdfs3_writer_opts o = fs->wopts;
+            if (blocksize > 0) o.block_size = blocksize;
+            // OutputStreamImpl::open rejects a block size that is not a multiple of the chunk
+            // size (Hdfs.cpp:686-696) before anything reaches the pipeline
+            if (o.bytes_per_checksum == 0 || o.block_size % o.bytes_per_checksum != 0) {
+                delete file;
+                set_msg("OutputStreamImpl: block size is not the multiply of chunk size.");
+                errno = EINVAL;
+                return nullptr;
+            }
+            rc = hdfs3_output_open(&o, e.sink, e.user, &file->out);
+        } else {
+            rc = hdfs3_input_open(e.blocks.data(), int(e.blocks.size()), fs->client_name.c_str(), &fs->ropts,
+                                  &file->in);
+        }
+    }
+    if (rc < 0) {
+        delete file;
+        set_msg(hdfs3_crc_last_error());
+        errno = -rc;
+        return nullptr;
+    }
+    return file;
+}
+
+int hdfsCloseFile(hdfsFS fs, hdfsFile file) {
+    PARAMETER_ASSERT(fs, -1, EINVAL);
+    if (!file) return 0;
+    int rc = 0;
+    if (file->input) {
+        rc = hdfs3_input_close(file->in);
+    } else {
+        rc = hdfs3_output_close(file->out);  // frees the stream even on error
+    }
+    delete file;  // freed even after an I/O error (hdfs.h:328-330)
+    if (rc < 0) return stream_failed(-1);
+    return 0;
+}
+
+int hdfsExists(hdfsFS fs, const char *path) {
+    PARAMETER_ASSERT(fs && path && std::strlen(path) > 0, -1, EINVAL);
+    std::lock_guard<std::mutex> lk(fs->mu);
+    auto it = fs->files.find(path);
+    return it != fs->files.end() && it->second.located ? 0 : -1;
+}
+
+int hdfsSeek(hdfsFS fs, hdfsFile file, tOffset desiredPos) {
+    PARAMETER_ASSERT(fs && file && desiredPos >= 0, -1, EINVAL);
+    PARAMETER_ASSERT(file->input, -1, EINVAL);
+    if (hdfs3_input_seek(file->in, desiredPos) < 0) return stream_failed(-1);
+    return 0;
+}
+
+tOffset hdfsTell(hdfsFS fs, hdfsFile file) {
+    PARAMETER_ASSERT(fs && file, -1, EINVAL);
+    const int64_t t = file->input ? hdfs3_input_tell(file->in) : hdfs3_output_tell(file->out);
+    if (t < 0) return stream_failed(tOffset(-1));
+    return t;
+}
+
+tSize hdfsRead(hdfsFS fs, hdfsFile file, void *buffer, tSize length) {
+    PARAMETER_ASSERT(fs && file && buffer && length > 0, -1, EINVAL);
+    PARAMETER_ASSERT(file->input, -1, EINVAL);
+    const int32_t n = hdfs3_input_read(file->in, buffer, length);
+    if (n < 0) return stream_failed(tSize(-1));
+    return n;  // 0 at end of file (HdfsEndOfStream, Hdfs.cpp:831-832)
+}
+
+tSize hdfsPread(hdfsFS fs, hdfsFile file, void *buffer, tSize length, tOffset position) {
+    PARAMETER_ASSERT(fs && file && buffer && length > 0 && position >= 0, -1, EINVAL);
+    PARAMETER_ASSERT(file->input, -1, EINVAL);
+    const int32_t n = hdfs3_input_pread(file->in, position, buffer, length);
+    if (n < 0) return stream_failed(tSize(-1));
+    return n;
+}
+
+tSize hdfsWrite(hdfsFS fs, hdfsFile file, const void *buffer, tSize length) {
+    PARAMETER_ASSERT(fs && file && buffer && length > 0, -1, EINVAL);
+    PARAMETER_ASSERT(!file->input, -1, EINVAL);
+    if (hdfs3_output_write(file->out, buffer, length) < 0) return stream_failed(tSize(-1));
+    return length;
+}
+
+int hdfsFlush(hdfsFS fs, hdfsFile file) {
+    PARAMETER_ASSERT(fs && file, -1, EINVAL);
+    return hdfsHFlush(fs, file);
+}
+
+int hdfsHFlush(hdfsFS fs, hdfsFile file) {
+    PARAMETER_ASSERT(fs && file, -1, EINVAL);
+    PARAMETER_ASSERT(!file->input, -1, EINVAL);
+    if (hdfs3_output_flush(file->out) < 0) return stream_failed(-1);
+    return 0;
+}
+
+int hdfsSync(hdfsFS fs, hdfsFile file) {
+    PARAMETER_ASSERT(fs && file, -1, EINVAL);
+    PARAMETER_ASSERT(!file->input, -1, EINVAL);
+    if (hdfs3_output_sync(file->out) < 0) return stream_failed(-1);
+    return 0;
+}
+
+int hdfsAvailable(hdfsFS fs, hdfsFile file) {
+    PARAMETER_ASSERT(fs && file, -1, EINVAL);
+    PARAMETER_ASSERT(file->input, -1, EINVAL);
+    const int a = hdfs3_input_available(file->in);
+    if (a < 0) return stream_failed(-1);
+    return a < std::numeric_limits<int>::max() ? a : std::numeric_limits<int>::max();
+}
+
+}  // extern "C"

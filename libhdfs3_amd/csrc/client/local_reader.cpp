@@ -42,6 +42,7 @@ constexpr int kMetaHeader = 7;             // HEADER_SIZE: version 2 + type 1 + 
 constexpr int kSlots = 3;
 constexpr int32_t kDefaultBuffer = 1 << 20;  // input.localread.default.buffersize
 constexpr int kDefaultWindowBuffers = 4;  // 4 MiB windows: first delivery sooner
+constexpr int32_t kMaxBuffer = 1 << 30;     // largest local buffer / window
 
 int hip_err(hipError_t e, const char *what) {
     return fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
@@ -200,6 +201,7 @@ struct hdfs3_local_reader {
     hdfs3_crc_ctx *ctx = nullptr;
     bool verify = true;
     int checksum_type = 2;
+    uint32_t flags = 0;                      // hdfs3_local_opts.flags
     uint32_t chunk_size = 0;
     int32_t buffer_size = kDefaultBuffer;    // localBufferSize (chunk-rounded when verifying)
     uint32_t window = 0;                     // bytes per GPU window (multiple of buffer_size)
@@ -240,9 +242,10 @@ struct hdfs3_local_reader {
         case wire::kChecksumNull: verify = false; break;
         case wire::kChecksumCrc32c:
         case wire::kChecksumCrc32:
-            // Divergence, on purpose: the reference checks CRC32 meta with its CRC32C engine
-            // (:82-96), so such a block can never pass a short-circuit read there; this
-            // verifies it with the polynomial the meta declares.
+            // Both types select the CRC32C engine (:85-98), as in the reference: a block
+            // whose meta declares CHECKSUM_CRC32 is verified with CRC32C and so fails with
+            // ChecksumException there and here. HDFS3_LOCAL_CRC32_AS_ZLIB opts into the
+            // polynomial the meta declares instead (see engine_type()).
             chunk_size = (uint32_t(h[3]) << 24) | (uint32_t(h[4]) << 16) | (uint32_t(h[5]) << 8) | h[6];
             break;
         default:
@@ -252,6 +255,12 @@ struct hdfs3_local_reader {
             return sticky(-EIO, "LocalBlockReader get an invalid checksum parameter, bytes per check: " +
                                     std::to_string(chunk_size));
         return 0;
+    }
+
+    // the polynomial the GPU checks this block with
+    int engine_type() const {
+        return checksum_type == wire::kChecksumCrc32 && (flags & HDFS3_LOCAL_CRC32_AS_ZLIB) ? HDFS3_CHECKSUM_TYPE_CRC32
+                                                                                          : HDFS3_CHECKSUM_TYPE_CRC32C;
     }
 
     // ---- loader thread ------------------------------------------------------------------
@@ -435,6 +444,8 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
     };
     const int device = opts ? opts->device : 0;
     if (opts && opts->buffer_size > 0) r->buffer_size = opts->buffer_size;
+    if (opts) r->flags = opts->flags;
+    if (opts && (opts->flags & ~HDFS3_LOCAL_CRC32_AS_ZLIB)) return bail(fail(-EINVAL, "unknown local reader flags"));
     const int wbuf = opts && opts->window_buffers > 0 ? opts->window_buffers : kDefaultWindowBuffers;
     r->data_fd = ::open(data_path, O_RDONLY | O_CLOEXEC);
     if (r->data_fd < 0) return bail(fail(-errno, "LocalBlockReader: cannot open block file %s", data_path));
@@ -447,15 +458,23 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
     if (offset > r->length) return bail(fail(-EINVAL, "offset beyond the block"));
     if (int rc = r->open_meta(opts ? opts->verify != 0 : true)) return bail(rc);
     if (r->verify) {  // chunk-rounded local buffer (:112-116); reads start on a chunk (skip, :232-263)
-        r->buffer_size = int32_t((int64_t(r->buffer_size) + r->chunk_size - 1) / r->chunk_size * r->chunk_size);
+        const int64_t rounded = (int64_t(r->buffer_size) + r->chunk_size - 1) / r->chunk_size * r->chunk_size;
+        if (rounded > kMaxBuffer)
+            return bail(fail(-EINVAL, "LocalBlockReader: local buffer of %lld bytes (chunk-rounded) exceeds %d",
+                             (long long)rounded, kMaxBuffer));
+        r->buffer_size = int32_t(rounded);
         r->first = offset / r->chunk_size * r->chunk_size;
     } else {
+        if (r->buffer_size > kMaxBuffer) return bail(fail(-EINVAL, "LocalBlockReader: local buffer above 1 GiB"));
         r->first = offset;
     }
     r->cursor = offset;
-    r->window = uint32_t(std::min<int64_t>(int64_t(r->buffer_size) * wbuf, 1ll << 30) / r->buffer_size * r->buffer_size);
+    // whole buffers per window, at least one (the buffer itself is at most 1 GiB)
+    r->window = uint32_t(std::max<int64_t>(1, std::min<int64_t>(wbuf, kMaxBuffer / r->buffer_size)) * r->buffer_size);
     r->cap_data = (size_t(r->window) + 255) & ~size_t(255);
     const size_t crc_bytes = r->verify ? 4 * ((size_t(r->window) + r->chunk_size - 1) / r->chunk_size) : 0;
+    // the windows live on `device`, whatever the calling thread's current device is
+    DeviceGuard guard(device);
     LocalResources pooled;
     if (take_pooled(device, r->cap_data + crc_bytes, &pooled)) {
         r->ctx = pooled.ctx;
@@ -473,10 +492,7 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
             a.cap = r->cap_data + crc_bytes;
         }
     }
-    if (int rc = hdfs3_crc_ctx_set_checksum_type(r->ctx, r->checksum_type == wire::kChecksumCrc32
-                                                             ? HDFS3_CHECKSUM_TYPE_CRC32
-                                                             : HDFS3_CHECKSUM_TYPE_CRC32C))
-        return bail(rc);
+    if (int rc = hdfs3_crc_ctx_set_checksum_type(r->ctx, r->engine_type())) return bail(rc);
     for (int i = 0; i < kSlots; ++i) r->free_slots.push_back(i);
     if (r->first < r->length) {
         r->loader = std::thread([r] { r->run_loader(); });

@@ -1,5 +1,6 @@
 // Kernel variants kept for in-process A/B and diagnostics (hdfs3x_set_variant, tools/ab.py;
-// DESIGN.md §5.0). Separate translation unit so the production kernels build in parallel.
+// DESIGN.md §5.0), and the read-ceiling kernels of the bench. Linked into the measurement
+// library libhdfs3_crc_lab.so only (HDFS3_LAB=1); the product libhdfs3_crc.so never sees it.
 // Bit-exact variants are parity-tested (tests/test_gpu_parity.py); the diagnostic ones
 // (no HBM / no math / fake lookups / timestamps) give wrong results on purpose.
 #include "crc32c_device.h"
@@ -157,6 +158,51 @@ hipError_t launch_experiment(int variant, const ChunkLaunch &a, bool verify, con
     case 65536: return launch_exp_v<65536>(variant, a, verify, tab, fold, grid_cap, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+void set_variant(int v) { g_variant = v; }
+void set_trace(uint64_t *d_trace) { g_trace = d_trace; }
+
+hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,
+                              hipStream_t stream, bool overlap_previous) {
+    // grid < 0: non-temporal loads over |grid| workgroups (the production kernels' policy);
+    // overlap_previous: AQL packet without the barrier bit, as the overlapped verify launches
+    const bool nt = grid < 0;
+    const dim3 g(nt ? -grid : grid), b(256);
+    auto k = nt ? stream_read_kernel<true> : stream_read_kernel<false>;
+    if (overlap_previous)
+        hipExtLaunchKernelGGL(k, g, b, 0, stream, nullptr, nullptr, hipExtAnyOrderLaunch, d, len / 16, sink);
+    else
+        hipLaunchKernelGGL(k, g, b, 0, stream, d, len / 16, sink);
+    return hipGetLastError();
+}
+
+hipError_t launch_lane_read(const uint8_t *d, uint64_t len, uint32_t bpc, uint32_t *sink,
+                            int grid_cap, hipStream_t stream) {
+    const int variant = int(bpc >> 16);  // probe selector rides in the high bits of bpc
+    bpc &= 0xFFFFu;
+    const uint64_t chunks = len / bpc;
+    const uint64_t lanes = variant == 2 ? chunks * 8 : variant == 3 ? chunks * 4 : chunks;
+    const uint64_t need = (lanes + kBlockThreads - 1) / kBlockThreads;
+    const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
+#define LR(B, V) hipLaunchKernelGGL((lane_read_kernel<B, V>), dim3(grid), dim3(kBlockThreads), 0, stream, d, chunks, sink)
+#define LRV(B)                          \
+    switch (variant) {                  \
+    case 0: LR(B, 0); break;            \
+    case 1: LR(B, 1); break;            \
+    case 2: LR(B, 2); break;            \
+    case 3: LR(B, 3); break;            \
+    default: LR(B, 4); break;           \
+    }
+    switch (bpc) {
+    case 512: LRV(512); break;
+    case 2048: LRV(2048); break;
+    case 4096: LRV(4096); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef LRV
+#undef LR
+    return hipGetLastError();
 }
 
 }  // namespace hdfs3crc

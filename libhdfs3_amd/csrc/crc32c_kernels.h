@@ -76,7 +76,15 @@ hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_
                           unsigned long long *result, const uint32_t *d_tables, int grid_cap,
                           hipStream_t stream);
 
-// Measurement knob: selects kernel variants for in-process A/B (0 = production).
+// HDFS3_LAB=1 builds the measurement library (libhdfs3_crc_lab.so: tools/, the A/B tests):
+// the same production launchers plus a process-wide kernel-variant knob, the kernel
+// variants of crc32c_experiments.hip and the read-ceiling kernels. The product library
+// (libhdfs3_crc.so) is built with HDFS3_LAB=0: g_variant is the constant 0, so no
+// variant, diagnostic or wrong-on-purpose kernel is reachable from it.
+#ifndef HDFS3_LAB
+#define HDFS3_LAB 0
+#endif
+#if HDFS3_LAB
 void set_variant(int v);
 extern int g_variant;
 extern uint64_t *g_trace;
@@ -91,5 +99,8 @@ hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, in
                               hipStream_t stream, bool overlap_previous = false);
 hipError_t launch_lane_read(const uint8_t *d, uint64_t len, uint32_t bpc, uint32_t *sink,
                             int grid_cap, hipStream_t stream);
+#else
+constexpr int g_variant = 0;
+#endif
 
 }  // namespace hdfs3crc

@@ -5,8 +5,10 @@
 
 namespace hdfs3crc {
 
+#if HDFS3_LAB
 int g_variant = 0;          // measurement knob (hdfs3x_set_variant); 0 = production choice
 uint64_t *g_trace = nullptr;  // timestamp buffer of the traced variants
+#endif
 
 namespace {
 
@@ -22,7 +24,9 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
     // the half fold image): variant 44 in the A/B, 1-1.5 % per 128 MiB launch. Compute at
     // bpc 512 holds its CRC words in VGPRs and stores them in bursts (variant 47: -2.8 % per
     // GiB, -0.8 % per 128 MiB; profiles/r01_kernel_study/ab_holdstore.jsonl).
+#if HDFS3_LAB
     if (g_variant != 0) return launch_experiment(g_variant, a, V, tab, fold, grid_cap, s);
+#endif
     constexpr int kOpt = (BPC <= kRoundBytes ? kOptLeanFill : 0) | (!V && BPC == 512 ? kOptHoldStore : 0);
     if (a.overlap_previous)
         return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
@@ -223,51 +227,6 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
     if (e != hipSuccess) return e;
     return launch_packets(d_arena, reinterpret_cast<const DevPacket *>(d_stage), n, bpc, verify, check_short_tail,
                           result, d_tables, grid_cap, stream);
-}
-
-void set_variant(int v) { g_variant = v; }
-void set_trace(uint64_t *d_trace) { g_trace = d_trace; }
-
-hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,
-                              hipStream_t stream, bool overlap_previous) {
-    // grid < 0: non-temporal loads over |grid| workgroups (the production kernels' policy);
-    // overlap_previous: AQL packet without the barrier bit, as the overlapped verify launches
-    const bool nt = grid < 0;
-    const dim3 g(nt ? -grid : grid), b(256);
-    auto k = nt ? stream_read_kernel<true> : stream_read_kernel<false>;
-    if (overlap_previous)
-        hipExtLaunchKernelGGL(k, g, b, 0, stream, nullptr, nullptr, hipExtAnyOrderLaunch, d, len / 16, sink);
-    else
-        hipLaunchKernelGGL(k, g, b, 0, stream, d, len / 16, sink);
-    return hipGetLastError();
-}
-
-hipError_t launch_lane_read(const uint8_t *d, uint64_t len, uint32_t bpc, uint32_t *sink,
-                            int grid_cap, hipStream_t stream) {
-    const int variant = int(bpc >> 16);  // probe selector rides in the high bits of bpc
-    bpc &= 0xFFFFu;
-    const uint64_t chunks = len / bpc;
-    const uint64_t lanes = variant == 2 ? chunks * 8 : variant == 3 ? chunks * 4 : chunks;
-    const uint64_t need = (lanes + kBlockThreads - 1) / kBlockThreads;
-    const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
-#define LR(B, V) hipLaunchKernelGGL((lane_read_kernel<B, V>), dim3(grid), dim3(kBlockThreads), 0, stream, d, chunks, sink)
-#define LRV(B)                          \
-    switch (variant) {                  \
-    case 0: LR(B, 0); break;            \
-    case 1: LR(B, 1); break;            \
-    case 2: LR(B, 2); break;            \
-    case 3: LR(B, 3); break;            \
-    default: LR(B, 4); break;           \
-    }
-    switch (bpc) {
-    case 512: LRV(512); break;
-    case 2048: LRV(2048); break;
-    case 4096: LRV(4096); break;
-    default: return hipErrorInvalidValue;
-    }
-#undef LRV
-#undef LR
-    return hipGetLastError();
 }
 
 }  // namespace hdfs3crc

@@ -17,6 +17,21 @@ namespace hdfs3crc {
 // Sets the thread-local message returned by hdfs3_crc_last_error(); returns `code`.
 int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// Makes `dev` the calling thread's current device for the guard's lifetime (hipMalloc,
+// hipHostMalloc and event creation act on the current device).
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 // Staging segment of the host-buffer API: 16 MiB of payload per H2D transfer.
 constexpr size_t kSegmentBytes = 16u << 20;
 

@@ -63,20 +63,12 @@ int hip_fail(hipError_t e, const char *what) {
 
 namespace {
 
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
-        else prev = -1;
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
-
 int check_args(hdfs3_crc_ctx *ctx, uint32_t bpc) {
     if (!ctx) return fail(-EINVAL, "null hdfs3_crc_ctx");
-    if (bpc == 0 || (bpc & 3u)) return fail(-EINVAL, "bytes per checksum %u must be a positive multiple of 4", bpc);
+    // any bytesPerChecksum > 0, as RemoteBlockReader::checkResponse accepts from a datanode
+    // (RemoteBlockReader.cpp:150-156): sizes the whole-round kernels do not take (not 512..4096
+    // or unaligned buffers) run on the byte-granular chunk-per-lane kernel
+    if (bpc == 0) return fail(-EINVAL, "bytes per checksum must be positive");
     return 0;
 }
 
@@ -783,7 +775,9 @@ int hdfs3_memset_dev(hdfs3_crc_ctx *ctx, void *d_dst, int value, size_t bytes) {
 
 }  // extern "C"
 
-// ---- measurement hooks (not part of hdfs3_crc.h; used by bench.py only) -------
+// ---- measurement hooks: libhdfs3_crc_lab.so only (HDFS3_LAB=1; bench.py's read ceiling,
+// tools/, the A/B tests). Not part of hdfs3_crc.h and not exported by libhdfs3_crc.so. ----
+#if HDFS3_LAB
 extern "C" {
 
 // Coalesced read-only stream over [d, d+len): the achievable HBM read ceiling.
@@ -818,3 +812,4 @@ void hdfs3x_set_variant(int v) { set_variant(v); }
 void hdfs3x_set_trace(void *d_trace) { set_trace(static_cast<uint64_t *>(d_trace)); }
 
 }  // extern "C"
+#endif  // HDFS3_LAB

@@ -55,12 +55,16 @@ class DeviceBuffer:
 class CrcContext:
     """One hdfs3_crc_ctx: like one Checksum instance per reader/writer in the reference."""
 
-    def __init__(self, device: int = 0):
-        self._lib = _native.lib()
+    def __init__(self, device: int = 0, lib=None):
+        """lib: the product library (default) or _native.lab() for the A/B tools."""
+        self._lib = lib if lib is not None else _native.lib()
         p = c_void_p()
-        check("hdfs3_crc_ctx_create", self._lib.hdfs3_crc_ctx_create(device, byref(p)))
+        self._check("hdfs3_crc_ctx_create", self._lib.hdfs3_crc_ctx_create(device, byref(p)))
         self.ctx = p.value
         self.device = device
+
+    def _check(self, fn: str, rc: int) -> int:
+        return check(fn, rc, self._lib)
 
     def close(self) -> None:
         if self.ctx:
@@ -85,18 +89,18 @@ class CrcContext:
         return int(self._lib.hdfs3_crc_ctx_kernel_launches(self.ctx))
 
     def set_stream(self, hip_stream: int | None) -> None:
-        check("hdfs3_crc_ctx_set_stream", self._lib.hdfs3_crc_ctx_set_stream(self.ctx, hip_stream))
+        self._check("hdfs3_crc_ctx_set_stream", self._lib.hdfs3_crc_ctx_set_stream(self.ctx, hip_stream))
 
     def set_checksum_type(self, ctype: int) -> None:
         """2 = CHECKSUM_CRC32C (default), 1 = CHECKSUM_CRC32 (zlib polynomial)."""
-        check("hdfs3_crc_ctx_set_checksum_type", self._lib.hdfs3_crc_ctx_set_checksum_type(self.ctx, ctype))
+        self._check("hdfs3_crc_ctx_set_checksum_type", self._lib.hdfs3_crc_ctx_set_checksum_type(self.ctx, ctype))
 
     @property
     def checksum_type(self) -> int:
         return int(self._lib.hdfs3_crc_ctx_get_checksum_type(self.ctx))
 
     def synchronize(self) -> None:
-        check("hdfs3_crc_ctx_synchronize", self._lib.hdfs3_crc_ctx_synchronize(self.ctx))
+        self._check("hdfs3_crc_ctx_synchronize", self._lib.hdfs3_crc_ctx_synchronize(self.ctx))
 
     def upload(self, host: np.ndarray, dev: DeviceBuffer | int | None = None, offset: int = 0):
         """Copy host bytes to a DeviceBuffer (bounds-checked) or a raw device address."""
@@ -108,25 +112,25 @@ class CrcContext:
             base = dev.ptr
         else:
             base = int(dev)
-        check("hdfs3_memcpy_h2d", self._lib.hdfs3_memcpy_h2d(self.ctx, base + offset, _ptr(host), host.nbytes))
+        self._check("hdfs3_memcpy_h2d", self._lib.hdfs3_memcpy_h2d(self.ctx, base + offset, _ptr(host), host.nbytes))
         return dev
 
     def download(self, dev: DeviceBuffer | int, nbytes: int, offset: int = 0) -> np.ndarray:
         out = np.empty(nbytes, dtype=np.uint8)
         base = dev.ptr if isinstance(dev, DeviceBuffer) else int(dev)
-        check("hdfs3_memcpy_d2h", self._lib.hdfs3_memcpy_d2h(self.ctx, _ptr(out), base + offset, nbytes))
+        self._check("hdfs3_memcpy_d2h", self._lib.hdfs3_memcpy_d2h(self.ctx, _ptr(out), base + offset, nbytes))
         return out
 
     def memset(self, dev: DeviceBuffer | int, value: int, nbytes: int, offset: int = 0) -> None:
         base = dev.ptr if isinstance(dev, DeviceBuffer) else int(dev)
-        check("hdfs3_memset_dev", self._lib.hdfs3_memset_dev(self.ctx, base + offset, value, nbytes))
+        self._check("hdfs3_memset_dev", self._lib.hdfs3_memset_dev(self.ctx, base + offset, value, nbytes))
 
     # -- host-buffer API ----------------------------------------------------------
     def compute(self, data: np.ndarray, bpc: int) -> np.ndarray:
         data = np.ascontiguousarray(data, dtype=np.uint8)
         n = (data.nbytes + bpc - 1) // bpc
         out = np.zeros(4 * n, dtype=np.uint8)
-        check("hdfs3_crc32c_compute",
+        self._check("hdfs3_crc32c_compute",
               self._lib.hdfs3_crc32c_compute(self.ctx, _ptr(data), data.nbytes, bpc, _ptr(out)))
         return out
 
@@ -134,19 +138,19 @@ class CrcContext:
         data = np.ascontiguousarray(data, dtype=np.uint8)
         crc_be = np.ascontiguousarray(crc_be, dtype=np.uint8)
         bad = c_int64(-2)
-        check("hdfs3_crc32c_verify",
+        self._check("hdfs3_crc32c_verify",
               self._lib.hdfs3_crc32c_verify(self.ctx, _ptr(data), data.nbytes, bpc, _ptr(crc_be),
                                             int(check_short_tail), byref(bad)))
         return bad.value
 
     # -- device-resident API --------------------------------------------------------
     def compute_dev(self, d_data: int, nbytes: int, bpc: int, d_out: int) -> None:
-        check("hdfs3_crc32c_compute_dev",
+        self._check("hdfs3_crc32c_compute_dev",
               self._lib.hdfs3_crc32c_compute_dev(self.ctx, d_data, nbytes, bpc, d_out))
 
     def verify_dev(self, d_data: int, nbytes: int, bpc: int, d_crc: int, check_short_tail: bool = False) -> int:
         bad = c_int64(-2)
-        check("hdfs3_crc32c_verify_dev",
+        self._check("hdfs3_crc32c_verify_dev",
               self._lib.hdfs3_crc32c_verify_dev(self.ctx, d_data, nbytes, bpc, d_crc,
                                                 int(check_short_tail), byref(bad)))
         return bad.value
@@ -157,11 +161,11 @@ class CrcContext:
         caller's guarantee: the previous op on the stream is a verify and this one's inputs
         were ready before it)."""
         if overlap_previous:
-            check("hdfs3_crc32c_verify_dev_async_ex",
+            self._check("hdfs3_crc32c_verify_dev_async_ex",
                   self._lib.hdfs3_crc32c_verify_dev_async_ex(self.ctx, d_data, nbytes, bpc, d_crc,
                                                              int(check_short_tail), d_result, 1))
             return
-        check("hdfs3_crc32c_verify_dev_async",
+        self._check("hdfs3_crc32c_verify_dev_async",
               self._lib.hdfs3_crc32c_verify_dev_async(self.ctx, d_data, nbytes, bpc, d_crc,
                                                       int(check_short_tail), d_result))
 
@@ -179,18 +183,18 @@ class CrcContext:
     def verify_blocks_dev(self, blocks, bpc: int, check_short_tail: bool = False):
         """blocks = [(d_data, d_crc, len)] -> first bad (block, chunk) or (-1, -1)."""
         bb, bc = c_int64(-2), c_int64(-2)
-        check("hdfs3_crc32c_verify_blocks_dev",
+        self._check("hdfs3_crc32c_verify_blocks_dev",
               self._lib.hdfs3_crc32c_verify_blocks_dev(self.ctx, self._blocks(blocks), len(blocks), bpc,
                                                        int(check_short_tail), byref(bb), byref(bc)))
         return bb.value, bc.value
 
     def verify_blocks_dev_async(self, blocks, bpc: int, d_result: int, check_short_tail: bool = False) -> None:
-        check("hdfs3_crc32c_verify_blocks_dev_async",
+        self._check("hdfs3_crc32c_verify_blocks_dev_async",
               self._lib.hdfs3_crc32c_verify_blocks_dev_async(self.ctx, self._blocks(blocks), len(blocks), bpc,
                                                              int(check_short_tail), d_result))
 
     def compute_blocks_dev(self, blocks, bpc: int) -> None:
-        check("hdfs3_crc32c_compute_blocks_dev",
+        self._check("hdfs3_crc32c_compute_blocks_dev",
               self._lib.hdfs3_crc32c_compute_blocks_dev(self.ctx, self._blocks(blocks), len(blocks), bpc))
 
     # -- block checksum (OP_BLOCK_CHECKSUM's "MD5 of CRC32") ----------------------------
@@ -198,7 +202,7 @@ class CrcContext:
         """MD5 of the block's BE CRC words (GPU CRCs, host MD5) and crcPerBlock."""
         out = np.zeros(16, dtype=np.uint8)
         n = ctypes.c_uint64(0)
-        check("hdfs3_block_checksum_dev",
+        self._check("hdfs3_block_checksum_dev",
               self._lib.hdfs3_block_checksum_dev(self.ctx, d_data, nbytes, bpc, _ptr(out), byref(n)))
         return out.tobytes(), n.value
 
@@ -214,7 +218,7 @@ class CrcContext:
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         d = self._descs(pk)
         bp, bc = c_int64(-2), c_int64(-2)
-        check("hdfs3_crc32c_verify_packets",
+        self._check("hdfs3_crc32c_verify_packets",
               self._lib.hdfs3_crc32c_verify_packets(self.ctx, _ptr(arena), arena.nbytes, d, len(pk), bpc,
                                                     int(check_short_tail), byref(bp), byref(bc)))
         return bp.value, bc.value
@@ -222,14 +226,14 @@ class CrcContext:
     def verify_packets_dev(self, d_arena: int, arena_len: int, pk, bpc: int, check_short_tail: bool = False):
         d = self._descs(pk)
         bp, bc = c_int64(-2), c_int64(-2)
-        check("hdfs3_crc32c_verify_packets_dev",
+        self._check("hdfs3_crc32c_verify_packets_dev",
               self._lib.hdfs3_crc32c_verify_packets_dev(self.ctx, d_arena, arena_len, d, len(pk), bpc,
                                                         int(check_short_tail), byref(bp), byref(bc)))
         return bp.value, bc.value
 
     def compute_packets_dev(self, d_arena: int, arena_len: int, pk, bpc: int) -> None:
         d = self._descs(pk)
-        check("hdfs3_crc32c_compute_packets_dev",
+        self._check("hdfs3_crc32c_compute_packets_dev",
               self._lib.hdfs3_crc32c_compute_packets_dev(self.ctx, d_arena, arena_len, d, len(pk), bpc))
 
 
@@ -495,9 +499,12 @@ class LocalBlockReader:
     its .meta file with GPU verification of every chunk."""
 
     def __init__(self, data_path: str, meta_path: str, *, num_bytes: int = 0, offset: int = 0, device: int = 0,
-                 verify: bool = True, buffer_size: int = 1 << 20, window_buffers: int = 4):
+                 verify: bool = True, buffer_size: int = 1 << 20, window_buffers: int = 4,
+                 crc32_as_zlib: bool = False):
+        """crc32_as_zlib: HDFS3_LOCAL_CRC32_AS_ZLIB (verify CHECKSUM_CRC32 meta with the zlib
+        polynomial; the default is the reference's CRC32C)."""
         self._lib = _native.lib()
-        opts = _native.LocalOpts(device, int(verify), buffer_size, window_buffers)
+        opts = _native.LocalOpts(device, int(verify), buffer_size, window_buffers, 1 if crc32_as_zlib else 0)
         p = c_void_p()
         check("hdfs3_local_reader_open",
               self._lib.hdfs3_local_reader_open(str(data_path).encode(), str(meta_path).encode(), num_bytes, offset,

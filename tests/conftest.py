@@ -25,3 +25,18 @@ def gpu_ctx():
     ctx = CrcContext(0)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture(scope="session")
+def lab_ctx():
+    """A context of the measurement library (libhdfs3_crc_lab.so): the same production
+    kernels plus the A/B variant knob (hdfs3x_set_variant). Variant tests run here, so the
+    product library never carries the knob."""
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import CrcContext, device_count
+
+    if device_count() < 1:
+        pytest.fail("no GPU visible for a -m gpu test")
+    ctx = CrcContext(0, lib=_native.lab())
+    yield ctx
+    ctx.close()

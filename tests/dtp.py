@@ -139,10 +139,11 @@ class Conn:
         self.s.close()
 
 
-def serve_once(script):
+def serve_once(script, received=None):
     """Test helper: a one-connection fake datanode on 127.0.0.1. After reading the client's
     OP_READ_BLOCK request it sends the bytes `script(request_fields)` returns, then keeps
-    the socket open until the client goes away. Returns (port, thread)."""
+    the socket open until the client goes away, appending whatever the client sends after
+    the request (its ClientReadStatusProto) to the list `received`. Returns (port, thread)."""
     import threading
 
     srv = socket.socket()
@@ -169,8 +170,12 @@ def serve_once(script):
                 body += c.recv(n - len(body))
             c.sendall(script(parse(body)))
             try:
-                while c.recv(65536):
-                    pass
+                while True:
+                    got = c.recv(65536)
+                    if not got:
+                        break
+                    if received is not None:
+                        received.append(got)
             except OSError:
                 pass
         finally:

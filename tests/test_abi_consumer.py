@@ -49,3 +49,41 @@ def test_cpp_client_consumer_round_trip_on_gpu():
     r = subprocess.run([CLIENT_BIN], capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "client_consumer ok" in r.stdout
+
+
+HDFS_BIN = os.path.join(REPO, "tests", "native", "hdfs_consumer")
+
+
+def _hdfs_consumer(*args, timeout=110):
+    if not os.path.exists(HDFS_BIN):
+        pytest.fail("tests/native/hdfs_consumer not built (run `make`)")
+    r = subprocess.run([HDFS_BIN, *args], capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert line, r.stdout
+    import json
+    return json.loads(line[-1])
+
+
+@pytest.mark.gpu
+def test_c_consumer_on_hdfs_h_surface():
+    """tests/native/hdfs_consumer.c, plain C against include/hdfs3_hdfs.h (the reference's
+    hdfs.h prototypes): hdfsOpenFile/hdfsWrite/hdfsFlush/hdfsSync/hdfsCloseFile with 1 KiB
+    packets (GPU words checked against the oracle), then hdfsRead (20 KiB + 1 reads,
+    CheckBuffer), hdfsPread across a block boundary, hdfsSeek/hdfsTell/hdfsAvailable, one
+    failover off a corrupt replica, EIO when only the corrupt replica is left, and the errno
+    of each misuse (ENOTSUP, ENOENT, EINVAL, EOVERFLOW)."""
+    j = _hdfs_consumer()
+    assert j["hdfs_consumer"] == "ok" and j["blocks"] == 4 and j["bytes"] == 3 * (1 << 20) + 234
+
+
+@pytest.mark.gpu
+def test_config5_1gib_file_through_hdfsRead():
+    """BASELINE.json configs[4] at its stated size: a 1 GiB file of 8 x 128 MiB blocks written
+    through hdfsWrite (64 KiB packets, every packet's words checked against the oracle), served
+    over loopback TCP by two replicas (block 1 of the first corrupt), read back through
+    hdfsRead in 4 MiB calls: every byte CheckBuffer'd, one failover, then EIO from the corrupt
+    replica alone. Prints the end-to-end rates."""
+    j = _hdfs_consumer("128", "8", timeout=115)
+    assert j["hdfs_consumer"] == "ok" and j["blocks"] == 8 and j["bytes"] == 1 << 30
+    print(j)

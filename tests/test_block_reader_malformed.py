@@ -27,11 +27,11 @@ GOOD = pkt(DATA.tobytes(), CRC, 0, 0)
 TRAILER = packet_header(4, 4096, 1, True, 0)
 
 
-def attempt(script, start=0, length=4096):
+def attempt(script, start=0, length=4096, received=None):
     from libhdfs3_amd.engine import BlockReader
     from libhdfs3_amd._native import Hdfs3CrcError
 
-    port, t = serve_once(script)
+    port, t = serve_once(script, received)
     try:
         with BlockReader("127.0.0.1", port, 1, start, length, timeout_ms=3000) as r:
             out = r.read_all(length)
@@ -81,3 +81,40 @@ def test_corrupt_crc_is_checksum_exception():
     bad[5] ^= 1  # chunk 1
     out, err = attempt(lambda req: block_op_response() + pkt(DATA.tobytes(), bytes(bad), 0, 0) + TRAILER)
     assert err is not None and "ChecksumException" in str(err)
+
+
+def test_status_only_after_the_empty_trailer():
+    """sendStatus runs only when readTrailingEmptyPacket sees {lastPacketInBlock, dataLen 0}
+    (RemoteBlockReader.cpp:274-286): CHECKSUM_OK (status 6) after a proper trailer; nothing
+    when the datanode keeps streaming a data packet after the range."""
+    got = []
+    out, err = attempt(lambda req: block_op_response() + GOOD + TRAILER, received=got)
+    assert err is None and out.tobytes() == DATA.tobytes()
+    msg = b"".join(got)
+    assert msg == varint(2) + bytes([0x08, 6]), msg  # ClientReadStatusProto{status: CHECKSUM_OK}
+    got = []
+    more = pkt(DATA.tobytes(), CRC, 4096, 1)  # a data packet where the trailer belongs
+    out, err = attempt(lambda req: block_op_response() + GOOD + more, received=got)
+    assert err is None and out.tobytes() == DATA.tobytes()
+    assert b"".join(got) == b""
+
+
+@pytest.mark.parametrize("bpc", [1, 3, 513, 517])
+def test_any_positive_chunk_size(bpc):
+    """RemoteBlockReader accepts any bytesPerChecksum > 0 from the datanode (:150-156); the
+    remote rule still ignores a short-tail mismatch (:319)."""
+    n = 4096
+    crc = oracle_compute(DATA[:n], bpc).tobytes()
+    script = lambda req: block_op_response(bpc=bpc) + pkt(DATA.tobytes(), crc, 0, 0) + TRAILER
+    out, err = attempt(script)
+    assert err is None and out.tobytes() == DATA.tobytes(), err
+    bad = bytearray(crc)
+    k = 1000 // bpc if bpc > 4 else 7
+    bad[4 * k] ^= 1
+    out, err = attempt(lambda req: block_op_response(bpc=bpc) + pkt(DATA.tobytes(), bytes(bad), 0, 0) + TRAILER)
+    assert err is not None and "ChecksumException" in str(err)
+    if n % bpc:  # a bad word on the short tail chunk is ignored remotely
+        tail = bytearray(crc)
+        tail[-1] ^= 1
+        out, err = attempt(lambda req: block_op_response(bpc=bpc) + pkt(DATA.tobytes(), bytes(tail), 0, 0) + TRAILER)
+        assert err is None and out.tobytes() == DATA.tobytes()

@@ -64,12 +64,14 @@ def test_ragged_lengths_host_and_device(ctx32, bpc):
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 14, 26, 27, 36, 40])
 @pytest.mark.parametrize("bpc", [512, 4096])
-def test_every_kernel_variant_crc32(ctx32, variant, bpc):
+def test_every_kernel_variant_crc32(lab_ctx, variant, bpc):
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import DeviceBuffer
 
-    lib = _native.lib()
+    lib = _native.lab()
+    ctx32 = lab_ctx
     try:
+        ctx32.set_checksum_type(1)
         lib.hdfs3x_set_variant(variant)
         for n in (4096 * 37, 4096 * 300 + bpc * 2 + 77):
             data = splitmix_bytes(n, variant * 7 + bpc + n)
@@ -86,6 +88,7 @@ def test_every_kernel_variant_crc32(ctx32, variant, bpc):
                 ctx32.upload(data[pos:pos + 1], d, offset=pos)
     finally:
         lib.hdfs3x_set_variant(0)
+        ctx32.set_checksum_type(2)
 
 
 def test_packets_api_crc32(ctx32):

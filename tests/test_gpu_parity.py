@@ -78,7 +78,9 @@ def test_packet_fixture_verify_semantics(gpu_ctx):
     assert gpu_ctx.verify(pkt[:n], 512, corrupt, True) == v["tail_corrupt_local"]
 
 
-@pytest.mark.parametrize("bpc", [4, 12, 64, 500, 512, 516, 1024, 2048, 4096, 65536])
+# bpc 1, 3, 513, 517: readers accept any bytesPerChecksum > 0 (RemoteBlockReader.cpp:150-156,
+# LocalBlockReader.cpp:110-115); the byte-granular kernel verifies them
+@pytest.mark.parametrize("bpc", [1, 3, 4, 12, 64, 500, 512, 513, 516, 517, 1024, 2048, 4096, 65536])
 def test_ragged_lengths_vs_oracle(gpu_ctx, bpc):
     rng = np.random.default_rng(bpc)
     for n in [0, 1, 3, bpc - 1, bpc, bpc + 1, 3 * bpc + 7] + [int(x) for x in rng.integers(0, 300_000, 6)]:
@@ -104,7 +106,7 @@ def test_unaligned_device_pointers(gpu_ctx, offset):
     data = splitmix_bytes(513 * 97 + 5, offset)
     d = DeviceBuffer(data.nbytes + 64)
     gpu_ctx.upload(data, d, offset=offset)
-    for bpc in (512, 2048, 516):
+    for bpc in (512, 2048, 516, 517, 3):
         want = oracle_compute(data, bpc)
         dc = DeviceBuffer(want.nbytes + 8)
         gpu_ctx.compute_dev(d.ptr + offset, data.nbytes, bpc, dc.ptr + 1)  # unaligned CRC array too
@@ -129,7 +131,7 @@ def _wire_arena(n_pkts, bpc, rng, short_last=True):
     return np.concatenate(parts), descs
 
 
-@pytest.mark.parametrize("bpc", [512, 4096])
+@pytest.mark.parametrize("bpc", [3, 512, 513, 4096])
 def test_packets_api(gpu_ctx, bpc):
     from libhdfs3_amd.engine import DeviceBuffer
 
@@ -140,7 +142,7 @@ def test_packets_api(gpu_ctx, bpc):
     d_off, _, _ = pk[5]
     bad[d_off + 3 * bpc + 11] ^= 1
     bad[pk[9][0] + 2] ^= 1
-    assert gpu_ctx.verify_packets(bad, pk, bpc) == (5, 3)
+    assert gpu_ctx.verify_packets(bad, pk, bpc) == (5, (3 * bpc + 11) // bpc)
     # corrupt the short tail chunk's CRC of the last packet: remote ignores, local flags
     last = len(pk) - 1
     data_off, crc_off, data_len = pk[last]
@@ -241,29 +243,29 @@ def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
 # or trace and give wrong results on purpose)
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 14, 16, 18, 20, 26, 27, 28, 30, 31, 32, 33, 36, 40, 42, 43, 44, 46, 47, 48])
 @pytest.mark.parametrize("bpc", [512, 1024, 2048, 4096, 8192])
-def test_every_kernel_variant_matches_oracle(gpu_ctx, variant, bpc):
+def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
     """All kernel designs kept for A/B (hdfs3x_set_variant) are parity-checked too:
     whole rounds, the slow region (len not a multiple of the 4 KiB round) and the tail."""
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import DeviceBuffer
 
-    lib = _native.lib()
+    lib = _native.lab()
     try:
         lib.hdfs3x_set_variant(variant)
         for n in (4096 * 37, 4096 * 64 * 17 + 3 * bpc, 4096 * 300 + bpc * 2 + 77, bpc * 65 + 5):
             data = splitmix_bytes(n, variant * 1000 + bpc + n)
             want = oracle_compute(data, bpc)
-            d = gpu_ctx.upload(data)
+            d = lab_ctx.upload(data)
             dc = DeviceBuffer(want.nbytes)
-            gpu_ctx.compute_dev(d.ptr, n, bpc, dc.ptr)
-            assert np.array_equal(gpu_ctx.download(dc, want.nbytes), want), (variant, bpc, n)
-            assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, True) == -1
+            lab_ctx.compute_dev(d.ptr, n, bpc, dc.ptr)
+            assert np.array_equal(lab_ctx.download(dc, want.nbytes), want), (variant, bpc, n)
+            assert lab_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, True) == -1
             nc = (n + bpc - 1) // bpc
             for k in (0, nc // 2, nc - 2):
                 pos = k * bpc + 1
-                gpu_ctx.upload(np.array([data[pos] ^ 4], np.uint8), d, offset=pos)
-                assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, False) == k, (variant, bpc, n, k)
-                gpu_ctx.upload(data[pos:pos + 1], d, offset=pos)
+                lab_ctx.upload(np.array([data[pos] ^ 4], np.uint8), d, offset=pos)
+                assert lab_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, False) == k, (variant, bpc, n, k)
+                lab_ctx.upload(data[pos:pos + 1], d, offset=pos)
     finally:
         lib.hdfs3x_set_variant(0)
 

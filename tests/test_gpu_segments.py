@@ -99,10 +99,10 @@ def test_many_small_blocks_binary_search(gpu_ctx):
 
 
 @pytest.mark.parametrize("bpc", [512, 4096])
-def test_packet_fast_path_agrees_with_packet_kernel(gpu_ctx, bpc):
+def test_packet_fast_path_agrees_with_packet_kernel(lab_ctx, bpc):
     from libhdfs3_amd import _native
 
-    lib = _native.lib()
+    lib = _native.lab()
     rng = np.random.default_rng(bpc)
     pk, parts, off = [], [], 0
     lens = [65536] * 40 + [65536 - 100, 777, 4096, 20000, 65536]
@@ -114,22 +114,22 @@ def test_packet_fast_path_agrees_with_packet_kernel(gpu_ctx, bpc):
         pk.append((off + pad + crc.nbytes, off + pad, n))
         off += pad + crc.nbytes + n
     arena = np.concatenate(parts)
-    d = gpu_ctx.upload(arena)
+    d = lab_ctx.upload(arena)
     try:
         for v in (0, 17):
             lib.hdfs3x_set_variant(v)
-            assert gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc) == (-1, -1)
+            assert lab_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc) == (-1, -1)
         for trial in range(4):
             bad = arena.copy()
             p = int(rng.integers(0, len(pk)))
             q = int(rng.integers(0, pk[p][2]))
             bad[pk[p][0] + q] ^= 0x80
-            gpu_ctx.upload(bad, d)
+            lab_ctx.upload(bad, d)
             got = []
             for v in (0, 17):
                 lib.hdfs3x_set_variant(v)
-                got.append((gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc),
-                            gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True)))
+                got.append((lab_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc),
+                            lab_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True)))
             assert got[0] == got[1], (p, q, got)
             chunk = q // bpc
             short = pk[p][2] % bpc and chunk == pk[p][2] // bpc
@@ -140,34 +140,34 @@ def test_packet_fast_path_agrees_with_packet_kernel(gpu_ctx, bpc):
         blank = arena.copy()
         for data_off, crc_off, n in pk:
             blank[crc_off:crc_off + 4 * ((n + bpc - 1) // bpc)] = 0
-        gpu_ctx.upload(blank, d)
-        gpu_ctx.compute_packets_dev(d.ptr, arena.nbytes, pk, bpc)
-        assert np.array_equal(gpu_ctx.download(d, arena.nbytes), arena)
+        lab_ctx.upload(blank, d)
+        lab_ctx.compute_packets_dev(d.ptr, arena.nbytes, pk, bpc)
+        assert np.array_equal(lab_ctx.download(d, arena.nbytes), arena)
     finally:
         lib.hdfs3x_set_variant(0)
 
 
 @pytest.mark.parametrize("bpc", [512, 2048, 4096])
 @pytest.mark.parametrize("variant", [0, 49])
-def test_single_segment_batch(gpu_ctx, bpc, variant):
+def test_single_segment_batch(lab_ctx, bpc, variant):
     """One block through the batch API (segmented kernel with one segment); variant 49 fixes
     the segment view at kernel start (A/B, tools/seg_ab.py). Words and first bad chunk."""
     from libhdfs3_amd import _native
 
-    lib = _native.lib()
+    lib = _native.lab()
     n = 4096 * 1000 + 3 * bpc + 77
     try:
         lib.hdfs3x_set_variant(variant)
-        blocks, keep, datas = make_blocks(gpu_ctx, [n], bpc, 4900 + bpc)
-        gpu_ctx.compute_blocks_dev(blocks, bpc)
+        blocks, keep, datas = make_blocks(lab_ctx, [n], bpc, 4900 + bpc)
+        lab_ctx.compute_blocks_dev(blocks, bpc)
         d, c, _ = blocks[0]
         want = oracle_compute(datas[0], bpc)
-        assert np.array_equal(gpu_ctx.download(c, want.nbytes), want)
-        assert gpu_ctx.verify_blocks_dev(blocks, bpc, True) == (-1, -1)
+        assert np.array_equal(lab_ctx.download(c, want.nbytes), want)
+        assert lab_ctx.verify_blocks_dev(blocks, bpc, True) == (-1, -1)
         k = (n // bpc) // 2
         pos = k * bpc + 5
-        gpu_ctx.upload(np.array([datas[0][pos] ^ 8], np.uint8), keep[0], offset=pos)
-        assert gpu_ctx.verify_blocks_dev(blocks, bpc, False) == (0, k)
+        lab_ctx.upload(np.array([datas[0][pos] ^ 8], np.uint8), keep[0], offset=pos)
+        assert lab_ctx.verify_blocks_dev(blocks, bpc, False) == (0, k)
     finally:
         lib.hdfs3x_set_variant(0)
 
@@ -175,13 +175,13 @@ def test_single_segment_batch(gpu_ctx, bpc, variant):
 @pytest.mark.gpu
 @pytest.mark.parametrize("bpc", [512, 4096])
 @pytest.mark.parametrize("last_len", [65536, 65536 - 300, 100])
-def test_constant_pitch_packets_without_descriptors(gpu_ctx, bpc, last_len):
+def test_constant_pitch_packets_without_descriptors(lab_ctx, bpc, last_len):
     """Packets at one pitch in one arena (the reader's and writer's layout) go to the
     segmented kernel with no descriptor array (SegLaunch::stride). Same keys and words as
     with descriptors (A/B variant 52) and as the packet kernel (variant 17)."""
     from libhdfs3_amd import _native
 
-    lib = _native.lib()
+    lib = _native.lab()
     rng = np.random.default_rng(bpc + last_len)
     n, plen = 40, 65536
     crc_bytes = 4 * (plen // bpc)
@@ -198,29 +198,29 @@ def test_constant_pitch_packets_without_descriptors(gpu_ctx, bpc, last_len):
         arena[crc_off:crc_off + crc.nbytes] = crc
         arena[data_off:data_off + dl] = data
         pk.append((data_off, crc_off, dl))
-    d = gpu_ctx.upload(arena)
+    d = lab_ctx.upload(arena)
     try:
         for v in (0, 52, 17):
             lib.hdfs3x_set_variant(v)
-            assert gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True) == (-1, -1), v
+            assert lab_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True) == (-1, -1), v
         for _ in range(3):
             p = int(rng.integers(0, n))
             q = int(rng.integers(0, pk[p][2]))
             bad = arena.copy()
             bad[pk[p][0] + q] ^= 0x20
-            gpu_ctx.upload(bad, d)
+            lab_ctx.upload(bad, d)
             got = set()
             for v in (0, 52, 17):
                 lib.hdfs3x_set_variant(v)
-                got.add(gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True))
+                got.add(lab_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True))
             assert got == {(p, q // bpc)}, (p, q, got)
         blank = arena.copy()
         for data_off, crc_off, dl in pk:
             blank[crc_off:data_off] = 0
         for v in (0, 52):
             lib.hdfs3x_set_variant(v)
-            gpu_ctx.upload(blank, d)
-            gpu_ctx.compute_packets_dev(d.ptr, arena.nbytes, pk, bpc)
-            assert np.array_equal(gpu_ctx.download(d, arena.nbytes), arena), v
+            lab_ctx.upload(blank, d)
+            lab_ctx.compute_packets_dev(d.ptr, arena.nbytes, pk, bpc)
+            assert np.array_equal(lab_ctx.download(d, arena.nbytes), arena), v
     finally:
         lib.hdfs3x_set_variant(0)

@@ -346,3 +346,42 @@ def test_reference_read_many_files_same_time():
     finally:
         for node, _ in nodes:
             node.stop()
+
+
+def test_config5_1gib_file_at_size():
+    """BASELINE.json configs[4]: hdfs3_input_read of a 1 GiB file (8 x 128 MiB blocks, 64 KiB
+    packets) from loopback datanodes. Stored words come from the oracle; the bytes read must
+    equal the source; with a corrupted replica listed first for block 5 the stream fails over
+    exactly once and still returns every byte."""
+    from loopback import LoopbackDatanode
+
+    nblk, bs = 8, 128 << 20
+    good, bad = LoopbackDatanode(), LoopbackDatanode()
+    try:
+        datas = [splitmix_bytes(bs, 9000 + i) for i in range(nblk)]
+        crcs = [oracle_compute(d, BPC) for d in datas]
+        corrupt = datas[5].copy()
+        corrupt[77 * BPC + 3] ^= 0x10
+        for i in range(nblk):
+            good.add_block(900 + i, datas[i], crcs[i], BPC)
+            bad.add_block(900 + i, corrupt if i == 5 else datas[i], crcs[i], BPC)
+        blocks = [(900 + i, bs) for i in range(nblk)]
+        from libhdfs3_amd.engine import InputStream
+        replicas = [("127.0.0.1", bad.port), ("127.0.0.1", good.port)]
+        with InputStream([(bid, n, replicas) for bid, n in blocks]) as s:
+            out = np.empty(4 << 20, np.uint8)
+            pos = 0
+            for i in range(nblk):
+                off = 0
+                while off < bs:
+                    n = s.read_into(out, 0, min(out.nbytes, bs - off))
+                    assert n > 0
+                    assert np.array_equal(out[:n], datas[i][off:off + n]), (i, off)
+                    off += n
+                pos += bs
+            assert s.read_into(out) == 0 and s.tell() == nblk * bs == 1 << 30
+            st = s.stats()
+            assert st["failovers"] == 1 and st["readers_opened"] >= nblk + 1
+    finally:
+        good.stop()
+        bad.stop()

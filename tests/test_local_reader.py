@@ -115,18 +115,84 @@ def test_bad_version_is_an_error(tmp_path):
     assert ei.value.rc == -errno.EIO and "version" in str(ei.value)
 
 
-def test_crc32_meta_verified_with_its_own_polynomial(tmp_path):
-    """Divergence from the reference on purpose: LocalBlockReader.cpp:82-96 checks CRC32
-    meta with a CRC32C engine (so such blocks always fail there); here they verify."""
+def test_crc32_meta_is_verified_with_crc32c_like_the_reference(tmp_path):
+    """LocalBlockReader.cpp:85-98: CHECKSUM_CRC32 and CHECKSUM_CRC32C both select the CRC32C
+    engine. A block whose meta declares type 1 with zlib words therefore fails at its first
+    chunk (ChecksumException -> EIO, nothing delivered) exactly where the oracle's CRC32C
+    verify of those words fails; type-1 meta holding CRC32C words reads clean."""
+    from libhdfs3_amd._native import Hdfs3CrcError
+    from libhdfs3_amd.engine import LocalBlockReader
+    from util import oracle_compute_crc32, oracle_verify
+
+    data = splitmix_bytes(1_000_003, 13)
+    zwords = oracle_compute_crc32(data, 512)
+    assert oracle_verify(data, 512, zwords, True) == 0  # the reference's verdict: chunk 0
+    d, m = write_block(tmp_path, "blk_crc32", data, ctype=1, crc=zwords)
+    with LocalBlockReader(d, m, buffer_size=1 << 18) as r:
+        out = np.zeros(data.nbytes, np.uint8)
+        with pytest.raises(Hdfs3CrcError) as ei:
+            r.read_into(out)
+        assert ei.value.rc == -errno.EIO and "ChecksumException" in str(ei.value)
+        assert r.stats()["checksum_type"] == 1
+    d, m = write_block(tmp_path, "blk_crc32_c", data, ctype=1)  # CRC32C words, type byte 1
+    out, st = read(d, m)
+    assert np.array_equal(out, data) and st["checksum_type"] == 1
+
+
+def test_crc32_meta_zlib_opt_in(tmp_path):
+    """HDFS3_LOCAL_CRC32_AS_ZLIB (opt-in departure from the reference): type-1 meta verified
+    with the zlib polynomial it declares."""
     from libhdfs3_amd._native import Hdfs3CrcError
     from util import oracle_compute_crc32
 
     data = splitmix_bytes(1_000_003, 13)
     d, m = write_block(tmp_path, "blk_crc32", data, ctype=1, crc=oracle_compute_crc32(data, 512))
-    out, st = read(d, m)
+    out, st = read(d, m, crc32_as_zlib=True)
     assert np.array_equal(out, data) and st["checksum_type"] == 1
     bad = data.copy()
     bad[-1] ^= 1  # short tail: checked locally
     d, m = write_block(tmp_path, "blk_crc32_bad", bad, ctype=1, crc=oracle_compute_crc32(data, 512))
     with pytest.raises(Hdfs3CrcError):
-        read(d, m)
+        read(d, m, crc32_as_zlib=True)
+
+
+@pytest.mark.parametrize("bpc", [1, 3, 513, 517])
+def test_any_positive_bytes_per_checksum(tmp_path, bpc):
+    """The reference accepts any bytesPerChecksum > 0 from the meta header (:110-115): chunk
+    sizes that are not a multiple of 4 verify, and a flipped bit is caught at the chunk the
+    oracle names (the whole local buffer holding it withheld)."""
+    from libhdfs3_amd._native import Hdfs3CrcError
+    from libhdfs3_amd.engine import LocalBlockReader
+    from util import oracle_verify
+
+    n = 200_000 + bpc * 7 + 5
+    data = splitmix_bytes(n, 100 + bpc)
+    d, m = write_block(tmp_path, f"blk_{bpc}", data, bpc)
+    out, st = read(d, m, buffer_size=1 << 16)
+    assert np.array_equal(out, data) and st["bytes_per_checksum"] == bpc
+    out, _ = read(d, m, offset=12345)
+    assert np.array_equal(out, data[12345:])
+    crc = oracle_compute(data, bpc)
+    bad = data.copy()
+    where = 150_001
+    bad[where] ^= 4
+    k = oracle_verify(bad, bpc, crc, True)
+    assert k == where // bpc
+    d, m = write_block(tmp_path, f"blk_{bpc}_bad", bad, bpc, crc=crc)
+    buf = (65536 + bpc - 1) // bpc * bpc  # chunk-rounded local buffer (:112-116)
+    with LocalBlockReader(d, m, buffer_size=1 << 16) as r:
+        got = np.zeros(n, np.uint8)
+        pos = 0
+        with pytest.raises(Hdfs3CrcError):
+            while True:
+                pos += r.read_into(got, pos, 50_000)
+    assert pos == (k * bpc) // buf * buf and np.array_equal(got[:pos], data[:pos])
+
+
+def test_local_buffer_above_1gib_is_rejected(tmp_path):
+    from libhdfs3_amd._native import Hdfs3CrcError
+    data = splitmix_bytes(8192, 14)
+    d, m = write_block(tmp_path, "blk_big", data)
+    with pytest.raises(Hdfs3CrcError) as ei:
+        read(d, m, buffer_size=(1 << 30) + 1)
+    assert ei.value.rc == -errno.EINVAL

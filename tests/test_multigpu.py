@@ -1,62 +1,124 @@
-"""Multi-GPU path (config 4) on CPU: world_size-2 gloo ranks run bench.py's sharding and
-aggregation helpers. Each rank owns distinct blocks (no data-path collective); the
-only collectives are the timing barrier and the max-over-ranks reduction. The per-rank
-CRC work is done by the oracle here (no GPU in this container) purely to exercise the
-harness; the GPU numbers come from bench.py on the box."""
+"""Multi-GPU path (BASELINE.json configs[3]: independent blocks, one set per GPU, no
+collectives on the data path).
+
+* CPU (gloo): the real `bench.py --gpus 2` entry — it spawns its own two rank processes before
+  any GPU call, they rendezvous, each derives its own block set, and rank 0 reports both ranks
+  and the max-over-ranks time (`--plumbing-check`: the N-rank plumbing without GPU work).
+* GPU: the same entry doing the real work on the one-GPU box (both ranks on cuda:0, gloo for
+  the timing collectives), and the in-library sharding API hdfs3_multi_* (block b ->
+  devices[b % n], a context, stream and worker thread per device) checked against the oracle.
+"""
+import json
 import os
-import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
+
+from util import oracle_compute, splitmix_bytes
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _bench(*args, timeout=120):
+    env = dict(os.environ, HDFS3_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO, env=env,
+                         capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 only
+    return json.loads(lines[0])
 
 
-def _rank_main(rank, world, port, out):
-    import sys
-    import time
-
-    import torch
-    import torch.distributed as dist
-
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, repo)
-    sys.path.insert(0, os.path.join(repo, "tests"))
-    import bench
-    from util import oracle_compute, oracle_verify, splitmix_bytes
-
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    blocks, nbytes = 3, 1 << 20
-    data = [splitmix_bytes(nbytes, bench.rank_seed(rank) + b) for b in range(blocks)]
-    crcs = [oracle_compute(d, 512) for d in data]
-    dist.barrier()
-    t0 = time.perf_counter()
-    bad = [oracle_verify(d, 512, c, False) for d, c in zip(data, crcs)]
-    elapsed = time.perf_counter() - t0 + 0.01 * (rank + 1)  # make ranks differ
-    dist.barrier()
-    emax = bench.max_over_ranks(dist, elapsed, torch.device("cpu"))
-    rate = bench.aggregate_rate(nbytes * blocks, world, emax)
-    first = torch.tensor([int(data[0][:8].view(np.int64)[0])], dtype=torch.int64)
-    firsts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(firsts, first)
-    out[rank] = (elapsed, emax, rate, bad, [int(f.item()) for f in firsts])
-    dist.destroy_process_group()
+def test_bench_gpus_2_spawns_two_ranks_cpu():
+    j = _bench("--gpus", "2", "--plumbing-check")
+    assert j["n_gpus"] == 2 and j["requested_gpus"] == 2
+    ranks = j["per_rank"]
+    assert [r["rank"] for r in ranks] == [0, 1] and [r["local_rank"] for r in ranks] == [0, 1]
+    assert ranks[0]["seed"] != ranks[1]["seed"]            # distinct block sets
+    assert ranks[0]["pid"] != ranks[1]["pid"]              # two processes
+    assert j["elapsed_max"] == pytest.approx(max(r["elapsed"] for r in ranks))
 
 
-def test_two_rank_sharding_and_max_time():
-    world = 2
-    port = _free_port()
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_rank_main, args=(world, port, out), nprocs=world, join=True)
-    (e0, m0, r0, b0, f0), (e1, m1, r1, b1, f1) = out[0], out[1]
-    assert m0 == m1 == pytest.approx(max(e0, e1))          # max over ranks, agreed by all
-    assert r0 == pytest.approx(2 * 3 * (1 << 20) / m0 / 2**30)
-    assert b0 == b1 == [-1, -1, -1]                          # every shard verifies clean
-    assert f0 == f1 and f0[0] != f0[1]                       # ranks hold distinct blocks
+def test_bench_gpus_4_spawns_four_ranks_cpu():
+    j = _bench("--gpus", "4", "--plumbing-check")
+    assert j["n_gpus"] == 4 and len({r["seed"] for r in j["per_rank"]}) == 4
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_real_run_on_one_gpu():
+    """`--gpus 2` end to end on the box: two ranks (both on cuda:0 here, one per GPU on a
+    node), each verifying its own blocks; value = both ranks' bytes / the slower rank's time."""
+    j = _bench("--gpus", "2", "--steps", "20", "--warmup", "5", "--blocks", "2", "--block-mib", "16",
+               "--no-cpu-baseline", "--no-pmc", timeout=240)
+    assert j["n_gpus"] == 2 and len(j["per_rank"]) == 2
+    a, b = j["per_rank"]
+    assert a["seed"] != b["seed"] and a["value"] > 0 and b["value"] > 0
+    slowest = max(a["ms_per_step"], b["ms_per_step"])
+    assert j["ms_per_step"] == pytest.approx(slowest, rel=1e-3)
+    assert j["value"] == pytest.approx(2 * (16 << 20) / (slowest * 1e-3) / 2**30, rel=2e-3)
+
+
+def _multi(devices):
+    import ctypes
+    from libhdfs3_amd import _native
+    lib = _native.lib()
+    arr = (ctypes.c_int * len(devices))(*devices)
+    m = ctypes.c_void_p()
+    _native.check("hdfs3_multi_create", lib.hdfs3_multi_create(arr, len(devices), ctypes.byref(m)))
+    return lib, m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workers", [1, 2])
+def test_multi_device_api_matches_oracle(gpu_ctx, workers):
+    """hdfs3_crc32c_{compute,verify}_blocks_multi on the visible devices (device 0 listed
+    `workers` times on a one-GPU box: two workers, streams and threads) vs the oracle, ragged
+    blocks, one corrupted block per worker, and the host-memory form."""
+    import ctypes
+    from libhdfs3_amd import _native
+    from libhdfs3_amd._native import DevBlock
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    lib, m = _multi([0] * workers)
+    try:
+        assert lib.hdfs3_multi_device_count(m) == workers
+        sizes = [4 << 20, (1 << 20) + 777, 4096 * 33, 512 * 9 + 100, 3 << 20]
+        datas = [splitmix_bytes(n, 31 + i) for i, n in enumerate(sizes)]
+        wants = [oracle_compute(d, 512) for d in datas]
+        keep = []
+        arr = (DevBlock * len(sizes))()
+        for i, (d, w) in enumerate(zip(datas, wants)):
+            dd, dc = gpu_ctx.upload(d), DeviceBuffer(w.nbytes)
+            keep += [dd, dc]
+            arr[i] = DevBlock(dd.ptr, dc.ptr, d.nbytes)
+        _native.check("compute_multi", lib.hdfs3_crc32c_compute_blocks_multi(m, arr, len(sizes), 512))
+        for i, w in enumerate(wants):
+            assert np.array_equal(gpu_ctx.download(keep[2 * i + 1], w.nbytes), w), i
+        bad = (ctypes.c_int64 * len(sizes))()
+        _native.check("verify_multi", lib.hdfs3_crc32c_verify_blocks_multi(m, arr, len(sizes), 512, 1, bad))
+        assert list(bad) == [-1] * len(sizes)
+        flips = {0: 3, 1: 2047}  # block -> chunk
+        for b, k in flips.items():
+            pos = k * 512 + 5
+            gpu_ctx.upload(np.array([datas[b][pos] ^ 2], np.uint8), keep[2 * b], offset=pos)
+        _native.check("verify_multi", lib.hdfs3_crc32c_verify_blocks_multi(m, arr, len(sizes), 512, 1, bad))
+        assert list(bad) == [flips.get(i, -1) for i in range(len(sizes))]
+        # host-memory blocks, staged per device
+        harr = (DevBlock * len(sizes))()
+        for i, (d, w) in enumerate(zip(datas, wants)):
+            harr[i] = DevBlock(d.ctypes.data, w.ctypes.data, d.nbytes)
+        _native.check("verify_host_multi", lib.hdfs3_crc32c_verify_host_multi(m, harr, len(sizes), 512, 1, bad))
+        assert list(bad) == [-1] * len(sizes)
+        outs = [np.zeros_like(w) for w in wants]
+        for i, (d, o) in enumerate(zip(datas, outs)):
+            harr[i] = DevBlock(d.ctypes.data, o.ctypes.data, d.nbytes)
+        _native.check("compute_host_multi", lib.hdfs3_crc32c_compute_host_multi(m, harr, len(sizes), 512))
+        assert all(np.array_equal(o, w) for o, w in zip(outs, wants))
+        # a host pointer where device memory is required: -EINVAL, nothing launched
+        arr[2] = DevBlock(datas[2].ctypes.data, keep[5].ptr, datas[2].nbytes)
+        assert lib.hdfs3_crc32c_verify_blocks_multi(m, arr, len(sizes), 512, 1, bad) == -22
+    finally:
+        lib.hdfs3_multi_destroy(m)

@@ -35,10 +35,10 @@ def main():
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import CrcContext
 
-    lib = _native.lib()
+    lib = _native.lab()
     dev = torch.device("cuda", 0)
     nstreams = [int(x) for x in args.streams.split(",")]
-    ctxs = [CrcContext(0) for _ in range(max(nstreams))]
+    ctxs = [CrcContext(0, lib=_native.lab()) for _ in range(max(nstreams))]
     streams = [torch.cuda.Stream(device=dev) for _ in ctxs]
     for c, st in zip(ctxs, streams):
         c.set_stream(st.cuda_stream)

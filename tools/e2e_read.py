@@ -60,7 +60,7 @@ def diag(dn, blocks, out, data, args):
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import BlockReader
 
-    lib = _native.lib()
+    lib = _native.lab()
     for verify in (True, False, True, False):
         acc = np.zeros(5, np.uint64)
         t0 = time.perf_counter()
@@ -179,7 +179,7 @@ def main():
 
     bsz = args.block_mib << 20
     total = args.blocks * bsz
-    ctx = CrcContext(0)
+    ctx = CrcContext(0, lib=_native.lab())
     # a deterministic 1 GiB "file" and its .meta words, computed on the GPU (checked below)
     rng = np.random.default_rng(0x5EED)
     data = rng.integers(0, 256, size=total, dtype=np.uint8)
@@ -193,7 +193,7 @@ def main():
     # (the words' parity with the reference is the -m gpu suite's job; this tool only times)
     print(json.dumps({**line, "mode": "host_verify_pageable",
                       "gib_s": round(host_verify(ctx, data, crc, args.bpc, args.reps), 2)}), flush=True)
-    lib = _native.lib()
+    lib = _native.lab()
     hp = ctypes.c_void_p()
     _native.check("hdfs3_host_malloc_pinned", lib.hdfs3_host_malloc_pinned(ctypes.byref(hp), total))
     pinned = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(hp.value))

@@ -16,11 +16,11 @@ def main():
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import CrcContext
 
-    lib = _native.lib()
+    lib = _native.lab()
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(st)
-    ctx = CrcContext(0)
+    ctx = CrcContext(0, lib=_native.lab())
     ctx.set_stream(st.cuda_stream)
     blocks, bb, bpc = 8, 128 << 20, 512
     data = torch.randint(0, 256, (blocks, bb), dtype=torch.uint8, device=dev)

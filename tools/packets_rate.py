@@ -21,8 +21,8 @@ def main():
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import CrcContext
 
-    lib = _native.lib()
-    ctx = CrcContext(0)
+    lib = _native.lab()
+    ctx = CrcContext(0, lib=_native.lab())
     bpc, pkt = 512, 65536
     n = (1 << 30) // pkt
     stride = 512 + pkt  # [128 CRC words][64 KiB data]: data stays 16 B aligned

@@ -20,8 +20,8 @@ def main():
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import CrcContext
 
-    lib = _native.lib()
-    ctx = CrcContext(0)
+    lib = _native.lab()
+    ctx = CrcContext(0, lib=_native.lab())
     dev = torch.device("cuda", 0)
     blocks, bb = 8, 128 << 20
     data = torch.randint(0, 256, (blocks, bb), dtype=torch.uint8, device=dev)

@@ -22,11 +22,11 @@ def main():
     from libhdfs3_amd.engine import CrcContext
 
     var = int(sys.argv[1]) if len(sys.argv) > 1 else 50
-    lib = _native.lib()
+    lib = _native.lab()
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(st)
-    ctx = CrcContext(0)
+    ctx = CrcContext(0, lib=_native.lab())
     ctx.set_stream(st.cuda_stream)
     nb, bb, bpc = 8, 128 << 20, 512
     total = nb * bb

@@ -17,9 +17,9 @@ def main():
     from libhdfs3_amd.engine import CrcContext
 
     variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,2").split(",")]
-    lib = _native.lib()
+    lib = _native.lab()
     dev = torch.device("cuda", 0)
-    ctx = CrcContext(0)
+    ctx = CrcContext(0, lib=_native.lab())
     st = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(st)
     ctx.set_stream(st.cuda_stream)

@@ -16,9 +16,9 @@ def main():
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import CrcContext
 
-    lib = _native.lib()
+    lib = _native.lab()
     dev = torch.device("cuda", 0)
-    ctx = CrcContext(0)
+    ctx = CrcContext(0, lib=_native.lab())
     st = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(st)
     ctx.set_stream(st.cuda_stream)
