@@ -32,7 +32,14 @@ CONSUMER := tests/native/abi_consumer
 CLIENT_CONSUMER := tests/native/client_consumer
 HDFS_CONSUMER := tests/native/hdfs_consumer
 
-all: $(LIB) $(LABLIB) $(LOOPBACK) oracle $(CONSUMER) $(CLIENT_CONSUMER) $(HDFS_CONSUMER)
+# Adapters of integration/ compiled against the reference's OWN headers (and, for the block
+# reader, linked with the reference's src/common/Exception.cpp, which builds from that one
+# file): only where /root/reference exists; outputs go to oracle/_ref/ and travel with the tree.
+REF      ?= /root/reference
+REFBIN   := oracle/_ref
+REFCHECK := $(if $(wildcard $(REF)/src/common/Checksum.h),$(REFBIN)/checksum_kat $(REFBIN)/blockreader_consumer,)
+
+all: $(LIB) $(LABLIB) $(LOOPBACK) oracle $(CONSUMER) $(CLIENT_CONSUMER) $(HDFS_CONSUMER) $(REFCHECK)
 
 define hip_rule
 $(OBJDIR)/$(call objname,$(1)): $(CSRC)/$(1) $(HDRS)
@@ -90,6 +97,19 @@ $(HDFS_CONSUMER): tests/native/hdfs_consumer.c include/hdfs3_hdfs.h $(OBJDIR)/co
 	gcc -O2 -std=c11 -Wall -Iinclude -Ioracle -o $@ tests/native/hdfs_consumer.c $(OBJDIR)/consumer_oracle.o \
 	    -L$(LIBDIR) -lhdfs3_crc -lhdfs3_loopback -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath-link,/opt/rocm/lib \
 	    -pthread
+
+$(REFBIN)/checksum_kat: tests/native/checksum_kat.cpp integration/GpuCrc32c.h include/hdfs3_crc.h $(LIB)
+	@mkdir -p $(REFBIN)
+	g++ -O2 -std=c++17 -Wall -Iinclude -Iintegration -I$(REF)/src/common -o $@ tests/native/checksum_kat.cpp \
+	    -L$(LIBDIR) -lhdfs3_crc -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath-link,/opt/rocm/lib -pthread
+
+$(REFBIN)/blockreader_consumer: tests/native/blockreader_consumer.cpp integration/GpuRemoteBlockReader.h \
+                                $(OBJDIR)/consumer_oracle.o $(LIB) $(LOOPBACK)
+	@mkdir -p $(REFBIN)
+	g++ -O2 -std=c++17 -Wall -Iinclude -Iintegration -Ioracle -I$(REF)/src/client -I$(REF)/src/common -o $@ \
+	    tests/native/blockreader_consumer.cpp $(REF)/src/common/Exception.cpp $(OBJDIR)/consumer_oracle.o \
+	    -L$(LIBDIR) -lhdfs3_crc -lhdfs3_loopback -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' \
+	    -Wl,-rpath-link,/opt/rocm/lib -pthread
 
 oracle:
 	$(MAKE) -C oracle all

@@ -82,7 +82,12 @@ struct Timer {  // adds the scope's duration to a counter
     ~Timer() { acc.fetch_add(now_ns() - t0, std::memory_order_relaxed); }
 };
 
+// Set on the failing thread by every HIP failure: a local GPU / pinned-memory fault, which
+// another replica cannot cure (the input stream must not fail over on it).
+thread_local bool t_hip_fault = false;
+
 int hip_err(hipError_t e, const char *what) {
+    t_hip_fault = true;
     return fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
 }
 
@@ -139,6 +144,7 @@ struct hdfs3_block_reader {
     int64_t last_seqno = -1;
     bool range_done = false;   // every packet of the range (and the trailer) received
     bool trailer_ok = false;   // the trailer was the empty last packet (readTrailingEmptyPacket)
+    std::atomic<bool> local_fault{false};  // the failure is this host's GPU/memory, not the replica
     bool have_pending_hdr = false;
     wire::PacketHeader pending_hdr;
 
@@ -324,12 +330,14 @@ struct hdfs3_block_reader {
                 free_slots.pop_front();
             }
             Batch &b = slot[s];
+            t_hip_fault = false;
             int rc = acquire(b);
             if (!rc) rc = receive(b);
             if (!rc && !b.pk.empty()) {
                 rc = launch(b);
                 if (rc) recv_msg = hdfs3_crc_last_error();
             }
+            if (rc && t_hip_fault) local_fault = true;
             {
                 std::lock_guard<std::mutex> lk(mu);
                 if (!rc && !b.pk.empty())
@@ -399,7 +407,10 @@ struct hdfs3_block_reader {
                 s = ready.front();
             }
             Batch &b = slot[s];
-            if (int rc = wait(b)) return total ? total : sticky(rc, hdfs3_crc_last_error());
+            if (int rc = wait(b)) {
+                local_fault = true;
+                return total ? total : sticky(rc, hdfs3_crc_last_error());
+            }
             const size_t limit = b.bad_pkt >= 0 ? size_t(b.bad_pkt) : b.pk.size();
             {
                 Timer tm(t_ns[4]);
@@ -478,6 +489,8 @@ struct hdfs3_block_reader {
 };
 
 namespace hdfs3crc {
+
+bool block_reader_local_fault(const hdfs3_block_reader *r) { return r && r->local_fault.load(); }
 
 int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int64_t start, int64_t len,
                       const char *client_name, const hdfs3_reader_opts *opts, hdfs3_crc_ctx *shared_ctx,

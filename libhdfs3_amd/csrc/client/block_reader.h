@@ -12,4 +12,8 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
                       const char *client_name, const hdfs3_reader_opts *opts, hdfs3_crc_ctx *shared_ctx,
                       hdfs3_block_reader **out);
 
+// true when the reader's failure came from this host's GPU or pinned memory (a HIP error),
+// not from the datanode: InputStreamImpl's replica failover must not run on it
+bool block_reader_local_fault(const hdfs3_block_reader *r);
+
 }  // namespace hdfs3crc

@@ -100,7 +100,7 @@ struct hdfs3_input_stream {
                 ++opened;
                 return 0;
             }
-            if (rc == -ENOTSUP || rc == -ENOMEM) {  // not a replica problem: another node cannot help
+            if (rc == -ENOTSUP || rc == -ENOMEM || rc == -ENODEV) {  // not a replica problem: another node cannot help
                 last_error = hdfs3_crc_last_error();
                 return rc;
             }
@@ -130,6 +130,12 @@ struct hdfs3_input_stream {
                 cursor += n;
                 return n;
             }
+            // a local GPU/memory fault is not the replica's: report it, do not burn the replicas
+            if (block_reader_local_fault(reader)) {
+                last_error = hdfs3_crc_last_error();
+                drop_reader();
+                return n < 0 ? n : -EIO;
+            }
             // ChecksumException or I/O failure: this replica is bad, try another (:682-708)
             ++failovers;
             failed.push_back(cur_node);
@@ -157,13 +163,20 @@ struct hdfs3_input_stream {
             Node node;
             if ((rc = setup(b, start, len, &r, &node))) break;
             int64_t got = 0;
+            int32_t n = 0;
             while (got < len) {
-                const int32_t n = hdfs3_block_reader_read(r, out + got, int32_t(std::min<int64_t>(len - got, 1 << 30)));
+                n = hdfs3_block_reader_read(r, out + got, int32_t(std::min<int64_t>(len - got, 1 << 30)));
                 if (n <= 0) break;
                 got += n;
             }
+            const bool local = block_reader_local_fault(r);
+            if (local) last_error = hdfs3_crc_last_error();
             hdfs3_block_reader_close(r);
             if (got == len) break;
+            if (local) {  // this host's GPU, not the replica: no failover
+                rc = n < 0 ? n : -EIO;
+                break;
+            }
             ++failovers;
             failed.push_back(node);
         }

@@ -334,6 +334,8 @@ int hdfs3_output_open(const hdfs3_writer_opts *opts, hdfs3_packet_sink sink, voi
         delete s;
         return rc;
     }
+    // arenas, events and launches belong to the ctx's device, whatever is current here
+    DeviceGuard g(device);
     if (int rc = s->init()) {
         delete s;
         return rc;
@@ -345,6 +347,7 @@ int hdfs3_output_open(const hdfs3_writer_opts *opts, hdfs3_packet_sink sink, voi
 int32_t hdfs3_output_write(hdfs3_output_stream *s, const void *buf, int32_t len) {
     if (!s || !buf || len <= 0) return posix_fail(EINVAL, "hdfsWrite: invalid argument");
     if (s->error) return posix_fail(EIO, s->error_msg);
+    DeviceGuard g(s->ctx->device);
     if (int rc = s->append(static_cast<const uint8_t *>(buf), len))
         return posix_fail(-rc, s->error ? s->error_msg : std::string(hdfs3_crc_last_error()));
     return len;
@@ -353,6 +356,7 @@ int32_t hdfs3_output_write(hdfs3_output_stream *s, const void *buf, int32_t len)
 int hdfs3_output_flush(hdfs3_output_stream *s) {
     if (!s) return posix_fail(EINVAL, "hdfsFlush: invalid argument");
     if (s->error) return posix_fail(EIO, s->error_msg);
+    DeviceGuard g(s->ctx->device);
     if (int rc = s->flush(false)) return posix_fail(-rc, s->error ? s->error_msg : hdfs3_crc_last_error());
     return 0;
 }
@@ -360,6 +364,7 @@ int hdfs3_output_flush(hdfs3_output_stream *s) {
 int hdfs3_output_sync(hdfs3_output_stream *s) {
     if (!s) return posix_fail(EINVAL, "hdfsSync: invalid argument");
     if (s->error) return posix_fail(EIO, s->error_msg);
+    DeviceGuard g(s->ctx->device);
     if (int rc = s->flush(true)) return posix_fail(-rc, s->error ? s->error_msg : hdfs3_crc_last_error());
     return 0;
 }
@@ -378,6 +383,7 @@ int hdfs3_output_stats(hdfs3_output_stream *s, uint64_t *packets, uint64_t *gpu_
 
 int hdfs3_output_close(hdfs3_output_stream *s) {
     if (!s) return posix_fail(EINVAL, "hdfsCloseFile: invalid argument");
+    DeviceGuard g(s->ctx->device);  // held through the destructor's frees too
     const int rc = s->close();
     const std::string msg = s->error ? s->error_msg : (rc ? std::string(hdfs3_crc_last_error()) : std::string());
     delete s;

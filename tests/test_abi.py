@@ -4,6 +4,7 @@ No compute calls are made here."""
 import ctypes
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -38,6 +39,43 @@ def test_library_exports_every_declared_symbol():
     client = declared_functions(CLIENT_HEADER)
     assert client and not [n for n in client if not hasattr(lib, n)]
     assert sorted(_native.CLIENT_API) == client
+
+
+HDFS_HEADER = os.path.join(REPO, "include", "hdfs3_hdfs.h")
+
+
+def test_hdfs_h_surface_exported():
+    """include/hdfs3_hdfs.h: the hdfs.h functions (reference prototypes) and the namenode
+    stand-in are exported by the product library and bound by _native.HDFS_API."""
+    from libhdfs3_amd import _native
+
+    src = re.sub(r"/\*.*?\*/", "", open(HDFS_HEADER).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(hdfs[A-Z]\w+|hdfs3_fs_\w+)\s*\(", src)))
+    for must in ["hdfsRead", "hdfsPread", "hdfsWrite", "hdfsFlush", "hdfsHFlush", "hdfsSync", "hdfsCloseFile",
+                 "hdfsOpenFile", "hdfsGetLastError"]:
+        assert must in names
+    lib = _native.load()
+    assert not [n for n in names if not hasattr(lib, n)]
+    assert sorted(_native.HDFS_API) == names
+
+
+def _exported(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+def test_product_library_exports_only_the_c_api():
+    """No A/B knob, diagnostic or wrong-on-purpose kernel is reachable from libhdfs3_crc.so:
+    the variant knob (hdfs3x_set_variant) and every hdfs3x_* hook live only in the measurement
+    library libhdfs3_crc_lab.so, and no internal C++ symbol is exported."""
+    from libhdfs3_amd import _native
+
+    prod = {s for s in _exported(_native.LIB_PATH) if not s.startswith("__")}
+    assert not [s for s in prod if s.startswith("hdfs3x_")]
+    assert not [s for s in prod if s.startswith("_Z")]
+    assert all(s.startswith("hdfs3_") or re.match(r"hdfs[A-Z]", s) for s in prod), sorted(prod)
+    lab = _exported(_native.LAB_PATH)
+    assert {"hdfs3x_set_variant", "hdfs3x_stream_read"} <= lab
 
 
 def test_library_is_gfx950_code_object():
