@@ -3,7 +3,7 @@
 // library libhdfs3_crc_lab.so only (HDFS3_LAB=1); the product libhdfs3_crc.so never sees it.
 // Bit-exact variants are parity-tested (tests/test_gpu_parity.py); the diagnostic ones
 // (no HBM / no math / fake lookups / timestamps) give wrong results on purpose.
-#include "crc32c_device.h"
+#include "crc32c_block.h"
 
 namespace hdfs3crc {
 namespace {
@@ -127,6 +127,18 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
     case 38:
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptSlotRegion | kOptWantBuf | kOptNoMath>(
             a, tab, fold, grid_cap, s);
+    case 60:  // block kernel (crc32c_block.h): computed tables + 4-round head
+    case 61: {  // block kernel with the wave kernel's 2-round head (tables still computed)
+        if constexpr (BPC == 512 || BPC == 1024) {
+            if (!a.fold_host || !a.poly) return hipErrorInvalidValue;
+            const uint32_t *cols = a.fold_host + (BPC == 512 ? 0 : 8 * 32);
+            return variant == 60 ? launch_block<BPC, V, true>(a, a.poly, cols, tab, grid_cap, s)
+                                 : launch_block<BPC, V, false>(a, a.poly, cols, tab, grid_cap, s);
+        } else {
+            constexpr int kOpt = (BPC <= kRoundBytes ? kOptLeanFill : 0);
+            return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
+        }
+    }
     case 34: {  // 24 (no table math) with timestamps
         if (!g_trace) return hipErrorInvalidValue;
         ChunkLaunch e = a;

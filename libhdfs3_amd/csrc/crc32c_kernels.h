@@ -23,6 +23,11 @@ struct ChunkLaunch {
     int check_short_tail;     // 1: tail chunk checked (LocalBlockReader semantics)
     uint64_t *trace = nullptr;  // diagnostic variant 13 only: 4 s_memrealtime stamps per wave
     bool overlap_previous = false;  // HDFS3_LAUNCH_OVERLAP_PREVIOUS: AQL packet without barrier bit
+    // the ctx's polynomial and its lane-fold matrices (host copy of crc32c_tables.h
+    // build_fold_matrices: G = 8 at word 0, G = 16 at word 8 * 32): the block kernel
+    // (crc32c_block.h) builds all its tables from these, with no table loads
+    uint32_t poly = 0;
+    const uint32_t *fold_host = nullptr;
 };
 
 // Packet-descriptor as seen by the device (mirrors hdfs3_pkt_desc).

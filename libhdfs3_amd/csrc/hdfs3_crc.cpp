@@ -43,6 +43,32 @@ int fail(int code, const char *fmt, ...) {
 
 }  // namespace hdfs3crc
 
+namespace hdfs3crc {
+
+// Per polynomial ([0] CRC32C, [1] CRC32): slice tables, then the fold image (kFoldWords
+// matrix columns and 4 nibble-table sets for G = 8, 16, 32, 64), built once per process.
+struct HostImage {
+    uint32_t t[kSlices][kTableEntries];
+    uint32_t fold[kFoldWords + 4 * kFoldNibbleWords];
+};
+
+const HostImage *host_images() {
+    static HostImage img[2];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const uint32_t polys[2] = {kPolyReflected, kPolyCrc32};
+        for (int p = 0; p < 2; ++p) {
+            build_slice_tables(img[p].t, polys[p]);
+            build_fold_matrices(img[p].t[0], img[p].fold);
+            for (int set = 0; set < 4; ++set)
+                build_fold_nibbles(img[p].fold, set, img[p].fold + kFoldWords + set * kFoldNibbleWords);
+        }
+    });
+    return img;
+}
+
+}  // namespace hdfs3crc
+
 namespace {
 
 int hip_fail(hipError_t e, const char *what) {
@@ -118,7 +144,10 @@ int finish_pending(Slot &s) {
     return 0;
 }
 
-int launch(hdfs3_crc_ctx *ctx, const ChunkLaunch &a, bool verify) {
+int launch(hdfs3_crc_ctx *ctx, const ChunkLaunch &in, bool verify) {
+    ChunkLaunch a = in;
+    a.poly = ctx->poly;
+    a.fold_host = ctx->fold_host;
     HIP_TRY(launch_chunks(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
     ++ctx->launches;
     return 0;
@@ -391,23 +420,7 @@ int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out) {
         hipHostMalloc(reinterpret_cast<void **>(&ctx->h_result), sizeof(unsigned long long),
                       hipHostMallocDefault) != hipSuccess)
         return bail(fail(-ENOMEM, "device allocation for ctx failed"));
-    // per polynomial: slice tables, then the fold image (kFoldWords matrix columns and 4
-    // nibble-table sets for G = 8,16,32,64), built once per process
-    struct Image {
-        uint32_t t[kSlices][kTableEntries];
-        uint32_t fold[kFoldWords + 4 * kFoldNibbleWords];
-    };
-    static Image img[2];
-    static std::once_flag once;
-    std::call_once(once, [] {
-        const uint32_t polys[2] = {kPolyReflected, kPolyCrc32};
-        for (int p = 0; p < 2; ++p) {
-            build_slice_tables(img[p].t, polys[p]);
-            build_fold_matrices(img[p].t[0], img[p].fold);
-            for (int set = 0; set < 4; ++set)
-                build_fold_nibbles(img[p].fold, set, img[p].fold + kFoldWords + set * kFoldNibbleWords);
-        }
-    });
+    const HostImage *img = host_images();
     for (int p = 0; p < 2; ++p) {
         if (hipMalloc(reinterpret_cast<void **>(&ctx->d_tables_by[p]), sizeof(img[p].t)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&ctx->d_fold_by[p]), sizeof(img[p].fold)) != hipSuccess)
@@ -418,6 +431,8 @@ int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out) {
     }
     ctx->d_tables = ctx->d_tables_by[0];
     ctx->d_fold = ctx->d_fold_by[0];
+    ctx->poly = kPolyReflected;
+    ctx->fold_host = img[0].fold;
     *out = ctx;
     return 0;
 }
@@ -473,6 +488,8 @@ int ctx_acquire(int device, hdfs3_crc_ctx **out) {
             ctx->checksum_type = HDFS3_CHECKSUM_TYPE_CRC32C;
             ctx->d_tables = ctx->d_tables_by[0];
             ctx->d_fold = ctx->d_fold_by[0];
+            ctx->poly = kPolyReflected;
+            ctx->fold_host = host_images()[0].fold;
             *out = ctx;
             return 0;
         }
@@ -522,6 +539,8 @@ int hdfs3_crc_ctx_set_checksum_type(hdfs3_crc_ctx *ctx, int type) {
     const int i = type == HDFS3_CHECKSUM_TYPE_CRC32C ? 0 : 1;
     ctx->d_tables = ctx->d_tables_by[i];
     ctx->d_fold = ctx->d_fold_by[i];
+    ctx->poly = i == 0 ? kPolyReflected : kPolyCrc32;
+    ctx->fold_host = host_images()[i].fold;
     ctx->checksum_type = type;
     return 0;
 }

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--streams", default="1", help="comma list: launches alternate over S streams")
     ap.add_argument("--block-mib", type=int, default=128)
     ap.add_argument("--blocks", type=int, default=8)
+    ap.add_argument("--warm", type=int, default=2000, help="launches of variant 0 before the first sample "
+                                                           "(the GPU needs ~25 ms of load to leave its idle clock)")
     ap.add_argument("--overlap", action="store_true",
                     help="launches after the first of each timed batch use HDFS3_LAUNCH_OVERLAP_PREVIOUS")
     args = ap.parse_args()
@@ -74,6 +76,8 @@ def main():
             cases.append(("coalesced_read_G8", lambda i: lib.hdfs3x_lane_read(
                 ctx.ctx, data[i % blocks].data_ptr(), bb, 512 | (2 << 16), sink.data_ptr())))
         samples = {name: [] for name, _ in cases}
+        for i in range(args.warm):
+            run(0, i, 1)
         for name, fn in cases:  # warm
             for i in range(4):
                 fn(i)
