@@ -51,10 +51,14 @@ public:
 
     int64_t available() override { return hdfs3_block_reader_available(r); }
 
-    /* RemoteBlockReader::read (:332-357): verified bytes only; 0 at the end of the range */
+    /* RemoteBlockReader::read (:332-357): verified bytes only; a read past the end of the
+     * range throws HdfsIOException (:335-338), as the reference does (callers stop on
+     * available()/their own cursor, InputStreamImpl.cpp:616-708) */
     int32_t read(char *buf, int32_t size) override {
         const int32_t n = hdfs3_block_reader_read(r, buf, size);
         if (n < 0) raise(n);
+        if (n == 0)
+            throw HdfsIOException("RemoteBlockReader: read over block end from Datanode", __FILE__, __LINE__, "");
         return n;
     }
 
@@ -63,10 +67,7 @@ public:
         std::vector<char> scratch(len < (1 << 20) ? static_cast<size_t>(len > 0 ? len : 0) : size_t(1) << 20);
         while (len > 0) {
             const int32_t want = static_cast<int32_t>(len < int64_t(scratch.size()) ? len : int64_t(scratch.size()));
-            const int32_t n = read(scratch.data(), want);
-            if (n == 0)
-                throw HdfsIOException("RemoteBlockReader: skip beyond the end of the block range", __FILE__, __LINE__, "");
-            len -= n;
+            len -= read(scratch.data(), want);
         }
     }
 

@@ -59,10 +59,17 @@ int main() {
     try {  // whole block through BlockReader::read
         auto r = open_reader(good, n);
         int64_t pos = 0;
-        for (int32_t got; (got = r->read(out.data() + pos, int32_t(std::min<int64_t>(1 << 20, n - pos)))) > 0;)
-            pos += got;
+        while (pos < n) pos += r->read(out.data() + pos, int32_t(std::min<int64_t>(1 << 20, n - pos)));
         CHECK(pos == n && std::memcmp(out.data(), data.data(), n) == 0, "clean read (%lld bytes)", (long long)pos);
         CHECK(r->available() == 0, "available at end");
+        bool over = false;  // RemoteBlockReader::read past the range end throws HdfsIOException (:335-338)
+        try {
+            char c;
+            r->read(&c, 1);
+        } catch (const Hdfs::HdfsIOException &) {
+            over = true;
+        }
+        CHECK(over, "read over the block end did not throw HdfsIOException");
     } catch (const Hdfs::HdfsException &e) {
         CHECK(false, "clean read threw: %s", e.what());
     }
@@ -71,9 +78,8 @@ int main() {
         r->skip(100000);
         std::vector<char> rest(n - 100000);
         int64_t pos = 0;
-        for (int32_t got; pos < int64_t(rest.size()) &&
-                          (got = r->read(rest.data() + pos, int32_t(std::min<int64_t>(1 << 20, rest.size() - pos)))) > 0;)
-            pos += got;
+        while (pos < int64_t(rest.size()))
+            pos += r->read(rest.data() + pos, int32_t(std::min<int64_t>(1 << 20, rest.size() - pos)));
         CHECK(pos == int64_t(rest.size()) && std::memcmp(rest.data(), data.data() + 100000, rest.size()) == 0,
               "read after skip");
     } catch (const Hdfs::HdfsException &e) {
@@ -83,8 +89,8 @@ int main() {
     int64_t delivered = 0;
     try {  // corrupt replica: verified bytes, then ChecksumException (readOneBlock's failover cue)
         auto r = open_reader(corrupt, n);
-        for (int32_t got; (got = r->read(out.data() + delivered, int32_t(std::min<int64_t>(1 << 16, n - delivered)))) > 0;)
-            delivered += got;
+        while (delivered < n)
+            delivered += r->read(out.data() + delivered, int32_t(std::min<int64_t>(1 << 16, n - delivered)));
     } catch (const Hdfs::ChecksumException &e) {
         checksum_thrown = true;
     } catch (const Hdfs::HdfsException &e) {
