@@ -197,6 +197,55 @@ int hdfs3_output_stats(hdfs3_output_stream *s, uint64_t *packets, uint64_t *gpu_
 int hdfs3_output_close(hdfs3_output_stream *s);
 
 /* ------------------------------------------------------------------------------------
+ * Write pipeline: PipelineImpl (src/client/Pipeline.cpp) for the blocks of one file, the
+ * transport PipelineImpl::send plugs into the sink above. Per block it connects to the
+ * first node, sends OP_WRITE_BLOCK (stage PIPELINE_SETUP_CREATE, the remaining nodes as
+ * targets, ChecksumProto{CRC32C, bytes_per_checksum}; DataTransferProtocolSender.cpp:
+ * 125-150) and checks the BlockOpResponseProto (createBlockOutputStream, Pipeline.cpp:
+ * 529-608); then writes each packet and consumes PipelineAckProto acks (one status per
+ * node) on the caller's thread: one non-blocking check after every send, blocking when more
+ * than max_unacked packets are outstanding, at flush and around the block's last packet
+ * (send/checkResponse/waitForAcks/close, :621-841).
+ *
+ * `blocks` stands in for the namenode: blocks[i] is what addBlock would return for the
+ * file's i-th block (its id and the pipeline's nodes, first node first); the byte counts
+ * and offsets of hdfs3_located_block are ignored here. Pipeline recovery (a namenode round,
+ * :610-619 and buildForAppendOrRecovery) is not rebuilt: any failure — an error status in an
+ * ack, a bad connect ack, a seqno out of order, a timeout — is sticky and surfaces as -EIO
+ * with the message the reference throws before it starts recovery
+ * ("processAck: ack report error at node: ...", "Bad connect ack with firstBadLink as ...").
+ * ---------------------------------------------------------------------------------- */
+typedef struct hdfs3_pipeline hdfs3_pipeline;
+
+typedef struct hdfs3_pipeline_opts {
+    int timeout_ms;      /* output.read.timeout / output.write.timeout analogue (60 s)       */
+    int max_unacked;     /* output.packetpool.size (1024, SessionConfig.cpp:126)            */
+    int checksum_type;   /* 0 or 2 (CHECKSUM_CRC32C, the only type the output stream makes) */
+} hdfs3_pipeline_opts;
+
+int hdfs3_pipeline_open(const hdfs3_located_block *blocks, int n_blocks, const char *client_name,
+                        uint32_t bytes_per_checksum, const hdfs3_pipeline_opts *opts, hdfs3_pipeline **out);
+/* an hdfs3_packet_sink (pass the pipeline as `user`): PipelineImpl::send, or ::close for a
+ * block's last packet (waits for every ack of the block, then closes its connection) */
+int hdfs3_pipeline_send(void *pipeline, const void *packet, size_t len, const hdfs3_packet_info *info);
+/* PipelineImpl::flush: waitForAcks(true) */
+int hdfs3_pipeline_flush(hdfs3_pipeline *p);
+/* bytes acked per block (lastBlock->setNumBytes(bytesAcked)), packets sent, acks received */
+int hdfs3_pipeline_stats(hdfs3_pipeline *p, int64_t *block_bytes_acked, int n_blocks, uint64_t *packets,
+                         uint64_t *acks);
+/* the sticky failure's message ("" while healthy) */
+const char *hdfs3_pipeline_error(hdfs3_pipeline *p);
+/* waits for outstanding acks, closes the connection and frees p; 0 or the sticky -errno */
+int hdfs3_pipeline_close(hdfs3_pipeline *p);
+
+/* hdfs3_output_open with the pipeline as its sink, plus PipelineImpl::flush at every
+ * flush/sync (OutputStreamImpl::flushInternal, :438-440): hdfsFlush/hdfsSync return after
+ * every node acked everything written so far. The pipeline's bytes_per_checksum must equal
+ * opts->bytes_per_checksum (-EINVAL). The stream does not own the pipeline. */
+int hdfs3_output_open_pipeline(const hdfs3_writer_opts *opts, hdfs3_pipeline *pipeline,
+                               hdfs3_output_stream **out);
+
+/* ------------------------------------------------------------------------------------
  * OP_BLOCK_CHECKSUM client (DataTransferProtocolSender::blockChecksum, a TODO in the
  * reference, DataTransferProtocolSender.cpp:169-180): sends version | 85 | varint len |
  * OpBlockChecksumProto to host:port and parses BlockOpResponseProto.checksumResponse

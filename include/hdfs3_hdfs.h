@@ -77,6 +77,14 @@ int hdfs3_fs_add_file(hdfsFS fs, const char *path, const hdfs3_located_block *bl
 /* where the write pipeline of `path` starts: every packet of a file opened O_WRONLY goes to
  * sink(user, ...) (hdfs3_client.h), in seqno order. 0, or -1 with errno (EINVAL). */
 int hdfs3_fs_set_sink(hdfsFS fs, const char *path, hdfs3_packet_sink sink, void *user);
+/* write `path` through datanodes instead: blocks[i] is what addBlock would return for the
+ * file's i-th block (id + pipeline nodes; sizes and offsets ignored). A file opened O_WRONLY
+ * then writes through hdfs3_pipeline (OP_WRITE_BLOCK, acks; include/hdfs3_client.h), and
+ * hdfsFlush/hdfsSync return once every node acked. A clean hdfsCloseFile registers the file for
+ * reading at the acked block lengths from the same nodes (completeFile + getBlockLocations), so
+ * hdfsOpenFile(O_RDONLY)/hdfsRead read back what was written. Takes precedence over a sink.
+ * 0, or -1 with errno (EINVAL). */
+int hdfs3_fs_set_pipeline(hdfsFS fs, const char *path, const hdfs3_located_block *blocks, int n_blocks);
 
 #ifdef __cplusplus
 }

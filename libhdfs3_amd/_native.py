@@ -149,6 +149,12 @@ class WriterOpts(ctypes.Structure):
                 ("block_size", c_int64), ("batch_packets", c_int)]
 
 
+class PipelineOpts(ctypes.Structure):
+    """hdfs3_pipeline_opts (include/hdfs3_client.h)."""
+
+    _fields_ = [("timeout_ms", c_int), ("max_unacked", c_int), ("checksum_type", c_int)]
+
+
 class BlockChecksumInfo(ctypes.Structure):
     """hdfs3_block_checksum_info (include/hdfs3_client.h)."""
 
@@ -189,6 +195,14 @@ CLIENT_API = {
     "hdfs3_output_tell": (c_int64, [c_void_p]),
     "hdfs3_output_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "hdfs3_output_close": (c_int, [c_void_p]),
+    "hdfs3_pipeline_open": (c_int, [POINTER(LocatedBlock), c_int, ctypes.c_char_p, c_uint32, POINTER(PipelineOpts),
+                                    POINTER(c_void_p)]),
+    "hdfs3_pipeline_send": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PacketInfo)]),
+    "hdfs3_pipeline_flush": (c_int, [c_void_p]),
+    "hdfs3_pipeline_stats": (c_int, [c_void_p, POINTER(c_int64), c_int, POINTER(c_uint64), POINTER(c_uint64)]),
+    "hdfs3_pipeline_error": (ctypes.c_char_p, [c_void_p]),
+    "hdfs3_pipeline_close": (c_int, [c_void_p]),
+    "hdfs3_output_open_pipeline": (c_int, [POINTER(WriterOpts), c_void_p, POINTER(c_void_p)]),
 }
 
 # every symbol include/hdfs3_hdfs.h declares (hdfs.h prototypes + the namenode stand-in)
@@ -212,6 +226,7 @@ HDFS_API = {
     "hdfs3_fs_new": (c_void_p, [ctypes.c_char_p, c_void_p, c_void_p]),
     "hdfs3_fs_add_file": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_int]),
     "hdfs3_fs_set_sink": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_void_p]),
+    "hdfs3_fs_set_pipeline": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_int]),
 }
 
 # measurement hooks (libhdfs3_crc_lab.so only; not in any public header)
@@ -279,7 +294,10 @@ def loopback() -> ctypes.CDLL:
         for fn, args, res in [("clear_blocks", [c_int], c_int), ("set_packet_bytes", [c_int, c_int], c_int),
                               ("set_fail_after", [c_int, c_int64], c_int), ("served_bytes", [c_int], c_uint64),
                               ("requests", [c_int], c_uint64), ("last_status", [c_int], c_int),
-                              ("stop", [c_int], c_int)]:
+                              ("stop", [c_int], c_int), ("set_write_fault", [c_int, c_int, c_int64], c_int),
+                              ("write_stats", [c_int] + [POINTER(c_uint64)] * 4, c_int),
+                              ("get_block", [c_int, c_uint64, POINTER(c_void_p), POINTER(c_uint64), POINTER(c_void_p),
+                                             POINTER(c_uint32)], c_int)]:
             f = getattr(lb, "hdfs3_loopback_" + fn)
             f.argtypes, f.restype = args, res
         _LOOPBACK = lb

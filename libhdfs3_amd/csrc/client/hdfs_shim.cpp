@@ -44,13 +44,47 @@ T stream_failed(T rv) {
     return rv;
 }
 
-struct FileEntry {
+// a deep copy of a LocatedBlocks table: the caller's strings and replica tables may go away
+struct BlockTable {
     std::vector<hdfs3_located_block> blocks;
     std::vector<std::vector<hdfs3_datanode>> replicas;
     std::vector<std::string> strings;  // pool ids and host names the tables point into
+
+    bool assign(const hdfs3_located_block *b, int n) {
+        blocks.assign(b, b + n);
+        replicas.assign(size_t(n), {});
+        strings.clear();
+        size_t nstr = 0;
+        for (int i = 0; i < n; ++i) nstr += 1 + size_t(b[i].n_replicas > 0 ? b[i].n_replicas : 0);
+        strings.reserve(nstr);  // no reallocation: the c_str() pointers below stay valid
+        for (int i = 0; i < n; ++i) {
+            if (b[i].n_replicas < 0 || (b[i].n_replicas > 0 && !b[i].replicas)) return false;
+            strings.emplace_back(b[i].block.pool_id ? b[i].block.pool_id : "");
+            blocks[size_t(i)].block.pool_id = strings.back().c_str();
+            for (int k = 0; k < b[i].n_replicas; ++k) {
+                if (!b[i].replicas[k].host) return false;
+                strings.emplace_back(b[i].replicas[k].host);
+                replicas[size_t(i)].push_back(hdfs3_datanode{strings.back().c_str(), b[i].replicas[k].port});
+            }
+            blocks[size_t(i)].replicas = replicas[size_t(i)].data();
+        }
+        return true;
+    }
+    BlockTable() = default;
+    BlockTable(const BlockTable &o) { assign(o.blocks.data(), int(o.blocks.size())); }
+    BlockTable &operator=(const BlockTable &o) {
+        if (this != &o) assign(o.blocks.data(), int(o.blocks.size()));
+        return *this;
+    }
+};
+
+struct FileEntry {
+    BlockTable located_blocks;
     bool located = false;  // registered by hdfs3_fs_add_file (a file of 0 blocks is empty)
     hdfs3_packet_sink sink = nullptr;
     void *user = nullptr;
+    BlockTable pipeline_blocks;  // hdfs3_fs_set_pipeline: the blocks addBlock would allocate
+    bool pipeline = false;
 };
 
 }  // namespace
@@ -67,6 +101,9 @@ struct HdfsFileInternalWrapper {
     bool input = true;
     hdfs3_input_stream *in = nullptr;
     hdfs3_output_stream *out = nullptr;
+    hdfs3_pipeline *pipe = nullptr;  // writes through datanodes (hdfs3_fs_set_pipeline)
+    BlockTable written;              // the pipeline's blocks, for completeFile
+    std::string path;
 };
 
 extern "C" {
@@ -100,30 +137,24 @@ hdfsFS hdfs3_fs_new(const char *client_name, const hdfs3_reader_opts *read_opts,
 int hdfs3_fs_add_file(hdfsFS fs, const char *path, const hdfs3_located_block *blocks, int n_blocks) {
     PARAMETER_ASSERT(fs && path && std::strlen(path) > 0 && n_blocks >= 0 && (n_blocks == 0 || blocks), -1,
                      EINVAL);
-    FileEntry e;
-    e.located = true;
-    e.blocks.assign(blocks, blocks + n_blocks);
-    e.replicas.resize(size_t(n_blocks));
-    // deep copy: the caller's strings and replica tables may go away after this call
-    size_t nstr = 0;
-    for (int i = 0; i < n_blocks; ++i) nstr += 1 + size_t(blocks[i].n_replicas > 0 ? blocks[i].n_replicas : 0);
-    e.strings.reserve(nstr);  // no reallocation: the c_str() pointers below stay valid
-    for (int i = 0; i < n_blocks; ++i) {
-        PARAMETER_ASSERT(blocks[i].n_replicas >= 0 && (blocks[i].n_replicas == 0 || blocks[i].replicas), -1, EINVAL);
-        e.strings.emplace_back(blocks[i].block.pool_id ? blocks[i].block.pool_id : "");
-        e.blocks[size_t(i)].block.pool_id = e.strings.back().c_str();
-        for (int k = 0; k < blocks[i].n_replicas; ++k) {
-            PARAMETER_ASSERT(blocks[i].replicas[k].host, -1, EINVAL);
-            e.strings.emplace_back(blocks[i].replicas[k].host);
-            e.replicas[size_t(i)].push_back(hdfs3_datanode{e.strings.back().c_str(), blocks[i].replicas[k].port});
-        }
-        e.blocks[size_t(i)].replicas = e.replicas[size_t(i)].data();
-    }
+    BlockTable t;
+    PARAMETER_ASSERT(t.assign(blocks, n_blocks), -1, EINVAL);
     std::lock_guard<std::mutex> lk(fs->mu);
     FileEntry &slot = fs->files[path];
-    e.sink = slot.sink;
-    e.user = slot.user;
-    slot = std::move(e);
+    slot.located_blocks = t;
+    slot.located = true;
+    return 0;
+}
+
+int hdfs3_fs_set_pipeline(hdfsFS fs, const char *path, const hdfs3_located_block *blocks, int n_blocks) {
+    PARAMETER_ASSERT(fs && path && std::strlen(path) > 0 && n_blocks > 0 && blocks, -1, EINVAL);
+    BlockTable t;
+    PARAMETER_ASSERT(t.assign(blocks, n_blocks), -1, EINVAL);
+    for (int i = 0; i < n_blocks; ++i) PARAMETER_ASSERT(blocks[i].n_replicas > 0, -1, EINVAL);
+    std::lock_guard<std::mutex> lk(fs->mu);
+    FileEntry &slot = fs->files[path];
+    slot.pipeline_blocks = t;
+    slot.pipeline = true;
     return 0;
 }
 
@@ -161,7 +192,7 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
         // held across the open: hdfs3_input_open copies the located blocks out of the table
         std::lock_guard<std::mutex> lk(fs->mu);
         auto it = fs->files.find(path);
-        if (it == fs->files.end() || (write ? !it->second.sink : !it->second.located)) {
+        if (it == fs->files.end() || (write ? !it->second.sink && !it->second.pipeline : !it->second.located)) {
             delete file;
             set_msg((std::string(write ? "no write pipeline registered for " : "file does not exist: ") + path).c_str());
             errno = ENOENT;  // FileNotFoundException -> ENOENT (Hdfs.cpp:243-327)
@@ -179,20 +210,51 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
                 errno = EINVAL;
                 return nullptr;
             }
-            rc = hdfs3_output_open(&o, e.sink, e.user, &file->out);
+            if (e.pipeline) {  // datanodes: PipelineImpl behind the stream
+                file->written = e.pipeline_blocks;
+                file->path = path;
+                rc = hdfs3_pipeline_open(file->written.blocks.data(), int(file->written.blocks.size()),
+                                         fs->client_name.c_str(), o.bytes_per_checksum, nullptr, &file->pipe);
+                if (rc == 0) rc = hdfs3_output_open_pipeline(&o, file->pipe, &file->out);
+            } else {
+                rc = hdfs3_output_open(&o, e.sink, e.user, &file->out);
+            }
         } else {
-            rc = hdfs3_input_open(e.blocks.data(), int(e.blocks.size()), fs->client_name.c_str(), &fs->ropts,
-                                  &file->in);
+            rc = hdfs3_input_open(e.located_blocks.blocks.data(), int(e.located_blocks.blocks.size()),
+                                  fs->client_name.c_str(), &fs->ropts, &file->in);
         }
     }
     if (rc < 0) {
-        delete file;
         set_msg(hdfs3_crc_last_error());
+        if (file->pipe) hdfs3_pipeline_close(file->pipe);
+        delete file;
         errno = -rc;
         return nullptr;
     }
     return file;
 }
+
+namespace {
+// completeFile: after a clean close through datanodes the file is readable at the length the
+// pipeline had acked per block (lastBlock->setNumBytes(bytesAcked), Pipeline.cpp:836), from the
+// nodes it was written to — what getBlockLocations returns after complete()
+void complete_written_file(hdfsFS fs, hdfsFile file) {
+    std::vector<int64_t> acked(file->written.blocks.size(), 0);
+    hdfs3_pipeline_stats(file->pipe, acked.data(), int(acked.size()), nullptr, nullptr);
+    BlockTable t = file->written;
+    int64_t off = 0;
+    size_t n = 0;
+    for (; n < acked.size() && acked[n] > 0; ++n) {
+        t.blocks[n].block.num_bytes = uint64_t(acked[n]);
+        t.blocks[n].offset = off;
+        off += acked[n];
+    }
+    std::lock_guard<std::mutex> lk(fs->mu);
+    FileEntry &slot = fs->files[file->path];
+    slot.located_blocks.assign(t.blocks.data(), int(n));
+    slot.located = true;
+}
+}  // namespace
 
 int hdfsCloseFile(hdfsFS fs, hdfsFile file) {
     PARAMETER_ASSERT(fs, -1, EINVAL);
@@ -202,6 +264,18 @@ int hdfsCloseFile(hdfsFS fs, hdfsFile file) {
         rc = hdfs3_input_close(file->in);
     } else {
         rc = hdfs3_output_close(file->out);  // frees the stream even on error
+        if (file->pipe) {
+            const int e = errno;
+            const int prc = hdfs3_pipeline_flush(file->pipe);
+            if (rc == 0 && prc == 0) complete_written_file(fs, file);
+            hdfs3_pipeline_close(file->pipe);
+            if (rc == 0 && prc < 0) {
+                rc = -1;
+                errno = -prc;
+            } else {
+                errno = e;
+            }
+        }
     }
     delete file;  // freed even after an I/O error (hdfs.h:328-330)
     if (rc < 0) return stream_failed(-1);

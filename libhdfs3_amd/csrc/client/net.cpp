@@ -24,6 +24,11 @@ static int wait_fd(int fd, short events, int timeout_ms) {
     }
 }
 
+int readable(int fd, int timeout_ms) {
+    const int rc = wait_fd(fd, POLLIN, timeout_ms);
+    return rc == 0 ? 1 : rc == -ETIMEDOUT ? 0 : rc;
+}
+
 int connect_tcp(const char *host, int port, int timeout_ms) {
     addrinfo hints{};
     hints.ai_family = AF_INET;

@@ -22,6 +22,8 @@ int read_varint32(int fd, uint32_t *out, int timeout_ms);
 // read a varint-length-prefixed message (bounded by max_len, RemoteBlockReader.cpp:116)
 int read_delimited(int fd, std::string &out, size_t max_len, int timeout_ms);
 int write_delimited(int fd, const std::string &msg, int timeout_ms);
+// poll for readability: 1 readable (or EOF/error pending), 0 not within timeout_ms, -errno
+int readable(int fd, int timeout_ms);
 void close_fd(int fd);
 
 }  // namespace net

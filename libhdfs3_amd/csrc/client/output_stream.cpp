@@ -29,6 +29,10 @@
 
 using namespace hdfs3crc;
 
+namespace hdfs3crc {
+uint32_t pipeline_bpc(const hdfs3_pipeline *p);  // client/pipeline.cpp
+}
+
 namespace {
 
 constexpr int kDefaultBatchPackets = 64;
@@ -76,6 +80,7 @@ struct hdfs3_output_stream {
     hdfs3_crc_ctx *ctx = nullptr;
     hdfs3_packet_sink sink = nullptr;
     void *user = nullptr;
+    hdfs3_pipeline *pipeline = nullptr;  // set by hdfs3_output_open_pipeline: flushed at flush/sync
     uint32_t bpc = 512;
     int32_t packet_size = 64 * 1024;
     int64_t block_size = 64ll << 20;
@@ -291,7 +296,10 @@ struct hdfs3_output_stream {
         if (!cur && need_sync && pipeline_open)
             if (int rc = open_packet()) return rc;  // an empty packet carries the sync
         if (cur) send_current();
-        return drain();
+        if (int rc = drain()) return rc;
+        if (pipeline && hdfs3_pipeline_flush(pipeline))  // pipeline->flush() (:438-440)
+            return sticky(-EIO, hdfs3_pipeline_error(pipeline));
+        return 0;
     }
 
     // close (:538-575)
@@ -308,6 +316,17 @@ struct hdfs3_output_stream {
 };
 
 extern "C" {
+
+int hdfs3_output_open_pipeline(const hdfs3_writer_opts *opts, hdfs3_pipeline *pipeline,
+                               hdfs3_output_stream **out) {
+    if (!pipeline || !out) return fail(-EINVAL, "invalid argument");
+    const uint32_t bpc = opts && opts->bytes_per_checksum ? opts->bytes_per_checksum : 512;
+    if (bpc != pipeline_bpc(pipeline))
+        return fail(-EINVAL, "the pipeline's bytes per checksum differ from the stream's");
+    if (int rc = hdfs3_output_open(opts, hdfs3_pipeline_send, pipeline, out)) return rc;
+    (*out)->pipeline = pipeline;
+    return 0;
+}
 
 int hdfs3_output_open(const hdfs3_writer_opts *opts, hdfs3_packet_sink sink, void *user,
                       hdfs3_output_stream **out) {

@@ -281,6 +281,7 @@ bool decode_read_block(const void *proto, size_t n, ReadBlockRequest &out) {
 std::string encode_block_op_response(const BlockOpResponse &r) {
     std::string out;
     put_uint(out, 1, uint64_t(r.status));
+    if (!r.first_bad_link.empty()) put_bytes(out, 2, r.first_bad_link);
     if (r.has_checksum_response) {
         const BlockChecksumResponse &c = r.checksum_response;
         std::string cr;
@@ -312,6 +313,8 @@ bool decode_block_op_response(const void *proto, size_t n, BlockOpResponse &out)
         if (field == 1 && wt == 0) {
             out.status = int(r.varint());
             have_status = true;
+        } else if (field == 2 && wt == 2) {
+            out.first_bad_link = r.bytes();
         } else if (field == 3 && wt == 2) {
             const std::string cr = r.bytes();
             Reader c(cr.data(), cr.size());
@@ -360,6 +363,165 @@ bool decode_block_op_response(const void *proto, size_t n, BlockOpResponse &out)
         }
     }
     return r.ok && have_status;
+}
+
+static std::string encode_datanode(const DatanodeAddr &d) {
+    std::string id;
+    put_bytes(id, 1, d.ip_addr);
+    put_bytes(id, 2, d.host_name);
+    put_bytes(id, 3, d.uuid);
+    put_uint(id, 4, d.xfer_port);
+    put_uint(id, 5, d.info_port);
+    put_uint(id, 6, d.ipc_port);
+    std::string info;
+    put_bytes(info, 1, id);
+    return info;
+}
+
+static bool decode_datanode(const std::string &s, DatanodeAddr &d) {
+    Reader r(s.data(), s.size());
+    while (r.more()) {
+        const uint64_t key = r.varint();
+        const int field = int(key >> 3), wt = int(key & 7);
+        if (field == 1 && wt == 2) {
+            const std::string id = r.bytes();
+            Reader i(id.data(), id.size());
+            while (i.more()) {
+                const uint64_t k2 = i.varint();
+                const int f2 = int(k2 >> 3), w2 = int(k2 & 7);
+                if (f2 == 1 && w2 == 2) d.ip_addr = i.bytes();
+                else if (f2 == 2 && w2 == 2) d.host_name = i.bytes();
+                else if (f2 == 3 && w2 == 2) d.uuid = i.bytes();
+                else if (f2 == 4 && w2 == 0) d.xfer_port = uint32_t(i.varint());
+                else if (f2 == 5 && w2 == 0) d.info_port = uint32_t(i.varint());
+                else if (f2 == 6 && w2 == 0) d.ipc_port = uint32_t(i.varint());
+                else i.skip(w2);
+            }
+            if (!i.ok) return false;
+        } else {
+            r.skip(wt);
+        }
+    }
+    return r.ok;
+}
+
+std::string encode_write_block(const WriteBlockRequest &w) {
+    std::string client_header;
+    put_bytes(client_header, 1, encode_base_header(w.block));
+    put_bytes(client_header, 2, w.client_name);
+    std::string op;
+    put_bytes(op, 1, client_header);
+    for (const DatanodeAddr &t : w.targets) put_bytes(op, 2, encode_datanode(t));
+    put_uint(op, 4, uint64_t(w.stage));
+    put_uint(op, 5, w.pipeline_size);
+    put_uint(op, 6, w.min_bytes_rcvd);
+    put_uint(op, 7, w.max_bytes_rcvd);
+    put_uint(op, 8, w.latest_generation_stamp);
+    std::string ck;
+    put_uint(ck, 1, uint64_t(w.checksum_type));
+    put_uint(ck, 2, w.bytes_per_checksum);
+    put_bytes(op, 9, ck);
+    return frame_op(kOpWriteBlock, op);
+}
+
+bool decode_write_block(const void *proto, size_t n, WriteBlockRequest &out) {
+    Reader r(proto, n);
+    int seen = 0;
+    while (r.more()) {
+        const uint64_t key = r.varint();
+        const int field = int(key >> 3), wt = int(key & 7);
+        if (field == 1 && wt == 2) {
+            const std::string ch = r.bytes();
+            Reader h(ch.data(), ch.size());
+            while (h.more()) {
+                const uint64_t k2 = h.varint();
+                const int f2 = int(k2 >> 3), w2 = int(k2 & 7);
+                if (f2 == 1 && w2 == 2) {
+                    const std::string base = h.bytes();
+                    Reader b(base.data(), base.size());
+                    while (b.more()) {
+                        const uint64_t k3 = b.varint();
+                        const int f3 = int(k3 >> 3), w3 = int(k3 & 7);
+                        if (f3 == 1 && w3 == 2) {
+                            if (!decode_extended_block(b.bytes(), out.block)) return false;
+                        } else {
+                            b.skip(w3);
+                        }
+                    }
+                    if (!b.ok) return false;
+                } else if (f2 == 2 && w2 == 2) {
+                    out.client_name = h.bytes();
+                } else {
+                    h.skip(w2);
+                }
+            }
+            if (!h.ok) return false;
+            seen |= 1;
+        } else if (field == 2 && wt == 2) {
+            DatanodeAddr d;
+            if (!decode_datanode(r.bytes(), d)) return false;
+            out.targets.push_back(d);
+        } else if (field == 4 && wt == 0) {
+            out.stage = int(r.varint()), seen |= 2;
+        } else if (field == 5 && wt == 0) {
+            out.pipeline_size = uint32_t(r.varint()), seen |= 4;
+        } else if (field == 6 && wt == 0) {
+            out.min_bytes_rcvd = r.varint(), seen |= 8;
+        } else if (field == 7 && wt == 0) {
+            out.max_bytes_rcvd = r.varint(), seen |= 16;
+        } else if (field == 8 && wt == 0) {
+            out.latest_generation_stamp = r.varint(), seen |= 32;
+        } else if (field == 9 && wt == 2) {
+            const std::string ck = r.bytes();
+            Reader c(ck.data(), ck.size());
+            while (c.more()) {
+                const uint64_t k2 = c.varint();
+                const int f2 = int(k2 >> 3), w2 = int(k2 & 7);
+                if (f2 == 1 && w2 == 0) out.checksum_type = int(c.varint());
+                else if (f2 == 2 && w2 == 0) out.bytes_per_checksum = uint32_t(c.varint());
+                else c.skip(w2);
+            }
+            if (!c.ok) return false;
+            seen |= 64;
+        } else {
+            r.skip(wt);
+        }
+    }
+    return r.ok && seen == 127;  // every required field (datatransfer.proto:78-109)
+}
+
+std::string encode_pipeline_ack(const PipelineAck &a) {
+    std::string out;
+    put_uint(out, 1, (uint64_t(a.seqno) << 1) ^ uint64_t(a.seqno >> 63));  // sint64: zigzag
+    for (int s : a.status) put_uint(out, 2, uint64_t(s));
+    if (a.downstream_ack_time_nanos) put_uint(out, 3, a.downstream_ack_time_nanos);
+    return out;
+}
+
+bool decode_pipeline_ack(const void *proto, size_t n, PipelineAck &out) {
+    Reader r(proto, n);
+    bool have_seqno = false;
+    while (r.more()) {
+        const uint64_t key = r.varint();
+        const int field = int(key >> 3), wt = int(key & 7);
+        if (field == 1 && wt == 0) {
+            const uint64_t z = r.varint();
+            out.seqno = int64_t(z >> 1) ^ -int64_t(z & 1);
+            have_seqno = true;
+        } else if (field == 2 && wt == 0) {
+            out.status.push_back(int(r.varint()));
+        } else if (field == 2 && wt == 2) {  // packed encoding is legal for a repeated enum
+            const std::string packed = r.bytes();
+            Reader p(packed.data(), packed.size());
+            while (p.more()) out.status.push_back(int(p.varint()));
+            if (!p.ok) return false;
+        } else if (field == 3 && wt == 0) {
+            out.downstream_ack_time_nanos = r.varint();
+        } else {
+            r.skip(wt);
+        }
+    }
+    return r.ok && have_seqno;
 }
 
 std::string encode_client_read_status(int status) {

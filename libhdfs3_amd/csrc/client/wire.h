@@ -107,6 +107,7 @@ bool decode_block_checksum(const void *proto, size_t n, ExtendedBlock &out);
 
 struct BlockOpResponse {           // BlockOpResponseProto, datatransfer.proto:189-209
     int status = kSuccess;
+    std::string first_bad_link;           // field 2 (WRITE_BLOCK setup replies, Pipeline.cpp:562)
     bool has_checksum_response = false;   // field 3 (OP_BLOCK_CHECKSUM replies)
     BlockChecksumResponse checksum_response;
     bool has_checksum_info = false;
@@ -117,6 +118,48 @@ struct BlockOpResponse {           // BlockOpResponseProto, datatransfer.proto:1
 };
 std::string encode_block_op_response(const BlockOpResponse &r);   // proto only
 bool decode_block_op_response(const void *proto, size_t n, BlockOpResponse &out);
+
+// OP_WRITE_BLOCK (DataTransferProtocolSender::writeBlock, DataTransferProtocolSender.cpp:
+// 125-150): version | op 80 | varint len | OpWriteBlockProto (datatransfer.proto:77-111)
+struct DatanodeAddr {              // DatanodeInfoProto.id (hdfs.proto:49-60,72-90): the fields
+    std::string ip_addr;           // BuildNodeInfo sets (DataTransferProtocolSender.cpp:80-90)
+    std::string host_name;
+    std::string uuid;
+    uint32_t xfer_port = 0;
+    uint32_t info_port = 0;
+    uint32_t ipc_port = 0;
+};
+enum BlockConstructionStage : int { kPipelineSetupCreate = 6, kPipelineClose = 4, kDataStreaming = 2 };
+struct WriteBlockRequest {
+    ExtendedBlock block;
+    std::string client_name;
+    std::vector<DatanodeAddr> targets;  // the downstream nodes (nodes[1..], Pipeline.cpp:539-543)
+    int stage = kPipelineSetupCreate;
+    uint32_t pipeline_size = 0;         // targets.size() (DataTransferProtocolSender.cpp:135)
+    uint64_t min_bytes_rcvd = 0;
+    uint64_t max_bytes_rcvd = 0;
+    uint64_t latest_generation_stamp = 0;
+    int checksum_type = kChecksumCrc32c;
+    uint32_t bytes_per_checksum = 512;
+};
+std::string encode_write_block(const WriteBlockRequest &r);
+bool decode_write_block(const void *proto, size_t n, WriteBlockRequest &out);
+
+// PipelineAckProto {1: sint64 seqno, 2: repeated Status, 3: uint64 downstreamAckTimeNanos}
+// (datatransfer.proto:168-172), varint-length-delimited on the wire (Pipeline.cpp:724-740)
+constexpr int64_t kHeartbeatSeqno = -1;   // Pipeline.h HEART_BEAT_SEQNO
+struct PipelineAck {
+    int64_t seqno = 0;
+    std::vector<int> status;            // one per node, upstream first
+    uint64_t downstream_ack_time_nanos = 0;
+    bool success() const {              // PipelineAck::isSuccess (PipelineAck.h:63-73)
+        for (int s : status)
+            if (s != kSuccess) return false;
+        return true;
+    }
+};
+std::string encode_pipeline_ack(const PipelineAck &a);   // proto only
+bool decode_pipeline_ack(const void *proto, size_t n, PipelineAck &out);
 
 std::string encode_client_read_status(int status);                // proto only
 bool decode_client_read_status(const void *proto, size_t n, int &status);

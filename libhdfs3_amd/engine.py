@@ -333,6 +333,73 @@ class HdfsIOError(OSError):
     """hdfs.h-style failure (-1 + errno) from an hdfs3_input_* call."""
 
 
+def _located_blocks(blocks, pool_id: bytes, generation_stamp: int):
+    """[(block_id, num_bytes, [(host, port), ...])] -> (LocatedBlock array, objects to keep alive)"""
+    arr = (_native.LocatedBlock * len(blocks))()
+    keep = [arr]
+    off = 0
+    for i, (bid, nbytes, reps) in enumerate(blocks):
+        dn = (_native.Datanode * max(1, len(reps)))()
+        for k, (host, port) in enumerate(reps):
+            h = host.encode() if isinstance(host, str) else host
+            keep.append(h)
+            dn[k].host, dn[k].port = h, port
+        keep.append(dn)
+        arr[i].block = _native.BlockId(pool_id, bid, generation_stamp, nbytes)
+        arr[i].offset = off
+        arr[i].replicas = dn
+        arr[i].n_replicas = len(reps)
+        off += nbytes
+    return arr, keep
+
+
+class Pipeline:
+    """hdfs3_pipeline (include/hdfs3_client.h): PipelineImpl for a file's blocks.
+    `blocks` = [(block_id, [(host, port), ...])]: what addBlock would return for each block,
+    pipeline nodes in order."""
+
+    def __init__(self, blocks, *, bytes_per_checksum: int = 512, timeout_ms: int = 60000, max_unacked: int = 1024,
+                 pool_id: bytes = b"BP-loopback", generation_stamp: int = 1, client_name: bytes = b"libhdfs3_amd"):
+        self._lib = _native.lib()
+        self.n_blocks = len(blocks)
+        arr, self._keep = _located_blocks([(bid, 0, nodes) for bid, nodes in blocks], pool_id, generation_stamp)
+        opts = _native.PipelineOpts(timeout_ms, max_unacked, 0)
+        p = c_void_p()
+        check("hdfs3_pipeline_open", self._lib.hdfs3_pipeline_open(arr, len(blocks), client_name, bytes_per_checksum,
+                                                                   byref(opts), byref(p)))
+        self.p = p.value
+
+    @property
+    def error(self) -> str:
+        return self._lib.hdfs3_pipeline_error(self.p).decode(errors="replace")
+
+    def stats(self):
+        from ctypes import c_int64, c_uint64
+        acked = (c_int64 * self.n_blocks)()
+        pk, ak = c_uint64(), c_uint64()
+        check("hdfs3_pipeline_stats", self._lib.hdfs3_pipeline_stats(self.p, acked, self.n_blocks, byref(pk), byref(ak)))
+        return {"block_bytes_acked": list(acked), "packets": pk.value, "acks": ak.value}
+
+    def close(self) -> int:
+        rc = 0
+        if self.p:
+            p, self.p = self.p, None
+            rc = self._lib.hdfs3_pipeline_close(p)
+        return rc
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class InputStream:
     """hdfs3_input_stream (include/hdfs3_client.h): hdfsRead/hdfsPread/hdfsSeek/hdfsTell over
     located blocks with replica failover. `blocks` = [(block_id, num_bytes, [(host, port), ...])]
@@ -341,21 +408,7 @@ class InputStream:
     def __init__(self, blocks, *, device: int = 0, verify: bool = True, batch_packets: int = 64,
                  timeout_ms: int = 60000, pool_id: bytes = b"BP-loopback", generation_stamp: int = 1):
         self._lib = _native.lib()
-        arr = (_native.LocatedBlock * len(blocks))()
-        self._keep = []
-        off = 0
-        for i, (bid, nbytes, reps) in enumerate(blocks):
-            dn = (_native.Datanode * max(1, len(reps)))()
-            for k, (host, port) in enumerate(reps):
-                h = host.encode() if isinstance(host, str) else host
-                self._keep.append(h)
-                dn[k].host, dn[k].port = h, port
-            self._keep.append(dn)
-            arr[i].block = _native.BlockId(pool_id, bid, generation_stamp, nbytes)
-            arr[i].offset = off
-            arr[i].replicas = dn
-            arr[i].n_replicas = len(reps)
-            off += nbytes
+        arr, self._keep = _located_blocks(blocks, pool_id, generation_stamp)
         opts = _native.ReaderOpts(device, int(verify), batch_packets, timeout_ms)
         p = c_void_p()
         check("hdfs3_input_open", self._lib.hdfs3_input_open(arr, len(blocks), b"libhdfs3_amd", byref(opts), byref(p)))
@@ -428,8 +481,19 @@ class OutputStream:
     packet in seqno order (PipelineImpl::send); by default packets are collected in .packets."""
 
     def __init__(self, *, device: int = 0, bytes_per_checksum: int = 512, packet_size: int = 65536,
-                 block_size: int = 64 << 20, batch_packets: int = 64, sink=None, raw_sink=None, raw_user=None):
+                 block_size: int = 64 << 20, batch_packets: int = 64, sink=None, raw_sink=None, raw_user=None,
+                 pipeline: "Pipeline | None" = None):
+        """pipeline: write to datanodes through hdfs3_output_open_pipeline (flush/sync wait
+        for every node's ack) instead of a sink."""
         self._lib = _native.lib()
+        self.pipeline = pipeline
+        if pipeline is not None:
+            opts = _native.WriterOpts(device, bytes_per_checksum, packet_size, block_size, batch_packets)
+            p = c_void_p()
+            check("hdfs3_output_open_pipeline",
+                  self._lib.hdfs3_output_open_pipeline(byref(opts), pipeline.p, byref(p)))
+            self.s = p.value
+            return
         self.packets: list[tuple[bytes, dict]] = []
         user_sink = sink
 

@@ -54,6 +54,36 @@ class LoopbackDatanode:
             st = self.lb.hdfs3_loopback_last_status(self.port)
         return st
 
+    # write side (OP_WRITE_BLOCK)
+    FAULT_NONE, FAULT_REFUSE_SETUP, FAULT_ACK_ERROR, FAULT_CORRUPT_IN_TRANSIT, FAULT_DROP_AT = range(5)
+
+    def set_write_fault(self, mode: int, seqno: int = -1) -> None:
+        assert self.lb.hdfs3_loopback_set_write_fault(self.port, mode, seqno) == 0
+
+    def write_stats(self) -> dict:
+        v = [ctypes.c_uint64() for _ in range(4)]
+        assert self.lb.hdfs3_loopback_write_stats(self.port, *[ctypes.byref(x) for x in v]) == 0
+        return dict(zip(("packets", "bytes", "checksum_errors", "finalized"), (x.value for x in v)))
+
+    def wait_finalized(self, n: int, timeout: float = 10.0) -> int:
+        deadline = time.time() + timeout
+        while self.write_stats()["finalized"] < n and time.time() < deadline:
+            time.sleep(0.005)
+        return self.write_stats()["finalized"]
+
+    def get_block(self, block_id: int):
+        """(data, crc_be, bpc) of a block this node holds (copies), or None"""
+        d, c = ctypes.c_void_p(), ctypes.c_void_p()
+        n, bpc = ctypes.c_uint64(), ctypes.c_uint32()
+        rc = self.lb.hdfs3_loopback_get_block(self.port, block_id, ctypes.byref(d), ctypes.byref(n), ctypes.byref(c),
+                                              ctypes.byref(bpc))
+        if rc != 0:
+            return None
+        nch = (n.value + bpc.value - 1) // bpc.value
+        data = np.frombuffer(ctypes.string_at(d, n.value), np.uint8).copy() if n.value else np.zeros(0, np.uint8)
+        crc = np.frombuffer(ctypes.string_at(c, 4 * nch), np.uint8).copy() if nch else np.zeros(0, np.uint8)
+        return data, crc, bpc.value
+
     def stop(self) -> None:
         if self.port:
             self.lb.hdfs3_loopback_stop(self.port)

@@ -257,6 +257,52 @@ int main(int argc, char **argv) {
     CHECK(off >= c.len[0] && off <= c.len[0] + flip, "error surfaced at %lld", (long long)off);
     CHECK(inb && hdfsCloseFile(fs, inb) == 0, "close bad");
 
+    /* through datanodes: hdfsWrite -> GPU CRCs -> OP_WRITE_BLOCK pipeline of 3 loopback
+     * nodes (acks per packet, the last node verifies every word) -> hdfsCloseFile registers the
+     * file at the acked lengths -> hdfsOpenFile(O_RDONLY) / hdfsRead back from the nodes */
+    int dn[3] = {0, 0, 0};
+    for (int i = 0; i < 3; ++i) CHECK(hdfs3_loopback_start(&dn[i]) == 0, "loopback start %d", i);
+    hdfs3_datanode chain[3] = {{"127.0.0.1", dn[0]}, {"127.0.0.1", dn[1]}, {"127.0.0.1", dn[2]}};
+    hdfs3_located_block alloc[MAX_BLOCKS];
+    for (int64_t b = 0; b <= nfull; ++b) {
+        hdfs3_located_block lb = {{"BP-loopback", (uint64_t)(5000 + b), 1, 0}, 0, chain, 3};
+        alloc[b] = lb;
+    }
+    CHECK(hdfs3_fs_set_pipeline(fs, "/tmp/dn", alloc, (int)nfull + 1) == 0, "set_pipeline");
+    hdfsFile wp = hdfsOpenFile(fs, "/tmp/dn", O_WRONLY | O_CREAT, 0, 3, 0);
+    CHECK(wp != NULL, "open through datanodes: %s", hdfsGetLastError());
+    double tp = now_s();
+    for (int64_t off = 0; wp && off < size;) {
+        const int32_t b = (int32_t)(size - off < (int64_t)wchunk ? size - off : (int64_t)wchunk);
+        fill_buffer(buf, (size_t)b, (size_t)off);
+        CHECK(hdfsWrite(fs, wp, buf, b) == b, "pipeline hdfsWrite at %lld: %s", (long long)off, hdfsGetLastError());
+        off += b;
+        if (!big && (off / (int64_t)wchunk) % 5 == 0) CHECK(hdfsHFlush(fs, wp) == 0, "pipeline hdfsHFlush");
+    }
+    CHECK(wp && hdfsCloseFile(fs, wp) == 0, "pipeline hdfsCloseFile: %s", hdfsGetLastError());
+    tp = now_s() - tp;
+    CHECK(hdfsExists(fs, "/tmp/dn") == 0, "written file exists after completeFile");
+    hdfsFile rp = hdfsOpenFile(fs, "/tmp/dn", O_RDONLY, 0, 0, 0);
+    CHECK(rp != NULL, "open the written file: %s", hdfsGetLastError());
+    int64_t roff = 0;
+    while (rp && roff < size) {
+        const int32_t want = (int32_t)(size - roff < (int64_t)rchunk ? size - roff : (int64_t)rchunk);
+        const int32_t got = hdfsRead(fs, rp, rbuf, want);
+        if (got <= 0) {
+            CHECK(0, "read back at %lld: %d (%s)", (long long)roff, got, hdfsGetLastError());
+            break;
+        }
+        if (!check_buffer(rbuf, (size_t)got, (size_t)roff)) {
+            CHECK(0, "read-back content at %lld", (long long)roff);
+            break;
+        }
+        roff += got;
+    }
+    CHECK(roff == size, "read back %lld of %lld bytes", (long long)roff, (long long)size);
+    CHECK(rp && hdfsRead(fs, rp, rbuf, 10) == 0, "read-back EOF");
+    CHECK(rp && hdfsCloseFile(fs, rp) == 0, "close read-back");
+    for (int i = 0; i < 3; ++i) hdfs3_loopback_stop(dn[i]);
+
     hdfs3_loopback_stop(good);
     hdfs3_loopback_stop(bad);
     CHECK(hdfsDisconnect(fs) == 0, "hdfsDisconnect");
@@ -273,8 +319,8 @@ int main(int argc, char **argv) {
         return 1;
     }
     printf("{\"hdfs_consumer\": \"ok\", \"bytes\": %lld, \"blocks\": %lld, \"packets\": %lld, "
-           "\"hdfsWrite_GiBps\": %.3f, \"hdfsRead_GiBps\": %.3f}\n",
+           "\"hdfsWrite_GiBps\": %.3f, \"hdfsRead_GiBps\": %.3f, \"hdfsWrite_3node_pipeline_GiBps\": %.3f}\n",
            (long long)size, (long long)c.nblocks, (long long)c.packets, (double)size / tw / (1 << 30),
-           (double)size / tr / (1 << 30));
+           (double)size / tr / (1 << 30), (double)size / tp / (1 << 30));
     return 0;
 }

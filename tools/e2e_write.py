@@ -42,6 +42,42 @@ def main():
         print(json.dumps({"bench": "e2e_write", "mode": "hdfsWrite", "bytes": total, "bpc": 512,
                           "batch_packets": batch, "packets": int(counts[0]), "wire_bytes": int(counts[1]),
                           "gib_s": round(best, 2)}), flush=True)
+    pipeline_rate(data)
+
+
+def pipeline_rate(data):
+    """hdfsWrite through datanodes (config 5's write twin): OP_WRITE_BLOCK pipelines of 1 and 3
+    loopback nodes over 127.0.0.1 TCP; every packet acked by every node, the last node
+    verifying every CRC word on its CPU. Socket-inclusive; GPU compute-on-write."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+    from loopback import LoopbackDatanode
+
+    from libhdfs3_amd.engine import OutputStream, Pipeline
+
+    total, bs = data.size, 128 << 20
+    for n_nodes in (1, 3):
+        nodes = [LoopbackDatanode() for _ in range(n_nodes)]
+        best = 0.0
+        for rep in range(2):
+            chain = [("127.0.0.1", d.port) for d in nodes]
+            blocks = [(7000 + 100 * rep + i, chain) for i in range(total // bs)]
+            with Pipeline(blocks) as pipe:
+                t0 = time.perf_counter()
+                with OutputStream(block_size=bs, batch_packets=64, pipeline=pipe) as s:
+                    for off in range(0, total, 1 << 20):
+                        s.write(data[off:off + (1 << 20)])
+                dt = time.perf_counter() - t0
+                acked = pipe.stats()["block_bytes_acked"]
+            assert acked == [bs] * len(blocks), acked
+            best = max(best, total / dt / 2**30)
+        errs = sum(d.write_stats()["checksum_errors"] for d in nodes)
+        for d in nodes:
+            d.stop()
+        assert errs == 0
+        print(json.dumps({"bench": "e2e_write", "mode": "hdfsWrite->pipeline", "nodes": n_nodes, "bytes": total,
+                          "bpc": 512, "batch_packets": 64, "gib_s": round(best, 2),
+                          "note": "loopback datanodes in this process; the last node verifies on its CPU"}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -8,7 +8,20 @@
 //   status   varint len | ClientReadStatusProto (CHECKSUM_OK / SUCCESS) from the client
 // CRC words are served as given (the caller computes them; corrupt ones for negative
 // tests). Data and CRC buffers are referenced, not copied.
+//
+// Write side (the datanode end of PipelineImpl, src/client/Pipeline.cpp): OP_WRITE_BLOCK
+// with targets forwards the request to the next node and answers with that node's outcome
+// (firstBadLink on failure), then receives packets, mirrors each downstream, verifies the
+// CRC words when it is the last node of the pipeline (as HDFS's BlockReceiver does), stores
+// the block and acks every packet with PipelineAckProto{seqno, [own status] + downstream
+// statuses} from a responder thread. After the last packet's ack the block is readable
+// through OP_READ_BLOCK. Fault injection: refuse the setup, an error status or a dropped
+// connection at a seqno, bytes corrupted in transit at a seqno.
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <vector>
 #include <cerrno>
 #include <cstdint>
 #include <cstring>
@@ -28,13 +41,51 @@ using namespace hdfs3crc;
 
 namespace {
 
+struct Stored {                     // a block received through OP_WRITE_BLOCK
+    std::vector<uint8_t> data, crc_be;
+};
+
 struct Block {
     const uint8_t *data;
     uint64_t len;
     const uint8_t *crc_be;  // ceil(len/bpc) words
     uint32_t bpc;
     int type;
+    std::shared_ptr<Stored> keep;  // owner of data/crc_be for written blocks
 };
+
+enum WriteFault : int { kNoFault = 0, kRefuseSetup = 1, kAckError = 2, kCorruptInTransit = 3, kDropAt = 4 };
+
+// the datanode's own CRC32C (slice-by-8 over the reflected polynomial 0x82F63B78), used to
+// verify received packets; independent of the GPU path under test
+struct SwCrc32c {
+    uint32_t t[8][256];
+    SwCrc32c() {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1)));
+            t[0][i] = c;
+        }
+        for (uint32_t i = 0; i < 256; ++i)
+            for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+    }
+    uint32_t operator()(const uint8_t *p, size_t n) const {
+        uint32_t c = 0xFFFFFFFFu;
+        while (n >= 8) {
+            uint32_t lo, hi;
+            std::memcpy(&lo, p, 4);
+            std::memcpy(&hi, p + 4, 4);
+            lo ^= c;
+            c = t[7][lo & 0xFF] ^ t[6][(lo >> 8) & 0xFF] ^ t[5][(lo >> 16) & 0xFF] ^ t[4][lo >> 24] ^
+                t[3][hi & 0xFF] ^ t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
+            p += 8;
+            n -= 8;
+        }
+        while (n--) c = (c >> 8) ^ t[0][(c ^ *p++) & 0xFF];
+        return ~c;
+    }
+};
+const SwCrc32c g_crc;
 
 // one loopback datanode, identified by its port; several run side by side to act as the
 // replicas of a block (InputStreamImpl failover)
@@ -50,6 +101,10 @@ struct Server {
     std::atomic<int> last_status{-1};
     std::atomic<int> active{0};
     std::thread accept;
+    // write side
+    std::atomic<int> write_fault{kNoFault};
+    std::atomic<int64_t> fault_seqno{-1};
+    std::atomic<uint64_t> write_packets{0}, write_bytes{0}, checksum_errors{0}, blocks_finalized{0};
 };
 
 std::mutex g_mu;
@@ -121,6 +176,189 @@ void serve_block_checksum(Server *sv, int fd, const std::string &proto, int vers
     net::close_fd(fd);
 }
 
+int own_port(Server *sv) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto &kv : g_servers)
+        if (kv.second == sv) return kv.first;
+    return 0;
+}
+
+// one entry per received packet, acked in order by the responder
+struct AckItem {
+    int64_t seqno;
+    int status;
+    bool last;
+    bool drop;   // injected: close the connection instead of acking
+};
+
+// OP_WRITE_BLOCK: BlockReceiver + PacketResponder of one datanode of the pipeline
+void serve_write(Server *sv, int fd, const std::string &proto, int version, int to) {
+    wire::WriteBlockRequest req;
+    wire::BlockOpResponse resp;
+    const std::string self = "127.0.0.1:" + std::to_string(own_port(sv));
+    if (version != wire::kDataTransferVersion || !wire::decode_write_block(proto.data(), proto.size(), req) ||
+        req.bytes_per_checksum == 0) {
+        resp.status = wire::kErrorInvalid;
+        resp.message = "bad write request";
+        (void)net::write_delimited(fd, wire::encode_block_op_response(resp), to);
+        net::close_fd(fd);
+        return;
+    }
+    if (sv->write_fault == kRefuseSetup) {
+        resp.status = wire::kError;
+        resp.first_bad_link = self;
+        (void)net::write_delimited(fd, wire::encode_block_op_response(resp), to);
+        net::close_fd(fd);
+        return;
+    }
+    int down = -1;  // mirror to the next node of the pipeline
+    if (!req.targets.empty()) {
+        const wire::DatanodeAddr next = req.targets[0];
+        wire::WriteBlockRequest fwd = req;
+        fwd.targets.erase(fwd.targets.begin());
+        fwd.pipeline_size = uint32_t(fwd.targets.size());
+        down = net::connect_tcp(next.ip_addr.c_str(), int(next.xfer_port), to);
+        std::string rb;
+        wire::BlockOpResponse dresp;
+        const std::string msg = wire::encode_write_block(fwd);
+        if (down < 0 || net::write_fully(down, msg.data(), msg.size(), to) ||
+            net::read_delimited(down, rb, 1 << 20, to) || !wire::decode_block_op_response(rb.data(), rb.size(), dresp) ||
+            dresp.status != wire::kSuccess) {
+            resp.status = wire::kError;
+            resp.first_bad_link = dresp.first_bad_link.empty() ? next.ip_addr + ":" + std::to_string(next.xfer_port)
+                                                               : dresp.first_bad_link;
+            (void)net::write_delimited(fd, wire::encode_block_op_response(resp), to);
+            net::close_fd(down);
+            net::close_fd(fd);
+            return;
+        }
+    }
+    resp.status = wire::kSuccess;
+    if (net::write_delimited(fd, wire::encode_block_op_response(resp), to)) {
+        net::close_fd(down);
+        net::close_fd(fd);
+        return;
+    }
+    const uint32_t bpc = req.bytes_per_checksum;
+    const bool verify = down < 0 && req.checksum_type == wire::kChecksumCrc32c;  // the last node verifies
+    auto stored = std::make_shared<Stored>();
+
+    std::mutex qmu;
+    std::condition_variable qcv;
+    std::deque<AckItem> q;
+    bool closing = false;
+    std::atomic<bool> broken{false};
+    std::thread responder([&] {
+        for (;;) {
+            AckItem it;
+            {
+                std::unique_lock<std::mutex> lk(qmu);
+                qcv.wait(lk, [&] { return !q.empty() || closing; });
+                if (q.empty()) return;
+                it = q.front();
+                q.pop_front();
+            }
+            if (it.drop) {
+                broken = true;
+                shutdown(fd, SHUT_RDWR);
+                return;
+            }
+            wire::PipelineAck ack;
+            ack.seqno = it.seqno;
+            ack.status.push_back(it.status);
+            if (down >= 0) {  // wait for the downstream ack of the same packet
+                std::string ab;
+                wire::PipelineAck dack;
+                if (net::read_delimited(down, ab, 1 << 16, to) || !wire::decode_pipeline_ack(ab.data(), ab.size(), dack) ||
+                    dack.seqno != it.seqno) {
+                    ack.status.push_back(wire::kError);
+                } else {
+                    ack.status.insert(ack.status.end(), dack.status.begin(), dack.status.end());
+                }
+            }
+            if (net::write_delimited(fd, wire::encode_pipeline_ack(ack), to)) {
+                broken = true;
+                return;
+            }
+            if (it.last && ack.success()) {  // finalize: the block becomes readable
+                std::lock_guard<std::mutex> lk(sv->mu);
+                const uint64_t len = stored->data.size();
+                sv->blocks[req.block.block_id] =
+                    Block{stored->data.data(), len, stored->crc_be.data(), bpc, req.checksum_type, stored};
+                ++sv->blocks_finalized;
+            }
+            if (it.last) return;
+        }
+    });
+
+    std::vector<uint8_t> pkt;
+    for (;;) {
+        uint8_t pre[6];
+        if (broken || net::read_fully(fd, pre, 6, to)) break;
+        const int32_t packet_len = int32_t(wire::rd_be32(pre));
+        const int hdr_len = wire::rd_be16(pre + 4);
+        if (packet_len < 4 || packet_len > (64 << 20) || hdr_len > 1024) break;
+        pkt.resize(6 + size_t(hdr_len) + size_t(packet_len) - 4);
+        std::memcpy(pkt.data(), pre, 6);
+        if (net::read_fully(fd, pkt.data() + 6, pkt.size() - 6, to)) break;
+        wire::PacketHeader h;
+        if (!h.decode(pkt.data(), pkt.size())) break;
+        const uint64_t chunks = (uint64_t(h.data_len) + bpc - 1) / bpc;
+        if (h.data_len < 0 || uint64_t(packet_len) != 4 + uint64_t(h.data_len) + 4 * chunks) break;
+        const int64_t fault_at = sv->fault_seqno.load();
+        const int fault = fault_at == h.seqno ? sv->write_fault.load() : kNoFault;
+        if (fault == kCorruptInTransit && h.data_len > 0) pkt[pkt.size() - 1] ^= 0x40;  // last data byte
+        if (down >= 0 && net::write_fully(down, pkt.data(), pkt.size(), to)) {
+            std::lock_guard<std::mutex> lk(qmu);
+            q.push_back(AckItem{h.seqno, wire::kError, h.last_packet_in_block, false});
+            qcv.notify_one();
+            break;
+        }
+        const uint8_t *sums = pkt.data() + 6 + hdr_len;
+        const uint8_t *data = sums + 4 * chunks;
+        int status = wire::kSuccess;
+        if (verify)
+            for (uint64_t c = 0; c < chunks; ++c) {
+                const uint64_t off = c * bpc;
+                const size_t n = size_t(std::min<uint64_t>(bpc, uint64_t(h.data_len) - off));
+                if (g_crc(data + off, n) != wire::rd_be32(sums + 4 * c)) {
+                    status = wire::kErrorChecksum;
+                    ++sv->checksum_errors;
+                    break;
+                }
+            }
+        if (fault == kAckError) status = wire::kError;
+        if (status == wire::kSuccess && h.data_len > 0) {
+            // a re-sent partial chunk (after hflush) overwrites from offsetInBlock
+            const uint64_t off = uint64_t(h.offset_in_block);
+            if (off > stored->data.size() || off % bpc) {
+                status = wire::kErrorInvalid;
+            } else {
+                stored->data.resize(off);
+                stored->crc_be.resize(off / bpc * 4);
+                stored->data.insert(stored->data.end(), data, data + h.data_len);
+                stored->crc_be.insert(stored->crc_be.end(), sums, sums + 4 * chunks);
+            }
+        }
+        ++sv->write_packets;
+        sv->write_bytes += uint64_t(h.data_len);
+        {
+            std::lock_guard<std::mutex> lk(qmu);
+            q.push_back(AckItem{h.seqno, status, h.last_packet_in_block, fault == kDropAt});
+            qcv.notify_one();
+        }
+        if (fault == kDropAt || h.last_packet_in_block) break;
+    }
+    {
+        std::lock_guard<std::mutex> lk(qmu);
+        closing = true;
+        qcv.notify_one();
+    }
+    responder.join();
+    net::close_fd(down);
+    net::close_fd(fd);
+}
+
 void serve(Server *sv, int fd) {
     const int to = 60000;
     uint8_t head[3];
@@ -133,6 +371,11 @@ void serve(Server *sv, int fd) {
     if (head[2] == wire::kOpBlockChecksum) {
         ++sv->requests;
         serve_block_checksum(sv, fd, proto, (head[0] << 8) | head[1], to);
+        return;
+    }
+    if (head[2] == wire::kOpWriteBlock) {
+        ++sv->requests;
+        serve_write(sv, fd, proto, (head[0] << 8) | head[1], to);
         return;
     }
     if (!wire::decode_read_block(proto.data(), proto.size(), req)) {
@@ -261,7 +504,7 @@ int hdfs3_loopback_add_block(int port, uint64_t block_id, const void *data, uint
     if (!sv || !bpc) return -EINVAL;
     std::lock_guard<std::mutex> lk(sv->mu);
     sv->blocks[block_id] = Block{static_cast<const uint8_t *>(data), len, static_cast<const uint8_t *>(crc_be), bpc,
-                                 checksum_type};
+                                 checksum_type, nullptr};
     return 0;
 }
 
@@ -315,6 +558,47 @@ int hdfs3_loopback_count_sink(void *user, const void *pkt, size_t len, const voi
     c[0] += 1;
     c[1] += len;
     c[2] += x & 1;  // keeps the loop
+    return 0;
+}
+
+/* write-side fault injection: mode 0 none, 1 refuse the pipeline setup (ERROR +
+ * firstBadLink = this node), 2 error status in the ack of `seqno`, 3 flip a data bit of
+ * packet `seqno` on arrival (the last node's verify then reports ERROR_CHECKSUM),
+ * 4 drop the connection instead of acking `seqno` */
+int hdfs3_loopback_set_write_fault(int port, int mode, int64_t seqno) {
+    Server *sv = find(port);
+    if (!sv) return -EINVAL;
+    sv->fault_seqno = seqno;
+    sv->write_fault = mode;
+    return 0;
+}
+
+/* packets and data bytes received by OP_WRITE_BLOCK, chunks that failed verification,
+ * blocks finalized */
+int hdfs3_loopback_write_stats(int port, uint64_t *packets, uint64_t *bytes, uint64_t *checksum_errors,
+                               uint64_t *finalized) {
+    Server *sv = find(port);
+    if (!sv) return -EINVAL;
+    if (packets) *packets = sv->write_packets;
+    if (bytes) *bytes = sv->write_bytes;
+    if (checksum_errors) *checksum_errors = sv->checksum_errors;
+    if (finalized) *finalized = sv->blocks_finalized;
+    return 0;
+}
+
+/* a block this node holds (served or written): pointers stay valid until the block is
+ * replaced or the node stops. 0, or -ENOENT */
+int hdfs3_loopback_get_block(int port, uint64_t block_id, const void **data, uint64_t *len, const void **crc_be,
+                             uint32_t *bpc) {
+    Server *sv = find(port);
+    if (!sv) return -EINVAL;
+    std::lock_guard<std::mutex> lk(sv->mu);
+    auto it = sv->blocks.find(block_id);
+    if (it == sv->blocks.end()) return -ENOENT;
+    if (data) *data = it->second.data;
+    if (len) *len = it->second.len;
+    if (crc_be) *crc_be = it->second.crc_be;
+    if (bpc) *bpc = it->second.bpc;
     return 0;
 }
 
