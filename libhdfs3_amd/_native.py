@@ -295,6 +295,7 @@ def loopback() -> ctypes.CDLL:
                               ("set_fail_after", [c_int, c_int64], c_int), ("served_bytes", [c_int], c_uint64),
                               ("requests", [c_int], c_uint64), ("last_status", [c_int], c_int),
                               ("stop", [c_int], c_int), ("set_write_fault", [c_int, c_int, c_int64], c_int),
+                              ("set_store_written", [c_int, c_int], c_int),
                               ("write_stats", [c_int] + [POINTER(c_uint64)] * 4, c_int),
                               ("get_block", [c_int, c_uint64, POINTER(c_void_p), POINTER(c_uint64), POINTER(c_void_p),
                                              POINTER(c_uint32)], c_int)]:

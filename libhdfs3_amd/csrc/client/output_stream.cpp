@@ -190,8 +190,10 @@ struct hdfs3_output_stream {
             ++packets;
             if (!error) {
                 const int rc = sink(user, pkt, size_t(kHeader) + 4ull * nch + p.data_len, &info);
-                if (rc) sticky(rc < 0 ? rc : -EIO, "Pipeline: the packet sink failed (seqno " +
-                                                       std::to_string(p.seqno) + ")");
+                if (rc)
+                    sticky(rc < 0 ? rc : -EIO, pipeline ? std::string(hdfs3_pipeline_error(pipeline))
+                                                        : "Pipeline: the packet sink failed (seqno " +
+                                                              std::to_string(p.seqno) + ")");
             }
         }
         b.pk.clear();

@@ -60,6 +60,9 @@ class LoopbackDatanode:
     def set_write_fault(self, mode: int, seqno: int = -1) -> None:
         assert self.lb.hdfs3_loopback_set_write_fault(self.port, mode, seqno) == 0
 
+    def set_store_written(self, store: bool) -> None:
+        assert self.lb.hdfs3_loopback_set_store_written(self.port, int(store)) == 0
+
     def write_stats(self) -> dict:
         v = [ctypes.c_uint64() for _ in range(4)]
         assert self.lb.hdfs3_loopback_write_stats(self.port, *[ctypes.byref(x) for x in v]) == 0

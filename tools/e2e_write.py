@@ -57,6 +57,8 @@ def pipeline_rate(data):
     total, bs = data.size, 128 << 20
     for n_nodes in (1, 3):
         nodes = [LoopbackDatanode() for _ in range(n_nodes)]
+        for d in nodes:  # verify + ack every packet, skip the in-memory copy (its page faults)
+            d.set_store_written(False)
         best = 0.0
         for rep in range(2):
             chain = [("127.0.0.1", d.port) for d in nodes]
@@ -69,6 +71,7 @@ def pipeline_rate(data):
                 dt = time.perf_counter() - t0
                 acked = pipe.stats()["block_bytes_acked"]
             assert acked == [bs] * len(blocks), acked
+            assert all(d.write_stats()["finalized"] == 0 for d in nodes)
             best = max(best, total / dt / 2**30)
         errs = sum(d.write_stats()["checksum_errors"] for d in nodes)
         for d in nodes:
@@ -76,7 +79,8 @@ def pipeline_rate(data):
         assert errs == 0
         print(json.dumps({"bench": "e2e_write", "mode": "hdfsWrite->pipeline", "nodes": n_nodes, "bytes": total,
                           "bpc": 512, "batch_packets": 64, "gib_s": round(best, 2),
-                          "note": "loopback datanodes in this process; the last node verifies on its CPU"}),
+                          "note": "loopback datanodes in this process; the last node verifies every word on its CPU "
+                                  "(SSE4.2); nodes do not keep the bytes (store off)"}),
               flush=True)
 
 

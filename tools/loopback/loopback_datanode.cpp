@@ -28,6 +28,8 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <thread>
@@ -56,33 +58,21 @@ struct Block {
 
 enum WriteFault : int { kNoFault = 0, kRefuseSetup = 1, kAckError = 2, kCorruptInTransit = 3, kDropAt = 4 };
 
-// the datanode's own CRC32C (slice-by-8 over the reflected polynomial 0x82F63B78), used to
+// the datanode's own CRC32C (SSE4.2 crc32q, the engine HDFS datanodes use on x86), used to
 // verify received packets; independent of the GPU path under test
 struct SwCrc32c {
-    uint32_t t[8][256];
-    SwCrc32c() {
-        for (uint32_t i = 0; i < 256; ++i) {
-            uint32_t c = i;
-            for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1)));
-            t[0][i] = c;
-        }
-        for (uint32_t i = 0; i < 256; ++i)
-            for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
-    }
-    uint32_t operator()(const uint8_t *p, size_t n) const {
-        uint32_t c = 0xFFFFFFFFu;
+    __attribute__((target("sse4.2"))) uint32_t operator()(const uint8_t *p, size_t n) const {
+        uint64_t c = 0xFFFFFFFFu;
         while (n >= 8) {
-            uint32_t lo, hi;
-            std::memcpy(&lo, p, 4);
-            std::memcpy(&hi, p + 4, 4);
-            lo ^= c;
-            c = t[7][lo & 0xFF] ^ t[6][(lo >> 8) & 0xFF] ^ t[5][(lo >> 16) & 0xFF] ^ t[4][lo >> 24] ^
-                t[3][hi & 0xFF] ^ t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
+            uint64_t w;
+            std::memcpy(&w, p, 8);
+            c = __builtin_ia32_crc32di(c, w);
             p += 8;
             n -= 8;
         }
-        while (n--) c = (c >> 8) ^ t[0][(c ^ *p++) & 0xFF];
-        return ~c;
+        uint32_t c32 = uint32_t(c);
+        while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+        return ~c32;
     }
 };
 const SwCrc32c g_crc;
@@ -104,6 +94,7 @@ struct Server {
     // write side
     std::atomic<int> write_fault{kNoFault};
     std::atomic<int64_t> fault_seqno{-1};
+    std::atomic<bool> store_written{true};  // false: verify + ack only (rate measurements)
     std::atomic<uint64_t> write_packets{0}, write_bytes{0}, checksum_errors{0}, blocks_finalized{0};
 };
 
@@ -280,7 +271,7 @@ void serve_write(Server *sv, int fd, const std::string &proto, int version, int 
                 broken = true;
                 return;
             }
-            if (it.last && ack.success()) {  // finalize: the block becomes readable
+            if (it.last && ack.success() && sv->store_written) {  // finalize: the block becomes readable
                 std::lock_guard<std::mutex> lk(sv->mu);
                 const uint64_t len = stored->data.size();
                 sv->blocks[req.block.block_id] =
@@ -328,7 +319,7 @@ void serve_write(Server *sv, int fd, const std::string &proto, int version, int 
                 }
             }
         if (fault == kAckError) status = wire::kError;
-        if (status == wire::kSuccess && h.data_len > 0) {
+        if (status == wire::kSuccess && h.data_len > 0 && sv->store_written) {
             // a re-sent partial chunk (after hflush) overwrites from offsetInBlock
             const uint64_t off = uint64_t(h.offset_in_block);
             if (off > stored->data.size() || off % bpc) {
@@ -469,6 +460,8 @@ void accept_loop(Server *sv) {
             if (sv->stop) return;
             continue;
         }
+        const int one = 1;  // acks are small writes: no Nagle delay behind the previous one
+        setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
         ++sv->active;
         std::thread([sv, fd] {
             serve(sv, fd);
@@ -570,6 +563,15 @@ int hdfs3_loopback_set_write_fault(int port, int mode, int64_t seqno) {
     if (!sv) return -EINVAL;
     sv->fault_seqno = seqno;
     sv->write_fault = mode;
+    return 0;
+}
+
+/* keep written blocks (default) or only verify and ack them: fresh-memory page faults of
+ * the in-memory store, not the client, bound a write-rate measurement otherwise */
+int hdfs3_loopback_set_store_written(int port, int store) {
+    Server *sv = find(port);
+    if (!sv) return -EINVAL;
+    sv->store_written = store != 0;
     return 0;
 }
 
