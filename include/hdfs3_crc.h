@@ -212,6 +212,37 @@ int hdfs3_crc32c_verify_packets_dev(hdfs3_crc_ctx *ctx, const void *d_arena, siz
  * fills each packet's CRC region in place. */
 int hdfs3_crc32c_compute_packets_dev(hdfs3_crc_ctx *ctx, void *d_arena, size_t arena_len,
                                      const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc);
+/* Asynchronous forms of the two calls above (readers with packet rings, a block scanner over a
+ * resident arena): one pass over pk[] on the host, descriptors staged in a ring slot of the
+ * ctx, nothing waits. *d_result (device, caller-zeroed) receives ~((packet << 32) | chunk) of
+ * the first bad chunk, 0 when clean (hdfs3_crc_decode_result returns the key). */
+int hdfs3_crc32c_verify_packets_dev_async(hdfs3_crc_ctx *ctx, const void *d_arena, size_t arena_len,
+                                          const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc, int check_short_tail,
+                                          uint64_t *d_result);
+int hdfs3_crc32c_compute_packets_dev_async(hdfs3_crc_ctx *ctx, void *d_arena, size_t arena_len,
+                                           const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc);
+
+/* A packet stream at one pitch — the layout of a received-packet ring and of the block
+ * reader's arenas: packet i's BE32 words at crc_off + i*pitch and its data at
+ * data_off + i*pitch, data_len bytes each except the last (last_len <= data_len).
+ * ONE launch with O(1) host work and no descriptor array: when data_len is a power-of-two
+ * number of 4 KiB rounds (64 KiB packets: 16) at bpc 512..4096 with 16-B aligned data, the
+ * wave kernel walks the packets directly; any other stream is expanded into
+ * descriptors once and takes the asynchronous descriptor path. Same result key; flags as
+ * hdfs3_crc32c_verify_dev_async_ex (HDFS3_LAUNCH_OVERLAP_PREVIOUS under the same contract). */
+typedef struct hdfs3_pkt_stream {
+    uint64_t crc_off;   /* packet 0's CRC region                        */
+    uint64_t data_off;  /* packet 0's data                              */
+    uint64_t pitch;     /* bytes from one packet to the next (> 0 if n > 1) */
+    uint64_t n;         /* packets                                      */
+    uint32_t data_len;  /* data bytes of every packet but the last      */
+    uint32_t last_len;  /* data bytes of the last packet                */
+} hdfs3_pkt_stream;
+int hdfs3_crc32c_verify_packet_stream_dev_async(hdfs3_crc_ctx *ctx, const void *d_arena, size_t arena_len,
+                                                const hdfs3_pkt_stream *ps, uint32_t bpc, int check_short_tail,
+                                                uint64_t *d_result, uint32_t flags);
+int hdfs3_crc32c_compute_packet_stream_dev_async(hdfs3_crc_ctx *ctx, void *d_arena, size_t arena_len,
+                                                 const hdfs3_pkt_stream *ps, uint32_t bpc);
 
 /* ---- streaming shim ---------------------------------------------------------
  * Checksum::update on a raw state (seed 0xFFFFFFFF = reset(), ~state = getValue()),

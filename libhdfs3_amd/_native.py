@@ -24,6 +24,13 @@ class Hdfs3CrcError(RuntimeError):
         self.rc = rc
 
 
+class PktStream(ctypes.Structure):
+    """hdfs3_pkt_stream (include/hdfs3_crc.h)."""
+
+    _fields_ = [("crc_off", c_uint64), ("data_off", c_uint64), ("pitch", c_uint64), ("n", c_uint64),
+                ("data_len", c_uint32), ("last_len", c_uint32)]
+
+
 class PktDesc(ctypes.Structure):
     """hdfs3_pkt_desc (include/hdfs3_crc.h)."""
 
@@ -68,6 +75,14 @@ PUBLIC_API = {
                                                 POINTER(c_int64)]),
     "hdfs3_crc32c_compute_packets_dev": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PktDesc),
                                                  c_size_t, c_uint32]),
+    "hdfs3_crc32c_verify_packets_dev_async": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PktDesc), c_size_t,
+                                                      c_uint32, c_int, c_void_p]),
+    "hdfs3_crc32c_compute_packets_dev_async": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PktDesc), c_size_t,
+                                                       c_uint32]),
+    "hdfs3_crc32c_verify_packet_stream_dev_async": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PktStream),
+                                                            c_uint32, c_int, c_void_p, c_uint32]),
+    "hdfs3_crc32c_compute_packet_stream_dev_async": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(PktStream),
+                                                             c_uint32]),
     "hdfs3_crc32c_update_host": (c_uint32, [c_uint32, c_void_p, c_size_t]),
     "hdfs3_dev_malloc": (c_int, [POINTER(c_void_p), c_size_t]),
     "hdfs3_dev_free": (c_int, [c_void_p]),

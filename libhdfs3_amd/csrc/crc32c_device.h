@@ -697,6 +697,13 @@ constexpr int kOptLineStore = 131072;
 //    each 8 rounds' 64 words into one VGPR (lane 8r + c = chunk c of round r) and keeps up
 //    to 8 such VGPRs (64 rounds), storing them only when full and at the end of its stream.
 constexpr int kOptHoldStore = 262144;
+//  kOptPitch: the rounds of a packet stream at a constant pitch (ChunkLaunch::pitch): round u
+//    is round u & (upp - 1) of packet u >> upp_log2, so a wave walks packets with two SALU ops
+//    per round more than a contiguous block, and the wire layout's per-packet CRC regions are
+//    read/written in place. Result keys are (packet << 32) | chunk. The packet API's constant-
+//    pitch streams (reader arenas, resident packet rings) take this instead of the segmented
+//    kernel.
+constexpr int kOptPitch = 524288;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -711,7 +718,23 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = lane % G;
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
-    const uint64_t nunits = a.len / kRoundBytes;
+    constexpr bool kPit = (OPT & kOptPitch) != 0;
+    const uint64_t nunits = kPit ? ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes : a.len / kRoundBytes;
+    // kPit: unit u -> (packet, round in packet); the contiguous case is packet 0 at pitch 0
+    const uint64_t umask = (uint64_t(1) << a.upp_log2) - 1;
+    auto unit_data = [&](uint64_t u) -> const uint8_t * {
+        if constexpr (kPit) return a.data + (u >> a.upp_log2) * a.pitch + (u & umask) * kRoundBytes;
+        return a.data + u * kRoundBytes;
+    };
+    // byte offset of chunk c of unit u's CRC word inside crc_be/out_be, and its result key
+    auto word_off = [&](uint64_t u, uint32_t c) -> uint64_t {
+        if constexpr (kPit) return (u >> a.upp_log2) * a.pitch + 4 * ((u & umask) * kChunksPerUnit + c);
+        return 4 * (u * kChunksPerUnit + c);
+    };
+    auto key_of = [&](uint64_t u, uint32_t c) -> uint64_t {
+        if constexpr (kPit) return ((u >> a.upp_log2) << 32) | ((u & umask) * kChunksPerUnit + c);
+        return a.chunk_base + u * kChunksPerUnit + c;
+    };
     const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
     // wave-uniform by construction; readfirstlane makes that provable to the compiler so
     // the end-of-stream prefetch guards below are scalar branches, not exec masks
@@ -749,7 +772,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             const uint64_t u = unit_of(k);
             return k < K && u < nunits ? a.data + u * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
         }
-        return k < K ? a.data + (first + k * stride) * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
+        return k < K ? unit_data(first + k * stride) : reinterpret_cast<const uint8_t *>(g_tab);
     };
 
     // TRACE (variant 13): lane 0 of each wave stamps entry, post-fill, post-first-step
@@ -851,8 +874,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                     reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, 4 * kChunksPerUnit, 0x00020000);
                 return __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (lane / G), 0, 0);
             }
-            const uint64_t chunk = (first + kk * stride) * kChunksPerUnit + lane / G;
-            return *reinterpret_cast<const uint32_t *>(a.crc_be + 4 * chunk);
+            return *reinterpret_cast<const uint32_t *>(a.crc_be + word_off(first + kk * stride, lane / G));
         }
         return 0;
     };
@@ -868,7 +890,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             if (uint32_t(i) < nheld) {
                 const uint64_t k = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
                 if (k < K)
-                    *reinterpret_cast<uint32_t *>(a.out_be + 4 * ((first + k * stride) * kChunksPerUnit + (lane & 7))) =
+                    *reinterpret_cast<uint32_t *>(a.out_be + word_off(first + k * stride, lane & 7)) =
                         __builtin_bswap32(~hold[i]);
             }
         }
@@ -903,18 +925,18 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             return;
         }
         if (k >= K || j != 0) return;
-        const uint64_t chunk = (first + k * stride) * kChunksPerUnit + lane / G;
+        const uint64_t u = first + k * stride;
         const uint32_t c = ~y;
         if constexpr (VERIFY) {
             const bool bad = (OPT & (kOptNoHbm | kOptNoFill | kOptNoMath | kOptFakeLut)) != 0 ? __builtin_bswap32(want) == ~c
                                                                                : __builtin_bswap32(want) != c;
-            if (bad) atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
+            if (bad) atomicMax(a.result, ~(unsigned long long)key_of(u, lane / G));
         } else if constexpr ((OPT & kOptNoStore) != 0) {
-            if (c == 0x9E3779B9u) *reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk) = c;
+            if (c == 0x9E3779B9u) *reinterpret_cast<uint32_t *>(a.out_be + word_off(u, lane / G)) = c;
         } else if constexpr ((OPT & kOptNtStore) != 0) {
-            __builtin_nontemporal_store(__builtin_bswap32(c), reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk));
+            __builtin_nontemporal_store(__builtin_bswap32(c), reinterpret_cast<uint32_t *>(a.out_be + word_off(u, lane / G)));
         } else {
-            *reinterpret_cast<uint32_t *>(a.out_be + 4 * chunk) = __builtin_bswap32(c);
+            *reinterpret_cast<uint32_t *>(a.out_be + word_off(u, lane / G)) = __builtin_bswap32(c);
         }
     };
     // word i (0..15) of the lane's 64-byte segment after regroup
@@ -1028,21 +1050,26 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     if constexpr (kHold) flush();
     stamp(3);
 
-    // slow region: chunks after the last whole round, plus the short tail chunk
-    const uint64_t nfull = a.len / BPC;
-    const uint64_t first_slow = nunits * kChunksPerUnit;
-    const uint64_t nslow = nfull - first_slow + (a.len % BPC ? 1 : 0);
+    // slow region: chunks after the last whole round, plus the short tail chunk (kPit: of the
+    // last packet, the only one that may end inside a round)
+    const uint64_t len = kPit ? a.last_len : a.len;
+    const uint8_t *sdata = kPit ? a.data + (a.npk - 1) * a.pitch : a.data;
+    const uint64_t soff = kPit ? (a.npk - 1) * a.pitch : 0;  // of the slow chunks' words
+    const uint64_t skey = kPit ? (a.npk - 1) << 32 : a.chunk_base;
+    const uint64_t nfull = len / BPC;
+    const uint64_t first_slow = (len / kRoundBytes) * kChunksPerUnit;
+    const uint64_t nslow = nfull - first_slow + (len % BPC ? 1 : 0);
     const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
     const bool crc_al4 = (reinterpret_cast<uintptr_t>(VERIFY ? a.crc_be : a.out_be) & 3u) == 0;
     if (gtid < nslow) {
         const uint64_t chunk = first_slow + gtid;
-        const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(a.len % BPC);
-        const uint32_t c = ~crc_run_lines(t, 0xFFFFFFFFu, a.data + chunk * BPC, sz);
+        const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(len % BPC);
+        const uint32_t c = ~crc_run_lines(t, 0xFFFFFFFFu, sdata + chunk * BPC, sz);
         if constexpr (VERIFY) {
-            if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(a.crc_be + 4 * chunk, crc_al4) != c)
-                atomicMax(a.result, ~(unsigned long long)(a.chunk_base + chunk));
+            if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(a.crc_be + soff + 4 * chunk, crc_al4) != c)
+                atomicMax(a.result, ~(unsigned long long)(skey + chunk));
         } else {
-            store_be32(a.out_be + 4 * chunk, c, crc_al4);
+            store_be32(a.out_be + soff + 4 * chunk, c, crc_al4);
         }
     }
 }
@@ -1706,9 +1733,11 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         constexpr int G = BPC / 64;
         constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
         const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
-        const uint64_t units = a.len / kRoundBytes;
+        const uint64_t units = (OPT & kOptPitch) != 0 ? ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes
+                                                      : a.len / kRoundBytes;
         const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
-        const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
+        int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
+        if (grid < 1) grid = 1;
         if (ANY_ORDER || a.overlap_previous)  // AQL packet without the barrier bit (variant 16, opt-in flag)
             hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
                                   dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);

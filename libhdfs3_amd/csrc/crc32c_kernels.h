@@ -28,6 +28,14 @@ struct ChunkLaunch {
     // (crc32c_block.h) builds all its tables from these, with no table loads
     uint32_t poly = 0;
     const uint32_t *fold_host = nullptr;
+    // Packet stream at a constant pitch (kOptPitch, launch_packet_stream): packet i's data at
+    // data + i*pitch, its BE32 words at crc_be/out_be + i*pitch; every packet but the last holds
+    // exactly 1 << upp_log2 whole 4 KiB rounds, the last one last_len <= that many bytes. len is
+    // unused; result keys are (packet << 32) | chunk.
+    uint64_t pitch = 0;
+    uint64_t npk = 0;
+    uint32_t upp_log2 = 0;
+    uint32_t last_len = 0;
 };
 
 // Packet-descriptor as seen by the device (mirrors hdfs3_pkt_desc).
@@ -68,10 +76,18 @@ constexpr uint32_t kMaxInlineSegments = 16;
 // h_stage/d_stage are pinned/device staging for n DevSegments. Uses the segmented wave
 // kernel when segments_fast() holds, else the chunk-per-lane packet kernel. Keys are
 // (packet << 32 | chunk).
+// constant-pitch packet streams (ChunkLaunch::pitch): whether the wave kernel's pitch mode
+// takes them (bpc 512..4096, aligned, every packet but the last a power-of-two number of
+// whole rounds), and its launcher (a.pitch/npk/upp_log2/last_len set)
+bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32_t bpc, const void *data,
+                      const void *crc, uint64_t pitch, uint32_t *upp_log2);
+hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
+                                int grid_cap, hipStream_t stream);
 hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
-                               hipStream_t stream);
+                               hipStream_t stream, uint64_t arena_len = 0, size_t *bad_index = nullptr,
+                               bool overlap_previous = false);
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream);

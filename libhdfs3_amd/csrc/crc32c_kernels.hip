@@ -40,7 +40,53 @@ hipError_t launch_rv(const ChunkLaunch &a, bool verify, const uint32_t *tab, con
                   : launch_r<BPC, false>(a, tab, fold, grid_cap, s);
 }
 
+// packet streams at a constant pitch: the production wave kernel with kOptPitch
+template <int BPC, bool V>
+hipError_t launch_p(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
+    constexpr int kOpt = kOptLeanFill | kOptPitch | (!V && BPC == 512 ? kOptHoldStore : 0);
+    if (a.overlap_previous)
+        return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
+    return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
+}
+
+template <int BPC>
+hipError_t launch_pv(const ChunkLaunch &a, bool verify, const uint32_t *tab, const uint32_t *fold, int grid_cap,
+                     hipStream_t s) {
+    return verify ? launch_p<BPC, true>(a, tab, fold, grid_cap, s) : launch_p<BPC, false>(a, tab, fold, grid_cap, s);
+}
+
 }  // namespace
+
+bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32_t bpc, const void *data,
+                      const void *crc, uint64_t pitch, uint32_t *upp_log2) {
+    if (bpc != 512 && bpc != 1024 && bpc != 2048 && bpc != 4096) return false;
+    if (npk == 0 || data_len == 0 || data_len % kRoundBytes || last_len > data_len) return false;
+    if (npk > 1 && pitch == 0) return false;
+    if (npk >= (uint64_t(1) << 31)) return false;  // keys are (packet << 32) | chunk
+    if ((reinterpret_cast<uintptr_t>(data) & 15u) || (reinterpret_cast<uintptr_t>(crc) & 3u) || (pitch & 15u))
+        return false;
+    const uint64_t upp = data_len / kRoundBytes;
+    if (upp & (upp - 1)) return false;  // rounds per packet: a power of two (64 KiB packets: 16)
+    if (((npk - 1) * upp + last_len / kRoundBytes) == 0) return false;
+    uint32_t l = 0;
+    while ((uint64_t(1) << l) < upp) ++l;
+    *upp_log2 = l;
+    return true;
+}
+
+hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
+                                int grid_cap, hipStream_t stream) {
+#if HDFS3_LAB
+    if (g_variant == 52 || g_variant == 53) return hipErrorNotSupported;  // A/B: force the segmented kernel
+#endif
+    switch (a.bpc) {
+    case 512: return launch_pv<512>(a, verify, d_tables, d_fold, grid_cap, stream);
+    case 1024: return launch_pv<1024>(a, verify, d_tables, d_fold, grid_cap, stream);
+    case 2048: return launch_pv<2048>(a, verify, d_tables, d_fold, grid_cap, stream);
+    case 4096: return launch_pv<4096>(a, verify, d_tables, d_fold, grid_cap, stream);
+    default: return hipErrorInvalidValue;
+    }
+}
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream) {
@@ -171,7 +217,7 @@ hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t unit
 hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
-                               hipStream_t stream) {
+                               hipStream_t stream, uint64_t arena_len, size_t *bad_index, bool overlap_previous) {
     if (n == 0) return hipSuccess;
     // one pass: descriptors, the alignment test of segments_fast and the unit plan of
     // plan_segments (16K packets per GiB: the host loop is on the call's critical path)
@@ -181,8 +227,17 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
     // constant pitch: packet i at data_off[0] + i*S, crc_off[0] + i*S, one data length
     // (the last may be shorter) -> the kernel derives every descriptor (SegLaunch::stride)
     const uint64_t pitch = n > 1 ? h_pk[1].data_off - h_pk[0].data_off : 0;
-    bool strided = n > kInlineSegments && g_variant != 52 && pitch > 0 && pitch == h_pk[1].crc_off - h_pk[0].crc_off;
+    bool strided = n > 1 && g_variant != 52 && pitch > 0 && pitch == h_pk[1].crc_off - h_pk[0].crc_off;
     for (size_t i = 0; i < n; ++i) {
+        if (arena_len) {  // bounds, fused into this pass (the API's only pass over pk[])
+            const hdfs3crc::DevPacket &d = h_pk[i];
+            const uint64_t chunks = (uint64_t(d.data_len) + bpc - 1) / bpc;
+            if (d.data_off > arena_len || d.data_len > arena_len - d.data_off || d.crc_off > arena_len ||
+                4 * chunks > arena_len - d.crc_off) {
+                if (bad_index) *bad_index = i;
+                return hipErrorInvalidValue;
+            }
+        }
         const uint8_t *data = d_arena + h_pk[i].data_off;
         const uint8_t *crc = d_arena + h_pk[i].crc_off;
         const uint64_t u = h_pk[i].data_len / kRoundBytes;
@@ -193,7 +248,26 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
                   (i + 1 == n || h_pk[i].data_len == h_pk[0].data_len);
         units += u;
     }
-    if (fast && strided && same && u0 > 0) {
+    uint32_t upp_log2 = 0;
+    if (fast && strided && n > 1 &&
+        packet_stream_ok(h_pk[0].data_len, h_pk[n - 1].data_len, n, bpc, d_arena + h_pk[0].data_off,
+                         d_arena + h_pk[0].crc_off, pitch, &upp_log2)) {
+        ChunkLaunch a{};
+        a.data = d_arena + h_pk[0].data_off;
+        a.crc_be = d_arena + h_pk[0].crc_off;
+        a.out_be = const_cast<uint8_t *>(d_arena) + h_pk[0].crc_off;
+        a.bpc = bpc;
+        a.result = result;
+        a.check_short_tail = check_short_tail;
+        a.pitch = pitch;
+        a.npk = n;
+        a.upp_log2 = upp_log2;
+        a.last_len = h_pk[n - 1].data_len;
+        a.overlap_previous = overlap_previous && verify;
+        const hipError_t e = launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream);
+        if (e != hipErrorNotSupported) return e;
+    }
+    if (fast && strided && same && u0 > 0 && n > kInlineSegments) {
         const DevSegment ends[2] = {
             DevSegment{d_arena + h_pk[0].data_off, const_cast<uint8_t *>(d_arena) + h_pk[0].crc_off,
                        h_pk[0].data_len, 0, 0},

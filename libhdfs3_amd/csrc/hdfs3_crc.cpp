@@ -242,27 +242,37 @@ static_assert(sizeof(hdfs3_pkt_desc) == sizeof(DevPacket) && offsetof(hdfs3_pkt_
                   offsetof(hdfs3_pkt_desc, data_len) == offsetof(DevPacket, data_len),
               "the packets API hands descriptors to the kernels unconverted");
 
+int stage_segments(hdfs3_crc_ctx *ctx, size_t n, hdfs3_crc_ctx::SegStage **out);
+
+// One launch over n packets, nothing waited for: a single host pass over pk[] (bounds, layout
+// detection, descriptors into a staging slot of the ctx's ring, which is reused only after its
+// launch ran). Constant-pitch streams of whole-round packets take the wave kernel's pitch mode
+// with no descriptor copy at all.
+int packets_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len, const hdfs3_pkt_desc *pk, size_t n,
+                  uint32_t bpc, bool verify, int check_short_tail, unsigned long long *d_result, bool overlap) {
+    // the result key is (packet << 32 | chunk)
+    if (n >= (size_t(1) << 31)) return fail(-EINVAL, "too many packets in one batch");
+    hdfs3_crc_ctx::SegStage *st = nullptr;
+    if (int rc = stage_segments(ctx, n, &st)) return rc;
+    // hdfs3_pkt_desc and DevPacket share one layout (asserted above): no conversion copy
+    const DevPacket *hp = reinterpret_cast<const DevPacket *>(pk);
+    size_t bad = 0;
+    const hipError_t e = launch_packet_batch(d_arena, hp, n, bpc, verify, check_short_tail, d_result, st->h, st->d,
+                                             ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream,
+                                             arena_len ? arena_len : 1, &bad, overlap);
+    if (e == hipErrorInvalidValue) return fail(-EINVAL, "packet %zu lies outside the %zu-byte arena", bad, arena_len);
+    HIP_TRY(e);
+    ++ctx->launches;
+    HIP_TRY(hipEventRecord(st->done, ctx->stream));
+    return 0;
+}
+
 int packets_common(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len,
                    const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc, bool verify,
                    int check_short_tail, int64_t *bad_packet, int64_t *bad_chunk) {
-    // the result key is (packet << 32 | chunk)
-    if (n >= (size_t(1) << 31)) return fail(-EINVAL, "too many packets in one batch");
-    for (size_t i = 0; i < n; ++i) {
-        const hdfs3_pkt_desc &d = pk[i];
-        const uint64_t chunks = (uint64_t(d.data_len) + bpc - 1) / bpc;
-        if (d.data_off > arena_len || d.data_len > arena_len - d.data_off ||
-            d.crc_off > arena_len || 4 * chunks > arena_len - d.crc_off)
-            return fail(-EINVAL, "packet %zu lies outside the %zu-byte arena", i, arena_len);
-    }
-    if (int rc = grow_pk(ctx, n)) return rc;
-    // the previous call's descriptors may still be in flight from h_pk
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    // hdfs3_pkt_desc and DevPacket share one layout (asserted below): no conversion copy
-    const DevPacket *hp = reinterpret_cast<const DevPacket *>(pk);
     if (verify) HIP_TRY(hipMemsetAsync(ctx->d_result, 0, sizeof(unsigned long long), ctx->stream));
-    HIP_TRY(launch_packet_batch(d_arena, hp, n, bpc, verify, check_short_tail, ctx->d_result, ctx->h_pk,
-                                ctx->d_pk, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
-    ++ctx->launches;
+    if (int rc = packets_async(ctx, d_arena, arena_len, pk, n, bpc, verify, check_short_tail, ctx->d_result, false))
+        return rc;
     if (verify) {
         HIP_TRY(hipMemcpyAsync(ctx->h_result, ctx->d_result, sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, ctx->stream));
@@ -275,6 +285,51 @@ int packets_common(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len,
         if (bad_chunk) *bad_chunk = r ? int64_t(key & 0xFFFFFFFFu) : -1;
     }
     return 0;
+}
+
+// hdfs3_pkt_stream: O(1) host work when the wave kernel's pitch mode takes the stream, else
+// the descriptors are generated (once) and go through packets_async
+int packet_stream_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len, const hdfs3_pkt_stream *ps,
+                        uint32_t bpc, bool verify, int check_short_tail, unsigned long long *d_result, bool overlap) {
+    if (ps->n == 0) return 0;
+    if (ps->n >= (uint64_t(1) << 31)) return fail(-EINVAL, "too many packets in one stream");
+    if (ps->last_len > ps->data_len) return fail(-EINVAL, "last_len above data_len");
+    // bounds: the first and the last packet delimit the stream (pitch >= 0, offsets grow)
+    const uint64_t last = ps->n - 1;
+    const uint64_t lchunks = (uint64_t(ps->last_len) + bpc - 1) / bpc, chunks = (uint64_t(ps->data_len) + bpc - 1) / bpc;
+    const unsigned __int128 ld = (unsigned __int128)ps->data_off + (unsigned __int128)last * ps->pitch;
+    const unsigned __int128 lc = (unsigned __int128)ps->crc_off + (unsigned __int128)last * ps->pitch;
+    if (ps->data_off + uint64_t(ps->n > 1 ? ps->data_len : ps->last_len) > arena_len || ld + ps->last_len > arena_len ||
+        ps->crc_off + 4 * (ps->n > 1 ? chunks : lchunks) > arena_len || lc + 4 * lchunks > arena_len ||
+        (ps->n > 1 && ps->pitch == 0))
+        return fail(-EINVAL, "the packet stream does not fit the %zu-byte arena", arena_len);
+    uint32_t upp_log2 = 0;
+    if (packet_stream_ok(ps->data_len, ps->last_len, ps->n, bpc, d_arena + ps->data_off, d_arena + ps->crc_off,
+                         ps->pitch, &upp_log2)) {
+        ChunkLaunch a{};
+        a.data = d_arena + ps->data_off;
+        a.crc_be = d_arena + ps->crc_off;
+        a.out_be = const_cast<uint8_t *>(d_arena) + ps->crc_off;
+        a.bpc = bpc;
+        a.result = d_result;
+        a.check_short_tail = check_short_tail;
+        a.pitch = ps->pitch;
+        a.npk = ps->n;
+        a.upp_log2 = upp_log2;
+        a.last_len = ps->last_len;
+        a.overlap_previous = overlap && verify;
+        const hipError_t e = launch_packet_stream(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream);
+        if (e != hipErrorNotSupported) {
+            HIP_TRY(e);
+            ++ctx->launches;
+            return 0;
+        }
+    }
+    std::vector<hdfs3_pkt_desc> pk(ps->n);
+    for (uint64_t i = 0; i < ps->n; ++i)
+        pk[i] = hdfs3_pkt_desc{ps->data_off + i * ps->pitch, ps->crc_off + i * ps->pitch,
+                               i == last ? ps->last_len : ps->data_len, 0};
+    return packets_async(ctx, d_arena, arena_len, pk.data(), pk.size(), bpc, verify, check_short_tail, d_result, false);
 }
 
 // a descriptor staging slot of the blocks API, reusable once its previous launch ran
@@ -674,6 +729,51 @@ int hdfs3_crc32c_compute_packets_dev(hdfs3_crc_ctx *ctx, void *d_arena, size_t a
     DeviceGuard g(ctx->device);
     return packets_common(ctx, static_cast<const uint8_t *>(d_arena), arena_len, pk, n, bpc, false,
                           0, nullptr, nullptr);
+}
+
+int hdfs3_crc32c_verify_packets_dev_async(hdfs3_crc_ctx *ctx, const void *d_arena, size_t arena_len,
+                                          const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc, int check_short_tail,
+                                          uint64_t *d_result) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (n == 0) return 0;
+    if (!d_arena || !pk || !d_result) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    return packets_async(ctx, static_cast<const uint8_t *>(d_arena), arena_len, pk, n, bpc, true, check_short_tail,
+                         reinterpret_cast<unsigned long long *>(d_result), false);
+}
+
+int hdfs3_crc32c_compute_packets_dev_async(hdfs3_crc_ctx *ctx, void *d_arena, size_t arena_len,
+                                           const hdfs3_pkt_desc *pk, size_t n, uint32_t bpc) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (n == 0) return 0;
+    if (!d_arena || !pk) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    return packets_async(ctx, static_cast<const uint8_t *>(d_arena), arena_len, pk, n, bpc, false, 0, nullptr, false);
+}
+
+int hdfs3_crc32c_verify_packet_stream_dev_async(hdfs3_crc_ctx *ctx, const void *d_arena, size_t arena_len,
+                                                const hdfs3_pkt_stream *ps, uint32_t bpc, int check_short_tail,
+                                                uint64_t *d_result, uint32_t flags) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (flags & ~HDFS3_LAUNCH_OVERLAP_PREVIOUS) return fail(-EINVAL, "unknown launch flags 0x%x", flags);
+    if (!ps) return fail(-EINVAL, "null stream");
+    if (ps->n == 0) return 0;
+    if (!d_arena || !d_result) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    return packet_stream_async(ctx, static_cast<const uint8_t *>(d_arena), arena_len, ps, bpc, true, check_short_tail,
+                               reinterpret_cast<unsigned long long *>(d_result),
+                               (flags & HDFS3_LAUNCH_OVERLAP_PREVIOUS) != 0);
+}
+
+int hdfs3_crc32c_compute_packet_stream_dev_async(hdfs3_crc_ctx *ctx, void *d_arena, size_t arena_len,
+                                                 const hdfs3_pkt_stream *ps, uint32_t bpc) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (!ps) return fail(-EINVAL, "null stream");
+    if (ps->n == 0) return 0;
+    if (!d_arena) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    return packet_stream_async(ctx, static_cast<const uint8_t *>(d_arena), arena_len, ps, bpc, false, 0, nullptr,
+                               false);
 }
 
 uint32_t hdfs3_crc32c_update_host(uint32_t state, const void *p, size_t len) {

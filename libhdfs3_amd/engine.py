@@ -17,7 +17,7 @@ from ctypes import byref, c_int, c_int64, c_void_p
 import numpy as np
 
 from . import _native
-from ._native import PktDesc, check
+from ._native import Hdfs3CrcError, PktDesc, check  # noqa: F401 (Hdfs3CrcError re-exported)
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -235,6 +235,33 @@ class CrcContext:
         d = self._descs(pk)
         self._check("hdfs3_crc32c_compute_packets_dev",
               self._lib.hdfs3_crc32c_compute_packets_dev(self.ctx, d_arena, arena_len, d, len(pk), bpc))
+
+    def verify_packets_dev_async(self, d_arena: int, arena_len: int, pk, bpc: int, d_result: int,
+                                 check_short_tail: bool = False) -> None:
+        self._check("hdfs3_crc32c_verify_packets_dev_async",
+              self._lib.hdfs3_crc32c_verify_packets_dev_async(self.ctx, d_arena, arena_len, self._descs(pk), len(pk),
+                                                              bpc, int(check_short_tail), d_result))
+
+    def compute_packets_dev_async(self, d_arena: int, arena_len: int, pk, bpc: int) -> None:
+        self._check("hdfs3_crc32c_compute_packets_dev_async",
+              self._lib.hdfs3_crc32c_compute_packets_dev_async(self.ctx, d_arena, arena_len, self._descs(pk), len(pk),
+                                                               bpc))
+
+    @staticmethod
+    def packet_stream(crc_off: int, data_off: int, pitch: int, n: int, data_len: int, last_len: int | None = None):
+        """hdfs3_pkt_stream: packet i's words at crc_off + i*pitch, data at data_off + i*pitch."""
+        return _native.PktStream(crc_off, data_off, pitch, n, data_len, data_len if last_len is None else last_len)
+
+    def verify_packet_stream_async(self, d_arena: int, arena_len: int, ps, bpc: int, d_result: int,
+                                   check_short_tail: bool = False, overlap_previous: bool = False) -> None:
+        self._check("hdfs3_crc32c_verify_packet_stream_dev_async",
+              self._lib.hdfs3_crc32c_verify_packet_stream_dev_async(self.ctx, d_arena, arena_len, byref(ps), bpc,
+                                                                    int(check_short_tail), d_result,
+                                                                    1 if overlap_previous else 0))
+
+    def compute_packet_stream_async(self, d_arena: int, arena_len: int, ps, bpc: int) -> None:
+        self._check("hdfs3_crc32c_compute_packet_stream_dev_async",
+              self._lib.hdfs3_crc32c_compute_packet_stream_dev_async(self.ctx, d_arena, arena_len, byref(ps), bpc))
 
 
 def block_checksum_crcs(crc_be: bytes | np.ndarray) -> bytes:

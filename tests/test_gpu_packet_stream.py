@@ -1,0 +1,175 @@
+"""GPU parity of packet streams at a constant pitch (hdfs3_pkt_stream, the asynchronous packet
+APIs, and the wave kernel's pitch mode that serves them): every (packet, chunk) result key and
+every computed word must equal the oracle's, for whole-round packets (pitch mode), packets the
+pitch mode does not take (65024-byte writer packets, other bpc: descriptor fallback), short
+last packets with remote/local tail semantics, and chained overlapped launches."""
+import numpy as np
+import pytest
+
+from util import oracle_compute, oracle_verify, splitmix_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+def build_arena(n, plen, last_len, bpc, seed, gap=32):
+    """[gap][words][data] per packet at one pitch (data 16 B aligned when gap + words is)."""
+    crc_bytes = 4 * (-(-plen // bpc))
+    pitch = gap + crc_bytes + plen
+    pitch += (-pitch) % 16
+    arena = np.zeros(n * pitch + 64, np.uint8)
+    datas = []
+    for i in range(n):
+        dl = plen if i + 1 < n else last_len
+        data = splitmix_bytes(dl, seed + i)
+        crc = oracle_compute(data, bpc)
+        crc_off = i * pitch + gap
+        arena[crc_off:crc_off + crc.nbytes] = crc
+        arena[crc_off + crc_bytes:crc_off + crc_bytes + dl] = data
+        datas.append(data)
+    return arena, pitch, gap, gap + crc_bytes, datas
+
+
+def oracle_key(datas, arena, pitch, crc_off, bpc, local):
+    for i, d in enumerate(datas):
+        words = arena[i * pitch + crc_off:i * pitch + crc_off + 4 * (-(-d.size // bpc))]
+        c = oracle_verify(d, bpc, words, local)
+        if c >= 0:
+            return i, c
+    return -1, -1
+
+
+def run_stream(ctx, d, nbytes, ps, bpc, local):
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    res = DeviceBuffer(8)
+    ctx.memset(res, 0, 8)
+    ctx.verify_packet_stream_async(d.ptr, nbytes, ps, bpc, res.ptr, local)
+    w = int(ctx.download(res, 8).view(np.uint64)[0])
+    if w == 0:
+        return -1, -1
+    key = ctx.decode_result(w)
+    return key >> 32, key & 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("bpc", [512, 1024, 2048, 4096])
+@pytest.mark.parametrize("plen,last", [(65536, 65536), (65536, 65536 - 300), (65536, 4096 * 3 + 1), (65536, 100),
+                                       (131072, 131072 - 7), (4096, 4096), (65024, 65024 - 11), (65536 + 512, 700)])
+def test_packet_stream_matches_oracle(gpu_ctx, bpc, plen, last):
+    from libhdfs3_amd.engine import CrcContext
+
+    n = 24
+    arena, pitch, crc_off, data_off, datas = build_arena(n, plen, last, bpc, 100 + bpc + plen % 997)
+    d = gpu_ctx.upload(arena)
+    ps = CrcContext.packet_stream(crc_off, data_off, pitch, n, plen, last)
+    for local in (False, True):
+        assert run_stream(gpu_ctx, d, arena.nbytes, ps, bpc, local) == (-1, -1)
+    rng = np.random.default_rng(bpc * 7 + plen)
+    for p, q in [(0, 0), (n - 1, last - 1), (int(rng.integers(0, n)), None)]:
+        q = int(rng.integers(0, datas[p].size)) if q is None else q
+        bad = arena.copy()
+        bad[p * pitch + data_off + q] ^= 0x04
+        gpu_ctx.upload(bad, d)
+        for local in (False, True):
+            want = oracle_key([np.frombuffer(bad[i * pitch + data_off:i * pitch + data_off + datas[i].size], np.uint8)
+                               for i in range(n)], bad, pitch, crc_off, bpc, local)
+            assert run_stream(gpu_ctx, d, arena.nbytes, ps, bpc, local) == want, (p, q, local)
+    # compute: every region rewritten with the oracle's words
+    blank = arena.copy()
+    for i in range(n):
+        blank[i * pitch + crc_off:i * pitch + data_off] = 0
+    gpu_ctx.upload(blank, d)
+    gpu_ctx.compute_packet_stream_async(d.ptr, arena.nbytes, ps, bpc)
+    assert np.array_equal(gpu_ctx.download(d, arena.nbytes), arena)
+
+
+def test_descriptor_async_equals_sync(gpu_ctx):
+    """hdfs3_crc32c_{verify,compute}_packets_dev_async: same keys and words as the sync calls,
+    for a ragged (non-constant-pitch) descriptor list."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    bpc = 512
+    sizes = [65536, 300, 65536 * 2, 4096 * 5 + 17, 512, 65536]
+    arena = np.zeros(sum(s + 4 * (-(-s // bpc)) + 48 for s in sizes), np.uint8)
+    pk, off = [], 16
+    for i, s in enumerate(sizes):
+        data = splitmix_bytes(s, 900 + i)
+        crc = oracle_compute(data, bpc)
+        arena[off:off + crc.nbytes] = crc
+        doff = off + crc.nbytes
+        doff += (-doff) % 16
+        arena[doff:doff + s] = data
+        pk.append((doff, off, s))
+        off = doff + s + 16
+    d = gpu_ctx.upload(arena)
+    res = DeviceBuffer(8)
+    for flip in (None, (3, 4096 * 2 + 5), (5, 65535)):
+        a = arena.copy()
+        if flip:
+            a[pk[flip[0]][0] + flip[1]] ^= 1
+        gpu_ctx.upload(a, d)
+        sync = gpu_ctx.verify_packets_dev(d.ptr, a.nbytes, pk, bpc, True)
+        gpu_ctx.memset(res, 0, 8)
+        gpu_ctx.verify_packets_dev_async(d.ptr, a.nbytes, pk, bpc, res.ptr, True)
+        w = int(gpu_ctx.download(res, 8).view(np.uint64)[0])
+        key = gpu_ctx.decode_result(w) if w else -1
+        got = (key >> 32, key & 0xFFFFFFFF) if w else (-1, -1)
+        assert got == sync == ((flip[0], flip[1] // bpc) if flip else (-1, -1))
+    blank = arena.copy()
+    for doff, coff, s in pk:
+        blank[coff:coff + 4 * (-(-s // bpc))] = 0
+    gpu_ctx.upload(blank, d)
+    gpu_ctx.compute_packets_dev_async(d.ptr, arena.nbytes, pk, bpc)
+    assert np.array_equal(gpu_ctx.download(d, arena.nbytes), arena)
+
+
+def test_stream_bounds_rejected(gpu_ctx):
+    from libhdfs3_amd.engine import CrcContext, DeviceBuffer, Hdfs3CrcError
+
+    arena, pitch, crc_off, data_off, _ = build_arena(4, 65536, 65536, 512, 5)
+    d = gpu_ctx.upload(arena)
+    res = DeviceBuffer(8)
+    ps = CrcContext.packet_stream(crc_off, data_off, pitch, 5, 65536, 65536)  # one packet too many
+    with pytest.raises(Hdfs3CrcError):
+        gpu_ctx.verify_packet_stream_async(d.ptr, arena.nbytes, ps, 512, res.ptr)
+    ps = CrcContext.packet_stream(crc_off, data_off, pitch, 4, 65536, 70000)  # last above data_len
+    with pytest.raises(Hdfs3CrcError):
+        gpu_ctx.verify_packet_stream_async(d.ptr, arena.nbytes, ps, 512, res.ptr)
+
+
+def test_overlapped_stream_chain_and_large_stream(gpu_ctx):
+    """256 MiB of 64 KiB packets: compute -> verify round trip, then 24 chained overlapped
+    verifies (HDFS3_LAUNCH_OVERLAP_PREVIOUS) over four resident arenas, one corrupted, each
+    into its own result word: every word reports exactly its arena's first bad key.
+    (No torch here: this process initialised HIP through the library first.)"""
+    from libhdfs3_amd.engine import CrcContext, DeviceBuffer
+
+    n, plen, bpc = 4096, 65536, 512
+    pitch = 512 + plen + 16
+    crc_off, data_off = 16, 16 + 512
+    host = np.random.default_rng(77).integers(0, 256, size=n * pitch, dtype=np.uint8)
+    arenas = [DeviceBuffer(n * pitch) for _ in range(4)]
+    ps = CrcContext.packet_stream(crc_off, data_off, pitch, n, plen)
+    for a in arenas:
+        gpu_ctx.upload(host, a)
+        gpu_ctx.compute_packet_stream_async(a.ptr, n * pitch, ps, bpc)
+    gpu_ctx.synchronize()
+    got = gpu_ctx.download(arenas[0], n * pitch)
+    for p in (0, n // 2, n - 1):
+        blob = got[p * pitch:(p + 1) * pitch]
+        assert np.array_equal(blob[crc_off:crc_off + 512], oracle_compute(blob[data_off:data_off + plen], bpc))
+    p_bad, q_bad = 3001, 40000
+    flipped = got[p_bad * pitch + data_off + q_bad:p_bad * pitch + data_off + q_bad + 1] ^ np.uint8(0x10)
+    gpu_ctx.upload(flipped, arenas[2], offset=p_bad * pitch + data_off + q_bad)
+    res = DeviceBuffer(24 * 8)
+    gpu_ctx.memset(res, 0, 24 * 8)
+    for i in range(24):
+        a = arenas[i % 4]
+        gpu_ctx.verify_packet_stream_async(a.ptr, n * pitch, ps, bpc, res.ptr + 8 * i, overlap_previous=i > 0)
+    gpu_ctx.synchronize()
+    words = gpu_ctx.download(res, 24 * 8).view(np.uint64).tolist()
+    for i, w in enumerate(words):
+        if i % 4 == 2:
+            key = gpu_ctx.decode_result(int(w))
+            assert (key >> 32, key & 0xFFFFFFFF) == (p_bad, q_bad // bpc), i
+        else:
+            assert w == 0, i

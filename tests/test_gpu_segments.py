@@ -176,9 +176,10 @@ def test_single_segment_batch(lab_ctx, bpc, variant):
 @pytest.mark.parametrize("bpc", [512, 4096])
 @pytest.mark.parametrize("last_len", [65536, 65536 - 300, 100])
 def test_constant_pitch_packets_without_descriptors(lab_ctx, bpc, last_len):
-    """Packets at one pitch in one arena (the reader's and writer's layout) go to the
-    segmented kernel with no descriptor array (SegLaunch::stride). Same keys and words as
-    with descriptors (A/B variant 52) and as the packet kernel (variant 17)."""
+    """Packets at one pitch in one arena (the reader's and writer's layout) go to the wave
+    kernel's pitch mode (variant 0) with no descriptor array. Same keys and words as the
+    segmented kernel's strided launch (A/B variant 53), with descriptors (variant 52) and as
+    the packet kernel (variant 17)."""
     from libhdfs3_amd import _native
 
     lib = _native.lab()
@@ -200,7 +201,7 @@ def test_constant_pitch_packets_without_descriptors(lab_ctx, bpc, last_len):
         pk.append((data_off, crc_off, dl))
     d = lab_ctx.upload(arena)
     try:
-        for v in (0, 52, 17):
+        for v in (0, 53, 52, 17):
             lib.hdfs3x_set_variant(v)
             assert lab_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True) == (-1, -1), v
         for _ in range(3):
@@ -210,14 +211,14 @@ def test_constant_pitch_packets_without_descriptors(lab_ctx, bpc, last_len):
             bad[pk[p][0] + q] ^= 0x20
             lab_ctx.upload(bad, d)
             got = set()
-            for v in (0, 52, 17):
+            for v in (0, 53, 52, 17):
                 lib.hdfs3x_set_variant(v)
                 got.add(lab_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, True))
             assert got == {(p, q // bpc)}, (p, q, got)
         blank = arena.copy()
         for data_off, crc_off, dl in pk:
             blank[crc_off:data_off] = 0
-        for v in (0, 52):
+        for v in (0, 53, 52):
             lib.hdfs3x_set_variant(v)
             lab_ctx.upload(blank, d)
             lab_ctx.compute_packets_dev(d.ptr, arena.nbytes, pk, bpc)
