@@ -109,6 +109,26 @@ def main():
         out.append({"bench": "packets_dev", "api": "async stream compute", "round": rnd,
                     "compute_GiBps": round(GiB / tc[0], 1), "contiguous_block_compute_GiBps": round(GiB / tb[0], 1),
                     "ratio_to_contiguous": round(tb[0] / tc[0], 4)})
+    # layout probe: the same stream with every packet's data on a 4 KiB boundary (pitch 68 KiB,
+    # words in the 512 B before the data) vs the wire-dense pitch above (64.5 KiB: rounds
+    # straddle 4 KiB pages)
+    apitch = pkt + 4096
+    arena2 = torch.randint(0, 256, (n * apitch,), dtype=torch.uint8, device="cuda")
+    ps2 = CrcContext.packet_stream(4096 - 512, 4096, apitch, n, pkt)
+    torch.cuda.synchronize()
+    lib.hdfs3_crc32c_compute_packet_stream_dev_async(ctx.ctx, arena2.data_ptr(), arena2.numel(), ctypes.byref(ps2), bpc)
+    for rnd in range(2):
+        for ovl in (0, 1):
+            tv = timed(lambda: lib.hdfs3_crc32c_verify_packet_stream_dev_async(ctx.ctx, arena.data_ptr(), arena.numel(),
+                                                                               ctypes.byref(ps), bpc, 0, res.data_ptr(),
+                                                                               ovl))
+            ta = timed(lambda: lib.hdfs3_crc32c_verify_packet_stream_dev_async(
+                ctx.ctx, arena2.data_ptr(), arena2.numel(), ctypes.byref(ps2), bpc, 0, res.data_ptr(), ovl))
+            tb = timed(lambda: lib.hdfs3_crc32c_verify_dev_async_ex(ctx.ctx, block.data_ptr(), block.numel(), bpc,
+                                                                    bwords.data_ptr(), 0, res.data_ptr(), ovl))
+            out.append({"bench": "packets_dev", "api": "async stream layout probe", "overlap": ovl, "round": rnd,
+                        "pitch_66048_us": round(tv[0] * 1e6, 1), "pitch_69632_aligned_us": round(ta[0] * 1e6, 1),
+                        "contiguous_us": round(tb[0] * 1e6, 1)})
     res.zero_()
     torch.cuda.synchronize()
     assert lib.hdfs3_crc32c_verify_packet_stream_dev_async(ctx.ctx, arena.data_ptr(), arena.numel(), ctypes.byref(ps),
