@@ -145,6 +145,10 @@ int32_t hdfs3_local_reader_read(hdfs3_local_reader *r, void *buf, int32_t len);
 int64_t hdfs3_local_reader_available(hdfs3_local_reader *r);
 int hdfs3_local_reader_stats(hdfs3_local_reader *r, uint32_t *bytes_per_checksum, int *checksum_type,
                              uint64_t *gpu_batches);
+/* windows whose pages were DMA'd straight from the mmap'd block file (mapped mode: the
+ * default when the read starts on a page and buffer_size is a page multiple; environment
+ * HDFS3_LOCAL_MMAP=0 disables it). The others were staged by pread into pinned windows. */
+uint64_t hdfs3_local_reader_mapped_windows(hdfs3_local_reader *r);
 int hdfs3_local_reader_close(hdfs3_local_reader *r);
 
 /* ------------------------------------------------------------------------------------

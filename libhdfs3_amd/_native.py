@@ -202,6 +202,7 @@ CLIENT_API = {
     "hdfs3_local_reader_read": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),
     "hdfs3_local_reader_available": (c_int64, [c_void_p]),
     "hdfs3_local_reader_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_int), POINTER(c_uint64)]),
+    "hdfs3_local_reader_mapped_windows": (c_uint64, [c_void_p]),
     "hdfs3_local_reader_close": (c_int, [c_void_p]),
     "hdfs3_output_open": (c_int, [POINTER(WriterOpts), PACKET_SINK, c_void_p, POINTER(c_void_p)]),
     "hdfs3_output_write": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),

@@ -12,8 +12,19 @@
 // Delivery granularity on a mismatch is the reference's: readAndVerify verifies one
 // buffer_size buffer before any of it is returned, so bytes of the buffer holding the
 // first bad chunk — and everything after — are withheld and -EIO is returned.
+//
+// Staging. Verification on: a window is pread into its pinned arena by the loader and the
+// helper threads together (a single pread thread was the single-stream limit), DMA'd, and
+// copied out. Verification off: the block file is mmap'd (MappedFileWrapper, MappedFileWrapper.cpp:
+// 58-70, is the reference's own mmap reader) and read() copies straight out of the page cache,
+// one copy per byte. HDFS3_LOCAL_MMAP=1 also maps verified reads: each window's page-cache pages
+// are registered with HIP (pinned in place) and DMA'd directly, then copied out of the mapping;
+// registration pins at ~23 GiB/s and serialises across threads in the runtime, so it is an
+// opt-in. HDFS3_LOCAL_MMAP=0 disables mapping altogether. Any mmap or
+// registration failure falls back to the pread path for that window or reader.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -121,25 +132,50 @@ class CopyPool {
         static CopyPool *p = new CopyPool();
         return *p;
     }
-    void copy(uint8_t *dst, const uint8_t *src, size_t n) {
+    void copy(uint8_t *dst, const uint8_t *src, size_t n) { split(dst, src, -1, 0, n); }
+    // pread of [off, off + n) of fd into dst, in parallel pieces; 0 or -errno
+    int pread(int fd, uint8_t *dst, size_t n, int64_t off) { return split(dst, nullptr, fd, off, n); }
+
+  private:
+    static constexpr size_t kHelpers = 3;
+    struct Job {
+        uint8_t *dst = nullptr;
+        const uint8_t *src = nullptr;  // memcpy source, or null: pread from fd at off
+        int fd = -1;
+        int64_t off = 0;
+        size_t n = 0;
+        std::atomic<int> *pending = nullptr;
+        std::atomic<int> *err = nullptr;
+    };
+    static void run(const Job &j) {
+        if (j.src) {
+            std::memcpy(j.dst, j.src, j.n);
+        } else if (int rc = pread_fully(j.fd, j.dst, j.n, j.off)) {
+            j.err->store(rc, std::memory_order_relaxed);
+        }
+        j.pending->fetch_sub(1, std::memory_order_release);
+    }
+    int split(uint8_t *dst, const uint8_t *src, int fd, int64_t foff, size_t n) {
         constexpr size_t kMin = 2u << 20;
+        std::atomic<int> pending{0}, err{0};
         if (n < kMin) {
-            std::memcpy(dst, src, n);
-            return;
+            run(Job{dst, src, fd, foff, n, &pending, &err});
+            return err.load();
         }
         const size_t parts = kHelpers + 1;
-        const size_t piece = (n / parts + 63) & ~size_t(63);
-        std::atomic<int> pending{0};
+        const size_t piece = (n / parts + 4095) & ~size_t(4095);
         size_t off = piece;
         {
             std::lock_guard<std::mutex> lk(mu_);
             for (size_t i = 1; i < parts && off < n; ++i, off += piece) {
-                jobs_.push_back(Job{dst + off, src + off, std::min(piece, n - off), &pending});
+                jobs_.push_back(Job{dst + off, src ? src + off : nullptr, fd, foff + int64_t(off), std::min(piece, n - off),
+                                    &pending, &err});
                 pending.fetch_add(1, std::memory_order_relaxed);
             }
         }
         cv_.notify_all();
-        std::memcpy(dst, src, std::min(piece, n));
+        pending.fetch_add(1, std::memory_order_relaxed);
+        run(Job{dst, src, fd, foff, std::min(piece, n), &pending, &err});
         // help with pieces no helper has taken yet, then wait for the rest
         for (;;) {
             Job j;
@@ -152,19 +188,7 @@ class CopyPool {
             run(j);
         }
         while (pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
-    }
-
-  private:
-    static constexpr size_t kHelpers = 3;
-    struct Job {
-        uint8_t *dst = nullptr;
-        const uint8_t *src = nullptr;
-        size_t n = 0;
-        std::atomic<int> *pending = nullptr;
-    };
-    static void run(const Job &j) {
-        std::memcpy(j.dst, j.src, j.n);
-        j.pending->fetch_sub(1, std::memory_order_release);
+        return err.load();
     }
     CopyPool() {
         for (size_t i = 0; i < kHelpers; ++i)
@@ -192,7 +216,11 @@ struct Window {
     uint32_t len = 0;         // data bytes
     int64_t bad_chunk = -1;   // first mismatching chunk (block-relative), after wait
     bool verified = false;
+    const uint8_t *src = nullptr;  // where read() copies from: a.h, or the mapping
+    void *reg = nullptr;           // mapped mode: the window's registered page range
 };
+
+constexpr int64_t kPage = 4096;
 
 }  // namespace
 
@@ -221,6 +249,11 @@ struct hdfs3_local_reader {
     int error = 0;
     std::string error_msg;
     std::atomic<uint64_t> batches{0};
+    // mapped mode
+    uint8_t *map = nullptr;
+    size_t map_len = 0;                      // length rounded up to a page
+    bool map_verified = false;               // HDFS3_LOCAL_MMAP=1: verified windows DMA'd from the mapping
+    std::atomic<uint64_t> mapped_windows{0};
 
     int sticky(int code, const std::string &msg) {
         error = code;
@@ -269,9 +302,28 @@ struct hdfs3_local_reader {
         w.len = uint32_t(std::min<int64_t>(window, length - start));
         w.bad_chunk = -1;
         w.verified = false;
-        if (int rc = pread_fully(data_fd, w.a.h, w.len, start)) {
-            load_msg = "LocalBlockReader: failed to read the block file";
-            return rc;
+        w.src = w.a.h;
+        w.reg = nullptr;
+        const uint8_t *h2d_src = w.a.h;
+        if (map && !verify) {
+            w.src = map + start;  // no staging at all: read() copies from the page cache
+        } else if (map && map_verified && start % kPage == 0) {
+            // pin the window's page-cache pages in place; the DMA reads them directly
+            const size_t reg_len = size_t(std::min<int64_t>((start + w.len + kPage - 1) / kPage * kPage,
+                                                            int64_t(map_len)) - start);
+            if (hipHostRegister(map + start, reg_len, hipHostRegisterReadOnly) == hipSuccess) {
+                w.reg = map + start;
+                w.src = h2d_src = map + start;
+                mapped_windows.fetch_add(1, std::memory_order_relaxed);
+            } else {
+                (void)hipGetLastError();  // pread path for this window
+            }
+        }
+        if (w.src == w.a.h) {
+            if (int rc = CopyPool::get().pread(data_fd, w.a.h, w.len, start)) {
+                load_msg = "LocalBlockReader: failed to read the block file";
+                return rc;
+            }
         }
         batches.fetch_add(1, std::memory_order_relaxed);
         if (!verify) {
@@ -284,7 +336,7 @@ struct hdfs3_local_reader {
             load_msg = "LocalBlockReader: failed to read the meta file";
             return rc;
         }
-        HIP_OK(hipMemcpyAsync(w.a.d, w.a.h, w.len, hipMemcpyHostToDevice, ctx->stream));
+        HIP_OK(hipMemcpyAsync(w.a.d, h2d_src, w.len, hipMemcpyHostToDevice, ctx->stream));
         HIP_OK(hipMemcpyAsync(w.a.d + cap_data, w.a.h + cap_data, 4 * chunks, hipMemcpyHostToDevice, ctx->stream));
         HIP_OK(hipMemsetAsync(w.a.d_res, 0, sizeof(unsigned long long), ctx->stream));
         if (int rc = hdfs3_crc32c_verify_dev_async(ctx, w.a.d, w.len, chunk_size, w.a.d + cap_data,
@@ -328,6 +380,13 @@ struct hdfs3_local_reader {
         std::lock_guard<std::mutex> lk(mu);
         load_done = true;
         cv.notify_all();
+    }
+
+    void release_pages(Window &w) {
+        if (w.reg) {
+            (void)hipHostUnregister(w.reg);
+            w.reg = nullptr;
+        }
     }
 
     // ---- caller side ----------------------------------------------------------------------
@@ -376,7 +435,7 @@ struct hdfs3_local_reader {
             const int64_t begin = std::max<int64_t>(cursor, w.start);
             if (begin < end) {
                 const int64_t n = std::min<int64_t>(end - begin, len - total);
-                CopyPool::get().copy(out + total, w.a.h + (begin - w.start), size_t(n));
+                CopyPool::get().copy(out + total, w.src + (begin - w.start), size_t(n));
                 total += int32_t(n);
                 cursor = begin + n;
             }
@@ -386,6 +445,7 @@ struct hdfs3_local_reader {
                 return total ? total : error;
             }
             if (cursor >= w.start + w.len) {
+                release_pages(w);  // its DMA completed: wait() saw the event
                 {
                     std::lock_guard<std::mutex> lk(mu);
                     ready.pop_front();
@@ -420,11 +480,14 @@ struct hdfs3_local_reader {
             res.ctx = ctx;
             for (int i = 0; i < kSlots; ++i) res.a[i] = slot[i].a;
             // a ctx whose stream completes cleanly goes back to the pool for the next reader
-            if (hipStreamSynchronize(ctx->stream) == hipSuccess && res.a[kSlots - 1].done)
+            const bool clean = hipStreamSynchronize(ctx->stream) == hipSuccess;
+            for (Window &w : slot) release_pages(w);  // no DMA is in flight any more
+            if (clean && res.a[kSlots - 1].done)
                 give_back(res);
             else
                 free_resources(res);
         }
+        if (map) munmap(map, map_len);
         if (data_fd >= 0) ::close(data_fd);
         if (meta_fd >= 0) ::close(meta_fd);
     }
@@ -471,6 +534,21 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
     r->cursor = offset;
     // whole buffers per window, at least one (the buffer itself is at most 1 GiB)
     r->window = uint32_t(std::max<int64_t>(1, std::min<int64_t>(wbuf, kMaxBuffer / r->buffer_size)) * r->buffer_size);
+    // mapped mode: verification off always (copies straight from the page cache); verified
+    // reads only with HDFS3_LOCAL_MMAP=1, and only when every window starts on a page (first
+    // and the window size page multiples), so windows register disjoint page ranges
+    const char *mm = getenv("HDFS3_LOCAL_MMAP");
+    r->map_verified = mm && mm[0] == '1' && r->verify && r->first % kPage == 0 && r->window % kPage == 0;
+    if (r->length > 0 && !(mm && mm[0] == '0') && (!r->verify || r->map_verified)) {
+        r->map_len = size_t((r->length + kPage - 1) / kPage * kPage);
+        void *m = mmap(nullptr, r->map_len, PROT_READ, MAP_SHARED, r->data_fd, 0);
+        if (m != MAP_FAILED) {
+            r->map = static_cast<uint8_t *>(m);
+            (void)madvise(m, r->map_len, MADV_SEQUENTIAL);
+        } else {
+            r->map_len = 0;
+        }
+    }
     r->cap_data = (size_t(r->window) + 255) & ~size_t(255);
     const size_t crc_bytes = r->verify ? 4 * ((size_t(r->window) + r->chunk_size - 1) / r->chunk_size) : 0;
     // the windows live on `device`, whatever the calling thread's current device is
@@ -517,6 +595,8 @@ int hdfs3_local_reader_stats(hdfs3_local_reader *r, uint32_t *bpc, int *checksum
     if (gpu_batches) *gpu_batches = r->batches.load();
     return 0;
 }
+
+uint64_t hdfs3_local_reader_mapped_windows(hdfs3_local_reader *r) { return r ? r->mapped_windows.load() : 0; }
 
 int hdfs3_local_reader_close(hdfs3_local_reader *r) {
     delete r;

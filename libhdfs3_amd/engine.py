@@ -621,7 +621,8 @@ class LocalBlockReader:
         from ctypes import c_uint32, c_uint64
         bpc, t, b = c_uint32(), c_int(), c_uint64()
         check("hdfs3_local_reader_stats", self._lib.hdfs3_local_reader_stats(self.r, byref(bpc), byref(t), byref(b)))
-        return {"bytes_per_checksum": bpc.value, "checksum_type": t.value, "gpu_batches": b.value}
+        return {"bytes_per_checksum": bpc.value, "checksum_type": t.value, "gpu_batches": b.value,
+                "mapped_windows": int(self._lib.hdfs3_local_reader_mapped_windows(self.r))}
 
     def close(self):
         if self.r:

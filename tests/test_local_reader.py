@@ -17,6 +17,19 @@ from util import oracle_compute, splitmix_bytes
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["default", "mmap", "pread"])
+def staging(request, monkeypatch):
+    """Every staging of the short-circuit reader must deliver identical results: default
+    (verified windows pread in parallel into pinned arenas; unverified reads copied straight
+    out of the mmap'd file), HDFS3_LOCAL_MMAP=1 (verified windows registered and DMA'd from the
+    mapping) and HDFS3_LOCAL_MMAP=0 (no mapping at all)."""
+    if request.param == "default":
+        monkeypatch.delenv("HDFS3_LOCAL_MMAP", raising=False)
+    else:
+        monkeypatch.setenv("HDFS3_LOCAL_MMAP", "1" if request.param == "mmap" else "0")
+    return request.param
+
+
 def write_block(tmp_path, name, data, bpc=512, ctype=2, version=1, crc=None):
     d, m = tmp_path / f"{name}", tmp_path / f"{name}.meta"
     d.write_bytes(data.tobytes())
@@ -34,12 +47,13 @@ def read(d, m, **kw):
 
 
 @pytest.mark.parametrize("bpc", [512, 4096])
-def test_full_and_offset_reads(tmp_path, bpc):
+def test_full_and_offset_reads(tmp_path, bpc, staging):
     data = splitmix_bytes(3 * (1 << 20) + 777, bpc)
     d, m = write_block(tmp_path, f"blk_{bpc}", data, bpc)
     out, st = read(d, m, buffer_size=1 << 18, window_buffers=3)
     assert np.array_equal(out, data)
     assert st["bytes_per_checksum"] == bpc and st["checksum_type"] == 2 and st["gpu_batches"] >= 4
+    assert (st["mapped_windows"] == st["gpu_batches"]) if staging == "mmap" else st["mapped_windows"] == 0
     for off in [1, bpc - 1, bpc + 5, 1 << 20, data.nbytes - 10, data.nbytes]:
         out, _ = read(d, m, offset=off)
         assert np.array_equal(out, data[off:]), off
@@ -53,7 +67,7 @@ def test_full_and_offset_reads(tmp_path, bpc):
 
 
 @pytest.mark.parametrize("where", [0, 300_000, (1 << 20) + 5, 3 * (1 << 20) + 700])
-def test_corruption_withholds_the_whole_local_buffer(tmp_path, where):
+def test_corruption_withholds_the_whole_local_buffer(tmp_path, where, staging):
     from libhdfs3_amd.engine import LocalBlockReader
     from libhdfs3_amd._native import Hdfs3CrcError
 
@@ -76,7 +90,7 @@ def test_corruption_withholds_the_whole_local_buffer(tmp_path, where):
     assert np.array_equal(out[:pos], data[:pos])
 
 
-def test_corrupt_meta_word_and_offset_recheck(tmp_path):
+def test_corrupt_meta_word_and_offset_recheck(tmp_path, staging):
     from libhdfs3_amd.engine import LocalBlockReader
     from libhdfs3_amd._native import Hdfs3CrcError
 
@@ -93,7 +107,7 @@ def test_corrupt_meta_word_and_offset_recheck(tmp_path):
     assert np.array_equal(out, data[51712:])
 
 
-def test_null_type_and_verify_off_read_without_checking(tmp_path):
+def test_null_type_and_verify_off_read_without_checking(tmp_path, staging):
     data = splitmix_bytes(500_000, 11)
     bad = data.copy()
     bad[1234] ^= 1

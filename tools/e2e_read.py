@@ -155,8 +155,10 @@ def local_reads(data, crc, args, line):
                     best = max(best, out.nbytes / dt / GIB)
                 assert np.array_equal(out, data[:out.nbytes])
                 out[:] = 0
+                staging = {"0": "pread", "1": "mmap"}.get(os.environ.get("HDFS3_LOCAL_MMAP", ""), "default")
                 print(json.dumps({**line, "mode": "local_read", "verify": verify, "streams": streams,
-                                  "read_mib": args.read_mib, "gib_s": round(best, 2)}), flush=True)
+                                  "read_mib": args.read_mib, "staging": staging, "gib_s": round(best, 2)}),
+                      flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
