@@ -28,6 +28,8 @@
 // 32-bit word costs 4 v_perm + 2 v_bitop3 + 4 ds_read_b32.
 #include <hip/hip_ext.h>
 
+#include <type_traits>
+
 #include "crc32c_kernels.h"
 #include "crc32c_tables.h"
 
@@ -704,6 +706,10 @@ constexpr int kOptHoldStore = 262144;
 //    pitch streams (reader arenas, resident packet rings) take this instead of the segmented
 //    kernel.
 constexpr int kOptPitch = 524288;
+//  kOptHead2: (PAIR 2, PF 1) the prologue loads the first TWO steps' rounds (4 rounds) before
+//    the LDS fill, and the first step issues no prefetch: the step-1 loads no longer wait for
+//    the fill barrier, while the steady-state depth (one step ahead) is unchanged.
+constexpr int kOptHead2 = 1048576;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -836,8 +842,9 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     };
     if constexpr ((OPT & kOptFillWait) != 0) fill();
     __builtin_amdgcn_sched_barrier(0);
-    constexpr int kPro = (OPT & kOptPf2) != 0 && PAIR == 2 ? 4 : PAIR;  // rounds loaded before the loop
-    Round b[kPro == 4 ? 6 : 2 * PAIR];
+    constexpr bool kHead2 = (OPT & kOptHead2) != 0 && PAIR == 2 && (OPT & kOptPf2) == 0;
+    constexpr int kPro = ((OPT & kOptPf2) != 0 && PAIR == 2) || kHead2 ? 4 : PAIR;  // rounds loaded before the loop
+    Round b[kPro == 4 && !kHead2 ? 6 : 2 * PAIR];
 #pragma unroll
     for (int i = 0; i < kPro; ++i) {
         load_any<NT, BUF>(b[i], round_ptr(i), lane_off);
@@ -960,15 +967,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         }
     } else {
         constexpr int PF = (OPT & kOptPf2) != 0 ? 2 : 1;  // steps of loads in flight
-        auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint64_t k) {
+        auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint64_t k, auto do_pf) {
+            constexpr bool kPf = decltype(do_pf)::value;
             const uint32_t w0 = want_of(k), w1 = want_of(k + 1);
-            constexpr bool kLate = (OPT & kOptLate) != 0, kSplit = (OPT & kOptSplit) != 0;
+            constexpr bool kLate = (OPT & kOptLate) != 0 || !kPf, kSplit = (OPT & kOptSplit) != 0;
             if constexpr (!kLate) load_any<NT, BUF>(p0, round_ptr(k + 2 * PF), lane_off);
             if constexpr (!kLate && !kSplit) load_any<NT, BUF>(p1, round_ptr(k + 2 * PF + 1), lane_off);
             __builtin_amdgcn_sched_barrier(0);
             regroup(c0);
             regroup(c1);
-            if constexpr (kLate) {
+            if constexpr (kLate && kPf) {
                 __builtin_amdgcn_sched_barrier(0);
                 load_any<NT, BUF>(p0, round_ptr(k + 2 * PF), lane_off);
                 load_any<NT, BUF>(p1, round_ptr(k + 2 * PF + 1), lane_off);
@@ -990,7 +998,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                if constexpr (kSplit && !kLate) {
+                if constexpr (kSplit && !kLate && kPf) {
                     if (i == 8) {
                         load_any<NT, BUF>(p1, round_ptr(k + 2 * PF + 1), lane_off);
                         __builtin_amdgcn_sched_barrier(0);
@@ -1027,23 +1035,37 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                 }
             }
         };
-        if constexpr (PF == 1) {
+        using pf_on = std::integral_constant<bool, true>;
+        using pf_off = std::integral_constant<bool, false>;
+        if constexpr (kHead2) {
+            // step 0 consumes b0/b1 without a prefetch (b2/b3 already hold step 1), then the
+            // usual one-step-ahead rotation from step 1 on
+            if (K > 0) {
+                step(b[0], b[1], b[2], b[3], 0, pf_off{});
+                stamp(2);
+            }
+            for (uint64_t k = 2; k < K; k += 4) {
+                step(b[2], b[3], b[0], b[1], k, pf_on{});
+                if (k + 2 >= K) break;
+                step(b[0], b[1], b[2], b[3], k + 2, pf_on{});
+            }
+        } else if constexpr (PF == 1) {
             for (uint64_t k = 0; k < K; k += 4) {
                 prio(k);
-                step(b[0], b[1], b[2], b[3], k);
+                step(b[0], b[1], b[2], b[3], k, pf_on{});
                 if (k == 0) stamp(2);
                 if (k + 2 >= K) break;
                 prio(k + 2);
-                step(b[2], b[3], b[0], b[1], k + 2);
+                step(b[2], b[3], b[0], b[1], k + 2, pf_on{});
             }
         } else {
             for (uint64_t k = 0; k < K; k += 6) {
-                step(b[0], b[1], b[4], b[5], k);
+                step(b[0], b[1], b[4], b[5], k, pf_on{});
                 if (k == 0) stamp(2);
                 if (k + 2 >= K) break;
-                step(b[2], b[3], b[0], b[1], k + 2);
+                step(b[2], b[3], b[0], b[1], k + 2, pf_on{});
                 if (k + 4 >= K) break;
-                step(b[4], b[5], b[2], b[3], k + 4);
+                step(b[4], b[5], b[2], b[3], k + 4, pf_on{});
             }
         }
     }

@@ -127,6 +127,10 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
     case 38:
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptSlotRegion | kOptWantBuf | kOptNoMath>(
             a, tab, fold, grid_cap, s);
+    case 70:  // production + two steps loaded before the fill (kOptHead2)
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptHead2>(a, tab, fold, grid_cap, s);
+    case 71:  // 70, overlapped launch
+        return launch_wave<BPC, V, 2, true, true, false, false, true, kOptLeanFill | kOptHead2>(a, tab, fold, grid_cap, s);
     case 60:  // block kernel (crc32c_block.h): computed tables + 4-round head
     case 61: {  // block kernel with the wave kernel's 2-round head (tables still computed)
         if constexpr (BPC == 512 || BPC == 1024) {
