@@ -631,12 +631,15 @@ constexpr int kPoolFoldOff = kLdsBytes;                 // 128 KiB
 constexpr int kPoolCtrOff = kLdsBytes + 16 * 1024;      // 144 KiB
 constexpr int kPoolLdsBytes = kPoolCtrOff + 16;
 
+// OFF: byte offset of the image; its 64 KiB part rides in address byte 2 (the nibble owns
+// byte 1), the rest in the ds_read immediate offset
+template <int OFF = kPoolFoldOff>
 __device__ __forceinline__ uint32_t fold_half(const uint8_t *lds, uint32_t x) {
     const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
-    const uint32_t fb = kPoolFoldOff + 4 * (threadIdx.x & 31);
+    const uint32_t fb = (OFF & ~0xFFFF) + 4 * (threadIdx.x & 31);
     auto at = [&](uint32_t src, uint32_t byte, int off) {
         const uint32_t addr = __builtin_amdgcn_perm(src, fb, 0x0C020000u | ((4u + byte) << 8));
-        return *reinterpret_cast<const uint32_t *>(lds + addr + off);
+        return *reinterpret_cast<const uint32_t *>(lds + addr + (OFF & 0xFFFF) + off);
     };
     const uint32_t a0 = at(lo, 0, 0), a1 = at(hi, 0, 128), a2 = at(lo, 1, 4096), a3 = at(hi, 1, 4096 + 128);
     const uint32_t a4 = at(lo, 2, 8192), a5 = at(hi, 2, 8192 + 128), a6 = at(lo, 3, 12288);
@@ -710,6 +713,13 @@ constexpr int kOptPitch = 524288;
 //    the LDS fill, and the first step issues no prefetch: the step-1 loads no longer wait for
 //    the fill barrier, while the steady-state depth (one step ahead) is unchanged.
 constexpr int kOptHead2 = 1048576;
+//  kOptFastTail: (PAIR 2, PF 1, G <= 32) a wave's LAST step runs each round as two 32-byte
+//    chains per lane (4 chains of 8 word steps instead of 2 of 16): the lookup chain that runs
+//    after the wave's last data arrived is half as long. The halves join as
+//    x = M_32(x_A) ^ x_B, M_32 = advance over 32 bytes, read from a lane-replicated nibble
+//    image in the LDS's last 16 KiB (ChunkLaunch::m32, 8 lookups per round, last step only).
+constexpr int kOptFastTail = 2097152;
+constexpr int kTailFoldOff = kLdsBytes + 16 * 1024;  // 144 KiB: M_32 nibble image (16 KiB)
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -797,12 +807,15 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     constexpr bool kHalfFold = kLean && G <= 32;
     uint32_t tv[kLean ? 1 : kFillPerThread];
     u32x4 n0, n1;
+    constexpr bool kFastTail = (OPT & kOptFastTail) != 0 && kLean && G <= 32 && PAIR == 2 && (OPT & (kOptPf2 | kOptHead2)) == 0;
+    uint32_t m32w = 0;  // kFastTail: this thread's word of the M_32 nibble image
     if constexpr (kLean) {
         const uint32_t t = threadIdx.x;
         tv[0] = g_tab[t];  // slice t >> 8, entry t & 255
         if constexpr (kHalfFold) {
             const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
             n0 = *reinterpret_cast<const u32x4 *>(g_nib + (fk * 16 + fe) * 64 + fc);
+            if constexpr (kFastTail) m32w = a.m32[fk * 16 + fe];
         } else {
             n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
             n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
@@ -827,6 +840,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             for (int r = 0; r < 8; ++r) l4[slot0 + ((r + t) & 7)] = u32x4{tv[0], tv[0], tv[0], tv[0]};
             if constexpr (kHalfFold) {
                 reinterpret_cast<u32x4 *>(lds + kPoolFoldOff / 4)[t] = n0;
+                if constexpr (kFastTail) reinterpret_cast<u32x4 *>(lds + kTailFoldOff / 4)[t] = u32x4{m32w, m32w, m32w, m32w};
             } else {
                 u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * t;
                 dst[0] = n0;
@@ -1037,7 +1051,53 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         };
         using pf_on = std::integral_constant<bool, true>;
         using pf_off = std::integral_constant<bool, false>;
-        if constexpr (kHead2) {
+        // kFastTail: the wave's last step, no prefetch, four half-round chains
+        auto tail = [&](Round &c0, Round &c1, uint64_t k) {
+            const uint32_t w0 = want_of(k), w1 = want_of(k + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            regroup(c0);
+            regroup(c1);
+            uint32_t xa0 = init ^ word(c0, 0), xb0 = word(c0, 8), xa1 = init ^ word(c1, 0), xb1 = word(c1, 8);
+            Look la0 = lookups(t, xa0), lb0 = lookups(t, xb0), la1, lb1;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                la1 = lookups(t, xa1);
+                lb1 = lookups(t, xb1);
+                __builtin_amdgcn_sched_barrier(0);
+                xa0 = combine(la0, i < 7 ? word(c0, i < 7 ? i + 1 : 7) : 0u);
+                xb0 = combine(lb0, i < 7 ? word(c0, i < 7 ? i + 9 : 15) : 0u);
+                __builtin_amdgcn_sched_barrier(0);
+                if (i < 7) {
+                    la0 = lookups(t, xa0);
+                    lb0 = lookups(t, xb0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                xa1 = combine(la1, i < 7 ? word(c1, i < 7 ? i + 1 : 7) : 0u);
+                xb1 = combine(lb1, i < 7 ? word(c1, i < 7 ? i + 9 : 15) : 0u);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const uint8_t *l8 = reinterpret_cast<const uint8_t *>(lds);
+            const uint32_t x0 = fold_half<kTailFoldOff>(l8, xa0) ^ xb0;
+            const uint32_t x1 = fold_half<kTailFoldOff>(l8, xa1) ^ xb1;
+            finish(k, group_xor<G>(fold(x0)), w0);
+            finish(k + 1, group_xor<G>(fold(x1)), w1);
+        };
+        if constexpr (kFastTail) {
+            for (uint64_t k = 0; k < K; k += 4) {
+                if (k + 2 >= K) {
+                    tail(b[0], b[1], k);
+                    break;
+                }
+                step(b[0], b[1], b[2], b[3], k, pf_on{});
+                if (k == 0) stamp(2);
+                if (k + 4 >= K) {
+                    tail(b[2], b[3], k + 2);
+                    break;
+                }
+                step(b[2], b[3], b[0], b[1], k + 2, pf_on{});
+            }
+        } else if constexpr (kHead2) {
             // step 0 consumes b0/b1 without a prefetch (b2/b3 already hold step 1), then the
             // usual one-step-ahead rotation from step 1 on
             if (K > 0) {
@@ -1757,15 +1817,17 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
         const uint64_t units = (OPT & kOptPitch) != 0 ? ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes
                                                       : a.len / kRoundBytes;
+        ChunkLaunch la = a;
+        if constexpr ((OPT & kOptFastTail) != 0) la.m32 = fold + kFoldM32Off;
         const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
         int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
         if (grid < 1) grid = 1;
         if (ANY_ORDER || a.overlap_previous)  // AQL packet without the barrier bit (variant 16, opt-in flag)
             hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
-                                  dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+                                  dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, la, tab, nib);
         else
             hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
-                               dim3(kBlockThreads), 0, s, a, tab, nib);
+                               dim3(kBlockThreads), 0, s, la, tab, nib);
         return hipGetLastError();
     }
 }

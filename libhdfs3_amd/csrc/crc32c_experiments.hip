@@ -131,6 +131,8 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptHead2>(a, tab, fold, grid_cap, s);
     case 71:  // 70, overlapped launch
         return launch_wave<BPC, V, 2, true, true, false, false, true, kOptLeanFill | kOptHead2>(a, tab, fold, grid_cap, s);
+    case 72:  // production + the fast tail (kOptFastTail)
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptFastTail>(a, tab, fold, grid_cap, s);
     case 60:  // block kernel (crc32c_block.h): computed tables + 4-round head
     case 61: {  // block kernel with the wave kernel's 2-round head (tables still computed)
         if constexpr (BPC == 512 || BPC == 1024) {

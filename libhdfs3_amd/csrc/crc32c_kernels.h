@@ -36,6 +36,9 @@ struct ChunkLaunch {
     uint64_t npk = 0;
     uint32_t upp_log2 = 0;
     uint32_t last_len = 0;
+    // kOptFastTail: the M_32 (advance over 32 bytes) nibble image of the ctx's polynomial,
+    // 128 words: word k*16 + e = M_32(e << 4k); set by launch_wave
+    const uint32_t *m32 = nullptr;
 };
 
 // Packet-descriptor as seen by the device (mirrors hdfs3_pkt_desc).

@@ -90,4 +90,15 @@ inline void build_fold_nibbles(const uint32_t fold[kFoldWords], int set, uint32_
     }
 }
 
+// M_32 (advance over 32 bytes) as a nibble image for the wave kernel's fast tail: word
+// k * 16 + e = M_32(e << 4k). Appended after the four lane-fold nibble sets.
+constexpr int kM32Words = 8 * 16;
+constexpr int kFoldM32Off = kFoldWords + 4 * kFoldNibbleWords;
+inline void build_m32_nibbles(const uint32_t t0[kTableEntries], uint32_t out[kM32Words]) {
+    uint32_t cols[32];
+    shift_cols(t0, 32, cols);
+    for (int k = 0; k < 8; ++k)
+        for (uint32_t e = 0; e < 16; ++e) out[k * 16 + e] = apply_cols(cols, e << (4 * k));
+}
+
 }  // namespace hdfs3crc

@@ -49,7 +49,7 @@ namespace hdfs3crc {
 // matrix columns and 4 nibble-table sets for G = 8, 16, 32, 64), built once per process.
 struct HostImage {
     uint32_t t[kSlices][kTableEntries];
-    uint32_t fold[kFoldWords + 4 * kFoldNibbleWords];
+    uint32_t fold[kFoldWords + 4 * kFoldNibbleWords + kM32Words];
 };
 
 const HostImage *host_images() {
@@ -62,6 +62,7 @@ const HostImage *host_images() {
             build_fold_matrices(img[p].t[0], img[p].fold);
             for (int set = 0; set < 4; ++set)
                 build_fold_nibbles(img[p].fold, set, img[p].fold + kFoldWords + set * kFoldNibbleWords);
+            build_m32_nibbles(img[p].t[0], img[p].fold + kFoldM32Off);
         }
     });
     return img;
