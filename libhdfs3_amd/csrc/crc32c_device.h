@@ -738,14 +738,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     const uint64_t nunits = kPit ? ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes : a.len / kRoundBytes;
     // kPit: unit u -> (packet, round in packet); the contiguous case is packet 0 at pitch 0
     const uint64_t umask = (uint64_t(1) << a.upp_log2) - 1;
+    const uint64_t cpitch = a.crc_pitch ? a.crc_pitch : a.pitch;  // the words' pitch
     auto unit_data = [&](uint64_t u) -> const uint8_t * {
         if constexpr (kPit) return a.data + (u >> a.upp_log2) * a.pitch + (u & umask) * kRoundBytes;
         return a.data + u * kRoundBytes;
     };
-    // byte offset of chunk c of unit u's CRC word inside crc_be/out_be, and its result key
-    auto word_off = [&](uint64_t u, uint32_t c) -> uint64_t {
-        if constexpr (kPit) return (u >> a.upp_log2) * a.pitch + 4 * ((u & umask) * kChunksPerUnit + c);
-        return 4 * (u * kChunksPerUnit + c);
+    // the CRC word of chunk c of unit u (stored words when verifying, the output when computing)
+    auto word_ptr = [&](uint64_t u, uint32_t c) -> uint8_t * {
+        uint8_t *base = VERIFY ? const_cast<uint8_t *>(a.crc_be) : a.out_be;
+        if constexpr (kPit) return base + (u >> a.upp_log2) * cpitch + 4 * ((u & umask) * kChunksPerUnit + c);
+        return base + 4 * (u * kChunksPerUnit + c);
     };
     auto key_of = [&](uint64_t u, uint32_t c) -> uint64_t {
         if constexpr (kPit) return ((u >> a.upp_log2) << 32) | ((u & umask) * kChunksPerUnit + c);
@@ -895,7 +897,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                     reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, 4 * kChunksPerUnit, 0x00020000);
                 return __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (lane / G), 0, 0);
             }
-            return *reinterpret_cast<const uint32_t *>(a.crc_be + word_off(first + kk * stride, lane / G));
+            return *reinterpret_cast<const uint32_t *>(word_ptr(first + kk * stride, lane / G));
         }
         return 0;
     };
@@ -911,7 +913,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             if (uint32_t(i) < nheld) {
                 const uint64_t k = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
                 if (k < K)
-                    *reinterpret_cast<uint32_t *>(a.out_be + word_off(first + k * stride, lane & 7)) =
+                    *reinterpret_cast<uint32_t *>(word_ptr(first + k * stride, lane & 7)) =
                         __builtin_bswap32(~hold[i]);
             }
         }
@@ -953,11 +955,11 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                                                                                : __builtin_bswap32(want) != c;
             if (bad) atomicMax(a.result, ~(unsigned long long)key_of(u, lane / G));
         } else if constexpr ((OPT & kOptNoStore) != 0) {
-            if (c == 0x9E3779B9u) *reinterpret_cast<uint32_t *>(a.out_be + word_off(u, lane / G)) = c;
+            if (c == 0x9E3779B9u) *reinterpret_cast<uint32_t *>(word_ptr(u, lane / G)) = c;
         } else if constexpr ((OPT & kOptNtStore) != 0) {
-            __builtin_nontemporal_store(__builtin_bswap32(c), reinterpret_cast<uint32_t *>(a.out_be + word_off(u, lane / G)));
+            __builtin_nontemporal_store(__builtin_bswap32(c), reinterpret_cast<uint32_t *>(word_ptr(u, lane / G)));
         } else {
-            *reinterpret_cast<uint32_t *>(a.out_be + word_off(u, lane / G)) = __builtin_bswap32(c);
+            *reinterpret_cast<uint32_t *>(word_ptr(u, lane / G)) = __builtin_bswap32(c);
         }
     };
     // word i (0..15) of the lane's 64-byte segment after regroup
@@ -1136,22 +1138,22 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     // last packet, the only one that may end inside a round)
     const uint64_t len = kPit ? a.last_len : a.len;
     const uint8_t *sdata = kPit ? a.data + (a.npk - 1) * a.pitch : a.data;
-    const uint64_t soff = kPit ? (a.npk - 1) * a.pitch : 0;  // of the slow chunks' words
+    uint8_t *sw = (VERIFY ? const_cast<uint8_t *>(a.crc_be) : a.out_be) + (kPit ? (a.npk - 1) * cpitch : 0);
     const uint64_t skey = kPit ? (a.npk - 1) << 32 : a.chunk_base;
     const uint64_t nfull = len / BPC;
     const uint64_t first_slow = (len / kRoundBytes) * kChunksPerUnit;
     const uint64_t nslow = nfull - first_slow + (len % BPC ? 1 : 0);
     const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
-    const bool crc_al4 = (reinterpret_cast<uintptr_t>(VERIFY ? a.crc_be : a.out_be) & 3u) == 0;
+    const bool crc_al4 = (reinterpret_cast<uintptr_t>(sw) & 3u) == 0;
     if (gtid < nslow) {
         const uint64_t chunk = first_slow + gtid;
         const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(len % BPC);
         const uint32_t c = ~crc_run_lines(t, 0xFFFFFFFFu, sdata + chunk * BPC, sz);
         if constexpr (VERIFY) {
-            if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(a.crc_be + soff + 4 * chunk, crc_al4) != c)
+            if ((sz == uint32_t(BPC) || a.check_short_tail) && load_be32(sw + 4 * chunk, crc_al4) != c)
                 atomicMax(a.result, ~(unsigned long long)(skey + chunk));
         } else {
-            store_be32(a.out_be + soff + 4 * chunk, c, crc_al4);
+            store_be32(sw + 4 * chunk, c, crc_al4);
         }
     }
 }

@@ -39,6 +39,9 @@ struct ChunkLaunch {
     // kOptFastTail: the M_32 (advance over 32 bytes) nibble image of the ctx's polynomial,
     // 128 words: word k*16 + e = M_32(e << 4k); set by launch_wave
     const uint32_t *m32 = nullptr;
+    // pitch mode over independent blocks at constant strides (a [blocks, bytes] tensor and its
+    // [blocks, words] tensor): the words' own pitch; 0 = `pitch` (the wire layout of packets)
+    uint64_t crc_pitch = 0;
 };
 
 // Packet-descriptor as seen by the device (mirrors hdfs3_pkt_desc).
@@ -86,6 +89,12 @@ bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32
                       const void *crc, uint64_t pitch, uint32_t *upp_log2);
 hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
                                 int grid_cap, hipStream_t stream);
+// batches of equal blocks (the last may be shorter) of a power-of-two number of whole rounds
+// whose data and words sit at two constant strides (blocks of one 2-D tensor): the pitch mode
+// with crc_pitch; hipErrorNotSupported = use the segmented kernel
+hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc, bool verify, int check_short_tail,
+                                 unsigned long long *result, const uint32_t *d_tables, const uint32_t *d_fold,
+                                 int grid_cap, hipStream_t stream);
 hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,

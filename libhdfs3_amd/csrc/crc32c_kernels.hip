@@ -55,6 +55,7 @@ hipError_t launch_pv(const ChunkLaunch &a, bool verify, const uint32_t *tab, con
     return verify ? launch_p<BPC, true>(a, tab, fold, grid_cap, s) : launch_p<BPC, false>(a, tab, fold, grid_cap, s);
 }
 
+
 }  // namespace
 
 bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32_t bpc, const void *data,
@@ -72,6 +73,39 @@ bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32
     while ((uint64_t(1) << l) < upp) ++l;
     *upp_log2 = l;
     return true;
+}
+
+hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc, bool verify, int check_short_tail,
+                                 unsigned long long *result, const uint32_t *d_tables, const uint32_t *d_fold,
+                                 int grid_cap, hipStream_t stream) {
+#if HDFS3_LAB
+    if (g_variant == 54) return hipErrorNotSupported;  // A/B: force the segmented kernel
+#endif
+    if (n < 2) return hipErrorNotSupported;
+    const int64_t dp = h_seg[1].data - h_seg[0].data, cp = h_seg[1].crc - h_seg[0].crc;
+    if (dp <= 0 || cp <= 0) return hipErrorNotSupported;
+    for (size_t i = 0; i < n; ++i)
+        if (h_seg[i].data != h_seg[0].data + int64_t(i) * dp || h_seg[i].crc != h_seg[0].crc + int64_t(i) * cp ||
+            (i + 1 < n && h_seg[i].len != h_seg[0].len) || h_seg[i].len > h_seg[0].len)
+            return hipErrorNotSupported;
+    uint32_t upp_log2 = 0;
+    if (!packet_stream_ok(h_seg[0].len, h_seg[n - 1].len, n, bpc, h_seg[0].data, h_seg[0].crc, uint64_t(dp),
+                          &upp_log2) ||
+        (cp & 3))
+        return hipErrorNotSupported;
+    ChunkLaunch a{};
+    a.data = h_seg[0].data;
+    a.crc_be = h_seg[0].crc;
+    a.out_be = h_seg[0].crc;
+    a.bpc = bpc;
+    a.result = result;
+    a.check_short_tail = check_short_tail;
+    a.pitch = uint64_t(dp);
+    a.crc_pitch = uint64_t(cp);
+    a.npk = n;
+    a.upp_log2 = upp_log2;
+    a.last_len = uint32_t(h_seg[n - 1].len);
+    return launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream);
 }
 
 hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,

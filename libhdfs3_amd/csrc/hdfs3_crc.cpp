@@ -364,7 +364,14 @@ int blocks_common(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, u
     for (size_t i = 0; i < n; ++i)
         st->h[i] = DevSegment{static_cast<const uint8_t *>(blocks[i].data), static_cast<uint8_t *>(blocks[i].crc_be),
                               blocks[i].len, 0, uint64_t(i) << 32};
-    if (segments_fast(st->h, n, bpc)) {
+    // blocks of one 2-D tensor (constant data and word strides, equal whole-round blocks): the
+    // wave kernel walks them directly (pitch mode); everything else: the segmented kernel
+    const hipError_t te = launch_strided_blocks(st->h, n, bpc, verify, check_short_tail, d_result, ctx->d_tables,
+                                                ctx->d_fold, ctx->grid_cap, ctx->stream);
+    if (te != hipErrorNotSupported) {
+        HIP_TRY(te);
+        ++ctx->launches;
+    } else if (segments_fast(st->h, n, bpc)) {
         uint64_t uniform = 0;
         const uint64_t units = plan_segments(st->h, n, &uniform);
         if (n <= kMaxInlineSegments) {  // descriptors in the kernel arguments: no copy first

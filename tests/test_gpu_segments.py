@@ -32,6 +32,8 @@ def make_blocks(ctx, sizes, bpc, seed, pad=0):
     [1 << 20] * 8,                                     # uniform: direct unit -> segment map
     [4096 * 5 + 700, 0, 300, 1 << 20, 4096, 8192 + 1],  # ragged: binary search, slow pass, empty
     [65536] * 37 + [1000],                              # packet-like
+    [1 << 20] * 5 + [(1 << 20) - 4096 * 3 - 300],       # equal blocks + shorter last: wave kernel table mode
+    [1 << 18] * 16,                                     # the table mode's 16-block limit
 ])
 def test_blocks_batch_matches_per_block_oracle(gpu_ctx, bpc, sizes):
     blocks, keep, datas = make_blocks(gpu_ctx, sizes, bpc, bpc * 13 + len(sizes))
@@ -223,5 +225,43 @@ def test_constant_pitch_packets_without_descriptors(lab_ctx, bpc, last_len):
             lab_ctx.upload(blank, d)
             lab_ctx.compute_packets_dev(d.ptr, arena.nbytes, pk, bpc)
             assert np.array_equal(lab_ctx.download(d, arena.nbytes), arena), v
+    finally:
+        lib.hdfs3x_set_variant(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bpc", [512, 2048])
+@pytest.mark.parametrize("last", [1 << 20, (1 << 20) - 4096 * 7 - 100, 300])
+def test_strided_blocks_take_the_wave_kernel(lab_ctx, bpc, last):
+    """Blocks of one 2-D arrangement (data at a constant stride, words at another; the bench's
+    [blocks, bytes] tensor) go to the wave kernel's pitch mode with its own word pitch (variant
+    0); the segmented kernel (variant 54) and the oracle must agree on every word and key."""
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    lib = _native.lab()
+    n, L = 6, 1 << 20
+    dstride, wstride = L + 4096, 4 * (L // bpc) + 64  # both padded: strides differ from sizes
+    datas = [splitmix_bytes(L if i + 1 < n else last, 300 + i + bpc) for i in range(n)]
+    dbuf, wbuf = DeviceBuffer(n * dstride), DeviceBuffer(n * wstride)
+    for i, d in enumerate(datas):
+        lab_ctx.upload(d, dbuf, offset=i * dstride)
+    blocks = [(dbuf.ptr + i * dstride, wbuf.ptr + i * wstride, d.size) for i, d in enumerate(datas)]
+    try:
+        for v in (0, 54):
+            lib.hdfs3x_set_variant(v)
+            lab_ctx.memset(wbuf, 0, n * wstride)
+            lab_ctx.compute_blocks_dev(blocks, bpc)
+            for i, d in enumerate(datas):
+                want = oracle_compute(d, bpc)
+                assert np.array_equal(lab_ctx.download(wbuf.ptr + i * wstride, want.nbytes), want), (v, i)
+            assert lab_ctx.verify_blocks_dev(blocks, bpc, True) == (-1, -1), v
+        for bi, pos in [(n - 1, last - 1), (2, 4096 * 9 + 3), (0, 0)]:
+            lab_ctx.upload(np.array([datas[bi][pos] ^ 0x80], np.uint8), dbuf, offset=bi * dstride + pos)
+            got = set()
+            for v in (0, 54):
+                lib.hdfs3x_set_variant(v)
+                got.add(lab_ctx.verify_blocks_dev(blocks, bpc, True))
+            assert got == {(bi, pos // bpc)}, (bi, pos, got)
     finally:
         lib.hdfs3x_set_variant(0)

@@ -58,7 +58,9 @@ def test_bench_gpus_2_real_run_on_one_gpu():
     assert a["seed"] != b["seed"] and a["value"] > 0 and b["value"] > 0
     slowest = max(a["ms_per_step"], b["ms_per_step"])
     assert j["ms_per_step"] == pytest.approx(slowest, rel=1e-3)
-    assert j["value"] == pytest.approx(2 * (16 << 20) / (slowest * 1e-3) / 2**30, rel=2e-3)
+    # aggregate = both ranks' bytes / the slower rank's time = 2 x the slower rank's own rate
+    # (per-rank rates carry 0.01 GiB/s rounding; ms_per_step only 4 decimals, too coarse here)
+    assert j["value"] == pytest.approx(2 * min(a["value"], b["value"]), rel=1e-3)
 
 
 def _multi(devices):
