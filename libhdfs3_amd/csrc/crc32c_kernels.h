@@ -99,7 +99,8 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                hipStream_t stream, uint64_t arena_len = 0, size_t *bad_index = nullptr,
-                               bool overlap_previous = false);
+                               bool overlap_previous = false)  // bad_index != null: check every packet
+                                                               // against [0, arena_len) first;
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream);

@@ -263,7 +263,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
     const uint64_t pitch = n > 1 ? h_pk[1].data_off - h_pk[0].data_off : 0;
     bool strided = n > 1 && g_variant != 52 && pitch > 0 && pitch == h_pk[1].crc_off - h_pk[0].crc_off;
     for (size_t i = 0; i < n; ++i) {
-        if (arena_len) {  // bounds, fused into this pass (the API's only pass over pk[])
+        if (bad_index) {  // bounds, fused into this pass (the API's only pass over pk[])
             const hdfs3crc::DevPacket &d = h_pk[i];
             const uint64_t chunks = (uint64_t(d.data_len) + bpc - 1) / bpc;
             if (d.data_off > arena_len || d.data_len > arena_len - d.data_off || d.crc_off > arena_len ||

@@ -259,8 +259,8 @@ int packets_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len, 
     const DevPacket *hp = reinterpret_cast<const DevPacket *>(pk);
     size_t bad = 0;
     const hipError_t e = launch_packet_batch(d_arena, hp, n, bpc, verify, check_short_tail, d_result, st->h, st->d,
-                                             ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream,
-                                             arena_len ? arena_len : 1, &bad, overlap);
+                                             ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, arena_len,
+                                             &bad, overlap);
     if (e == hipErrorInvalidValue) return fail(-EINVAL, "packet %zu lies outside the %zu-byte arena", bad, arena_len);
     HIP_TRY(e);
     ++ctx->launches;
