@@ -95,12 +95,13 @@ hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_
 hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc, bool verify, int check_short_tail,
                                  unsigned long long *result, const uint32_t *d_tables, const uint32_t *d_fold,
                                  int grid_cap, hipStream_t stream);
+// bad_index != null: every packet is first checked against [0, arena_len) (hipErrorInvalidValue
+// and *bad_index = the first one outside)
 hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                hipStream_t stream, uint64_t arena_len = 0, size_t *bad_index = nullptr,
-                               bool overlap_previous = false)  // bad_index != null: check every packet
-                                                               // against [0, arena_len) first;
+                               bool overlap_previous = false);
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream);
