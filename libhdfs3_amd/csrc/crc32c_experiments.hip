@@ -4,6 +4,7 @@
 // Bit-exact variants are parity-tested (tests/test_gpu_parity.py); the diagnostic ones
 // (no HBM / no math / fake lookups / timestamps) give wrong results on purpose.
 #include "crc32c_block.h"
+#include "crc32c_wave2.h"
 
 namespace hdfs3crc {
 namespace {
@@ -133,6 +134,16 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
         return launch_wave<BPC, V, 2, true, true, false, false, true, kOptLeanFill | kOptHead2>(a, tab, fold, grid_cap, s);
     case 72:  // production + the fast tail (kOptFastTail)
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptFastTail>(a, tab, fold, grid_cap, s);
+    case 73:  // production + uneven work per workgroup (kOptSkew)
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptSkew>(a, tab, fold, grid_cap, s);
+    case 74:    // two 512-thread workgroups per CU, slice-by-2 tables (crc32c_wave2.h)
+    case 75: {  // the same kernel, one workgroup per CU per launch (grid = CUs)
+        if constexpr (BPC <= 2048) {
+            return launch_wave2<BPC, V>(a, tab, fold, grid_cap, s, variant == 74 ? 2 : 1);
+        } else {
+            return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill>(a, tab, fold, grid_cap, s);
+        }
+    }
     case 60:  // block kernel (crc32c_block.h): computed tables + 4-round head
     case 61: {  // block kernel with the wave kernel's 2-round head (tables still computed)
         if constexpr (BPC == 512 || BPC == 1024) {
