@@ -720,6 +720,14 @@ constexpr int kOptHead2 = 1048576;
 //    image in the LDS's last 16 KiB (ChunkLaunch::m32, 8 lookups per round, last step only).
 constexpr int kOptFastTail = 2097152;
 constexpr int kTailFoldOff = kLdsBytes + 16 * 1024;  // 144 KiB: M_32 nibble image (16 KiB)
+//  kOptSkew: uneven work per workgroup for back-to-back overlapped launches. The first half of
+//    the workgroups take base + base/4 rounds per wave, the second half base - base/4 (rounds
+//    0 .. (base - base/4) * nwaves - 1 round-robin over every wave as usual, the rest
+//    round-robin over the heavy waves only). With overlapped launches the CP hands the next
+//    launch's first (heavy) workgroups to the CUs that freed first (they ran light ones), so
+//    CUs alternate heavy/light and their launch heads — dispatch, fill, first-data latency,
+//    when a CU pulls no HBM bytes — no longer line up across the chip.
+constexpr int kOptSkew = 8388608;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -779,6 +787,19 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     } else {
         K = wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0;
     }
+    // kOptSkew geometry (even base only; otherwise the plain round-robin above)
+    constexpr bool kSkewOpt = (OPT & kOptSkew) != 0 && !kLine && (OPT & kOptSlotRegion) == 0;
+    const uint64_t sk_base = kSkewOpt ? nunits / nwaves : 0;
+    const bool skew = kSkewOpt && nunits % nwaves == 0 && sk_base >= 4 && sk_base % 4 == 0 && gridDim.x % 2 == 0;
+    const uint64_t sk_light = sk_base - sk_base / 4, sk_half = nwaves / 2;
+    if (skew) K = wave < sk_half ? sk_base + sk_base / 4 : sk_light;
+    // unit of the wave's round k
+    auto uk = [&](uint64_t k) -> uint64_t {
+        if constexpr (kSkewOpt) {
+            if (skew && k >= sk_light) return sk_light * nwaves + wave + (k - sk_light) * sk_half;
+        }
+        return first + k * stride;
+    };
     // Prefetches past the wave's last round stay unconditional (a branch around them
     // makes the waitcnt pass drain every load at the loop head) but read the 4 KiB slice
     // table image instead: cache-resident, so they cost no HBM bytes (re-reading data
@@ -790,7 +811,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             const uint64_t u = unit_of(k);
             return k < K && u < nunits ? a.data + u * kRoundBytes : reinterpret_cast<const uint8_t *>(g_tab);
         }
-        return k < K ? unit_data(first + k * stride) : reinterpret_cast<const uint8_t *>(g_tab);
+        return k < K ? unit_data(uk(k)) : reinterpret_cast<const uint8_t *>(g_tab);
     };
 
     // TRACE (variant 13): lane 0 of each wave stamps entry, post-fill, post-first-step
@@ -897,7 +918,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                     reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, 4 * kChunksPerUnit, 0x00020000);
                 return __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (lane / G), 0, 0);
             }
-            return *reinterpret_cast<const uint32_t *>(word_ptr(first + kk * stride, lane / G));
+            return *reinterpret_cast<const uint32_t *>(word_ptr(uk(kk), lane / G));
         }
         return 0;
     };
@@ -913,7 +934,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             if (uint32_t(i) < nheld) {
                 const uint64_t k = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
                 if (k < K)
-                    *reinterpret_cast<uint32_t *>(word_ptr(first + k * stride, lane & 7)) =
+                    *reinterpret_cast<uint32_t *>(word_ptr(uk(k), lane & 7)) =
                         __builtin_bswap32(~hold[i]);
             }
         }
@@ -948,7 +969,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             return;
         }
         if (k >= K || j != 0) return;
-        const uint64_t u = first + k * stride;
+        const uint64_t u = uk(k);
         const uint32_t c = ~y;
         if constexpr (VERIFY) {
             const bool bad = (OPT & (kOptNoHbm | kOptNoFill | kOptNoMath | kOptFakeLut)) != 0 ? __builtin_bswap32(want) == ~c
