@@ -87,21 +87,34 @@ constexpr uint32_t kMaxInlineSegments = 16;
 // whole rounds), and its launcher (a.pitch/npk/upp_log2/last_len set)
 bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32_t bpc, const void *data,
                       const void *crc, uint64_t pitch, uint32_t *upp_log2);
+// Compute mode over a stream whose CRC words sit inside each packet (the wire layout: 512 B of
+// words per 64 KiB packet, 66 KiB apart) writes 8 MiB per GiB as small regions scattered over
+// the arena, interleaved with the read stream: 1 GiB took 213 us against 186 us with the words
+// written densely (tools/compute_layout_probe.py). With a WordScratch the words
+// go densely into it and one copy kernel scatters them to the packets afterwards.
+struct WordScratch {
+    uint8_t *d = nullptr;
+    uint64_t cap = 0;
+    hipEvent_t used = nullptr;  // recorded after the last launch that read the scratch
+    void release();
+};
+// word regions at most this long (per packet) take the dense path: 64 KiB = 8 MiB packets at bpc 512
+constexpr uint64_t kDenseWordsMaxRegion = 64 * 1024;
 hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
-                                int grid_cap, hipStream_t stream);
+                                int grid_cap, hipStream_t stream, WordScratch *ws = nullptr);
 // batches of equal blocks (the last may be shorter) of a power-of-two number of whole rounds
 // whose data and words sit at two constant strides (blocks of one 2-D tensor): the pitch mode
 // with crc_pitch; hipErrorNotSupported = use the segmented kernel
 hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc, bool verify, int check_short_tail,
                                  unsigned long long *result, const uint32_t *d_tables, const uint32_t *d_fold,
-                                 int grid_cap, hipStream_t stream);
+                                 int grid_cap, hipStream_t stream, WordScratch *ws = nullptr);
 // bad_index != null: every packet is first checked against [0, arena_len) (hipErrorInvalidValue
 // and *bad_index = the first one outside)
 hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                hipStream_t stream, uint64_t arena_len = 0, size_t *bad_index = nullptr,
-                               bool overlap_previous = false);
+                               bool overlap_previous = false, WordScratch *ws = nullptr);
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream);

@@ -77,7 +77,7 @@ bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32
 
 hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc, bool verify, int check_short_tail,
                                  unsigned long long *result, const uint32_t *d_tables, const uint32_t *d_fold,
-                                 int grid_cap, hipStream_t stream) {
+                                 int grid_cap, hipStream_t stream, WordScratch *ws) {
 #if HDFS3_LAB
     if (g_variant == 54) return hipErrorNotSupported;  // A/B: force the segmented kernel
 #endif
@@ -105,14 +105,28 @@ hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc
     a.npk = n;
     a.upp_log2 = upp_log2;
     a.last_len = uint32_t(h_seg[n - 1].len);
-    return launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream);
+    return launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream, ws);
 }
 
-hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
+namespace {
+
+// packet p's `words` bytes (`last` for the last packet) from src + p * src_pitch to
+// dst + p * dst_pitch: one wave per packet at a time, 64 consecutive words per store
+__global__ __launch_bounds__(256) void crc32c_scatter_words_kernel(const uint8_t *__restrict__ src, uint8_t *dst,
+                                                                   uint64_t src_pitch, uint64_t dst_pitch,
+                                                                   uint64_t npk, uint32_t words, uint32_t last) {
+    const uint64_t nwaves = uint64_t(gridDim.x) * 4;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t p = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); p < npk; p += nwaves) {
+        const uint32_t nw = (p + 1 == npk ? last : words) / 4;
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(src + p * src_pitch);
+        uint32_t *d = reinterpret_cast<uint32_t *>(dst + p * dst_pitch);
+        for (uint32_t i = lane; i < nw; i += 64) d[i] = s[i];
+    }
+}
+
+hipError_t launch_stream_kernel(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
                                 int grid_cap, hipStream_t stream) {
-#if HDFS3_LAB
-    if (g_variant == 52 || g_variant == 53) return hipErrorNotSupported;  // A/B: force the segmented kernel
-#endif
     switch (a.bpc) {
     case 512: return launch_pv<512>(a, verify, d_tables, d_fold, grid_cap, stream);
     case 1024: return launch_pv<1024>(a, verify, d_tables, d_fold, grid_cap, stream);
@@ -120,6 +134,60 @@ hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_
     case 4096: return launch_pv<4096>(a, verify, d_tables, d_fold, grid_cap, stream);
     default: return hipErrorInvalidValue;
     }
+}
+
+}  // namespace
+
+void WordScratch::release() {
+    if (d) (void)hipFree(d);
+    if (used) (void)hipEventDestroy(used);
+    *this = WordScratch();
+}
+
+hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
+                                int grid_cap, hipStream_t stream, WordScratch *ws) {
+#if HDFS3_LAB
+    if (g_variant == 52 || g_variant == 53) return hipErrorNotSupported;  // A/B: force the segmented kernel
+    if (g_variant == 55) ws = nullptr;  // A/B: words written in place (no dense scratch)
+#endif
+    if (a.bpc != 512 && a.bpc != 1024 && a.bpc != 2048 && a.bpc != 4096) return hipErrorInvalidValue;
+    const uint64_t cpitch = a.crc_pitch ? a.crc_pitch : a.pitch;
+    const uint64_t wpp = (uint64_t(kRoundBytes) << a.upp_log2) / a.bpc * 4;  // word bytes per packet
+    if (!verify && ws && a.npk > 1 && cpitch > wpp && wpp <= kDenseWordsMaxRegion) {
+        const uint64_t last = (uint64_t(a.last_len) + a.bpc - 1) / a.bpc * 4;
+        const uint64_t need = (a.npk - 1) * wpp + last;
+        if (need > ws->cap) {
+            // the old scratch may still be read by a launch in flight (any stream)
+            if (ws->used) {
+                hipError_t e = hipEventSynchronize(ws->used);
+                if (e != hipSuccess) return e;
+            }
+            if (ws->d) (void)hipFree(ws->d);
+            ws->d = nullptr;
+            ws->cap = 0;
+            hipError_t e = hipMalloc(reinterpret_cast<void **>(&ws->d), need);
+            if (e != hipSuccess) return e;
+            ws->cap = need;
+        }
+        if (!ws->used) {
+            hipError_t e = hipEventCreateWithFlags(&ws->used, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        ChunkLaunch b = a;
+        b.out_be = ws->d;
+        b.crc_be = ws->d;
+        b.crc_pitch = wpp;
+        hipError_t e = launch_stream_kernel(b, false, d_tables, d_fold, grid_cap, stream);
+        if (e != hipSuccess) return e;
+        const uint64_t need_waves = a.npk, cap_waves = 4096;
+        const int grid = int(((need_waves < cap_waves ? need_waves : cap_waves) + 3) / 4);
+        hipLaunchKernelGGL(crc32c_scatter_words_kernel, dim3(grid), dim3(256), 0, stream, ws->d, a.out_be, wpp, cpitch,
+                           a.npk, uint32_t(wpp), uint32_t(last));
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return hipEventRecord(ws->used, stream);
+    }
+    return launch_stream_kernel(a, verify, d_tables, d_fold, grid_cap, stream);
 }
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
@@ -251,7 +319,8 @@ hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t unit
 hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
-                               hipStream_t stream, uint64_t arena_len, size_t *bad_index, bool overlap_previous) {
+                               hipStream_t stream, uint64_t arena_len, size_t *bad_index, bool overlap_previous,
+                               WordScratch *ws) {
     if (n == 0) return hipSuccess;
     // one pass: descriptors, the alignment test of segments_fast and the unit plan of
     // plan_segments (16K packets per GiB: the host loop is on the call's critical path)
@@ -298,7 +367,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         a.upp_log2 = upp_log2;
         a.last_len = h_pk[n - 1].data_len;
         a.overlap_previous = overlap_previous && verify;
-        const hipError_t e = launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream);
+        const hipError_t e = launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream, ws);
         if (e != hipErrorNotSupported) return e;
     }
     if (fast && strided && same && u0 > 0 && n > kInlineSegments) {

@@ -97,9 +97,6 @@ struct hdfs3_crc_ctx {
     const uint32_t *fold_host = nullptr;  // host fold matrices of checksum_type (ChunkLaunch::fold_host)
     unsigned long long *d_result = nullptr;
     unsigned long long *h_result = nullptr;  // pinned
-    hdfs3crc::DevSegment *d_pk = nullptr;              // packets-API descriptor staging
-    hdfs3crc::DevSegment *h_pk = nullptr;              // pinned
-    size_t pk_cap = 0;
     // blocks API: a ring of descriptor stagings, each reusable once its event fired
     struct SegStage {
         hdfs3crc::DevSegment *h = nullptr, *d = nullptr;
@@ -107,6 +104,7 @@ struct hdfs3_crc_ctx {
         hipEvent_t done = nullptr;
     } seg_ring[4];
     unsigned seg_next = 0;
+    hdfs3crc::WordScratch words;  // dense CRC words of compute over in-packet word regions
     hdfs3crc::Slot slot[2];
     std::atomic<uint64_t> launches{0};
     std::mutex arena_mu;                          // guards arena_cache

@@ -121,20 +121,6 @@ int grow_slot(Slot &s, size_t data_bytes, size_t crc_bytes) {
     return 0;
 }
 
-int grow_pk(hdfs3_crc_ctx *ctx, size_t n) {
-    if (n <= ctx->pk_cap) return 0;
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    if (ctx->d_pk) (void)hipFree(ctx->d_pk);
-    if (ctx->h_pk) (void)hipHostFree(ctx->h_pk);
-    ctx->d_pk = nullptr;
-    ctx->h_pk = nullptr;
-    ctx->pk_cap = 0;
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&ctx->d_pk), n * sizeof(DevSegment)));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_pk), n * sizeof(DevSegment), hipHostMallocDefault));
-    ctx->pk_cap = n;
-    return 0;
-}
-
 int finish_pending(Slot &s) {
     if (s.pending_out) {
         HIP_TRY(hipEventSynchronize(s.done));
@@ -260,7 +246,7 @@ int packets_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len, 
     size_t bad = 0;
     const hipError_t e = launch_packet_batch(d_arena, hp, n, bpc, verify, check_short_tail, d_result, st->h, st->d,
                                              ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, arena_len,
-                                             &bad, overlap);
+                                             &bad, overlap, &ctx->words);
     if (e == hipErrorInvalidValue) return fail(-EINVAL, "packet %zu lies outside the %zu-byte arena", bad, arena_len);
     HIP_TRY(e);
     ++ctx->launches;
@@ -319,7 +305,8 @@ int packet_stream_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena
         a.upp_log2 = upp_log2;
         a.last_len = ps->last_len;
         a.overlap_previous = overlap && verify;
-        const hipError_t e = launch_packet_stream(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream);
+        const hipError_t e =
+            launch_packet_stream(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, &ctx->words);
         if (e != hipErrorNotSupported) {
             HIP_TRY(e);
             ++ctx->launches;
@@ -367,7 +354,7 @@ int blocks_common(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, u
     // blocks of one 2-D tensor (constant data and word strides, equal whole-round blocks): the
     // wave kernel walks them directly (pitch mode); everything else: the segmented kernel
     const hipError_t te = launch_strided_blocks(st->h, n, bpc, verify, check_short_tail, d_result, ctx->d_tables,
-                                                ctx->d_fold, ctx->grid_cap, ctx->stream);
+                                                ctx->d_fold, ctx->grid_cap, ctx->stream, &ctx->words);
     if (te != hipErrorNotSupported) {
         HIP_TRY(te);
         ++ctx->launches;
@@ -518,8 +505,7 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx) {
         if (st.d) (void)hipFree(st.d);
         if (st.done) (void)hipEventDestroy(st.done);
     }
-    if (ctx->d_pk) (void)hipFree(ctx->d_pk);
-    if (ctx->h_pk) (void)hipHostFree(ctx->h_pk);
+    ctx->words.release();
     for (int p = 0; p < 2; ++p) {
         if (ctx->d_tables_by[p]) (void)hipFree(ctx->d_tables_by[p]);
         if (ctx->d_fold_by[p]) (void)hipFree(ctx->d_fold_by[p]);

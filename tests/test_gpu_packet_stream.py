@@ -173,3 +173,28 @@ def test_overlapped_stream_chain_and_large_stream(gpu_ctx):
             assert (key >> 32, key & 0xFFFFFFFF) == (p_bad, q_bad // bpc), i
         else:
             assert w == 0, i
+
+
+def test_compute_word_scratch_grows_across_calls(gpu_ctx):
+    """Compute over in-packet words goes through the ctx's dense word scratch and a scatter
+    kernel. Streams of growing length on one ctx (the scratch is reallocated between them, after
+    the previous use completed), each with a short last packet: every packet's words equal the
+    oracle's and no other byte of the arena changes."""
+    from libhdfs3_amd.engine import CrcContext
+
+    bpc, plen = 512, 16384
+    for n, last in [(3, plen), (40, plen - 700), (300, 1), (40, 4096)]:
+        arena, pitch, crc_off, data_off, datas = build_arena(n, plen, last, bpc, 4000 + n)
+        blank = arena.copy()
+        for i in range(n):
+            blank[i * pitch + crc_off:i * pitch + data_off] = 0xA5
+        d = gpu_ctx.upload(blank)
+        ps = CrcContext.packet_stream(crc_off, data_off, pitch, n, plen, last)
+        gpu_ctx.compute_packet_stream_async(d.ptr, arena.nbytes, ps, bpc)
+        got = gpu_ctx.download(d, arena.nbytes)
+        # the words of a short last packet end before its region does: the rest keeps 0xA5
+        want = arena.copy()
+        lw = 4 * (-(-last // bpc))
+        want[(n - 1) * pitch + crc_off + lw:(n - 1) * pitch + data_off] = 0xA5
+        assert np.array_equal(got, want), (n, last)
+

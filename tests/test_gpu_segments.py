@@ -235,7 +235,9 @@ def test_constant_pitch_packets_without_descriptors(lab_ctx, bpc, last_len):
 def test_strided_blocks_take_the_wave_kernel(lab_ctx, bpc, last):
     """Blocks of one 2-D arrangement (data at a constant stride, words at another; the bench's
     [blocks, bytes] tensor) go to the wave kernel's pitch mode with its own word pitch (variant
-    0); the segmented kernel (variant 54) and the oracle must agree on every word and key."""
+    0); the segmented kernel (variant 54) and the oracle must agree on every word and key. Compute
+    writes the words densely into the ctx's scratch and scatters them (variant 55: in place); no
+    byte between the word regions may change."""
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import DeviceBuffer
 
@@ -248,18 +250,21 @@ def test_strided_blocks_take_the_wave_kernel(lab_ctx, bpc, last):
         lab_ctx.upload(d, dbuf, offset=i * dstride)
     blocks = [(dbuf.ptr + i * dstride, wbuf.ptr + i * wstride, d.size) for i, d in enumerate(datas)]
     try:
-        for v in (0, 54):
+        for v in (0, 54, 55):
             lib.hdfs3x_set_variant(v)
-            lab_ctx.memset(wbuf, 0, n * wstride)
+            lab_ctx.memset(wbuf, 0xA5, n * wstride)
             lab_ctx.compute_blocks_dev(blocks, bpc)
+            got = lab_ctx.download(wbuf, n * wstride)
             for i, d in enumerate(datas):
                 want = oracle_compute(d, bpc)
-                assert np.array_equal(lab_ctx.download(wbuf.ptr + i * wstride, want.nbytes), want), (v, i)
+                assert np.array_equal(got[i * wstride:i * wstride + want.nbytes], want), (v, i)
+                end = (i + 1) * wstride if i + 1 < n else n * wstride
+                assert (got[i * wstride + want.nbytes:end] == 0xA5).all(), (v, i)
             assert lab_ctx.verify_blocks_dev(blocks, bpc, True) == (-1, -1), v
         for bi, pos in [(n - 1, last - 1), (2, 4096 * 9 + 3), (0, 0)]:
             lab_ctx.upload(np.array([datas[bi][pos] ^ 0x80], np.uint8), dbuf, offset=bi * dstride + pos)
             got = set()
-            for v in (0, 54):
+            for v in (0, 54, 55):
                 lib.hdfs3x_set_variant(v)
                 got.add(lab_ctx.verify_blocks_dev(blocks, bpc, True))
             assert got == {(bi, pos // bpc)}, (bi, pos, got)
