@@ -68,6 +68,27 @@ def main():
         lib.hdfs3_crc32c_compute_packet_stream_dev_async(ctx.ctx, a0, arena.numel(), ps_ref, bpc)
         lib.hdfs3x_set_variant(0)
     cases["pitch_data/in_packet_words (packet stream, in place: variant 55)"] = in_place_stream
+    # writer-shaped wire packets (127 chunks = 65,024 B of data, not whole 4 KiB rounds): the
+    # segmented kernel, words in each packet vs in one array
+    wl = 127 * bpc
+    wn = (1 << 30) // wl
+    wwords = 127 * 4
+    wpitch = 32 + wwords + wl
+    wpitch += (-wpitch) % 16
+    warena = torch.randint(0, 256, (wn * wpitch,), dtype=torch.uint8, device="cuda")
+    wdense = torch.zeros(wn * wwords, dtype=torch.uint8, device="cuda")
+    wa0, wd0 = warena.data_ptr(), wdense.data_ptr()
+    wdata_off = wpitch - wl
+    wps = CrcContext.packet_stream(wdata_off - wwords, wdata_off, wpitch, wn, wl)
+    wps_ref = ctypes.byref(wps)
+    cases["wire 65,024 B packets: in_packet_words (packet stream -> segmented kernel)"] = \
+        lambda: lib.hdfs3_crc32c_compute_packet_stream_dev_async(ctx.ctx, wa0, warena.numel(), wps_ref, bpc)
+    pk_w_in = ctx._blocks([(wa0 + i * wpitch + wdata_off, wa0 + i * wpitch + wdata_off - wwords, wl) for i in range(wn)])
+    pk_w_dense = ctx._blocks([(wa0 + i * wpitch + wdata_off, wd0 + i * wwords, wl) for i in range(wn)])
+    cases["wire 65,024 B packets: in_packet_words (blocks API, segmented)"] = \
+        lambda: _native.check("compute_blocks", lib.hdfs3_crc32c_compute_blocks_dev(ctx.ctx, pk_w_in, wn, bpc))
+    cases["wire 65,024 B packets: contiguous_words (blocks API, segmented)"] = \
+        lambda: _native.check("compute_blocks", lib.hdfs3_crc32c_compute_blocks_dev(ctx.ctx, pk_w_dense, wn, bpc))
     torch.cuda.synchronize()
 
     def timed(fn, reps=10):
