@@ -728,6 +728,20 @@ constexpr int kTailFoldOff = kLdsBytes + 16 * 1024;  // 144 KiB: M_32 nibble ima
 //    CUs alternate heavy/light and their launch heads — dispatch, fill, first-data latency,
 //    when a CU pulls no HBM bytes — no longer line up across the chip.
 constexpr int kOptSkew = 8388608;
+//  kOptDiagTail (diagnostic only, wrong results): a wave's last step replaces the table CRC by an
+//    xor of its words, so the compute that runs after the wave's last data arrived is ~free. The
+//    difference to production is what the per-launch tail costs.
+constexpr int kOptDiagTail = 16777216;
+//  kOptSoloTail: the wave's last two rounds run one after the other as single chains (no
+//    interleave), so the first one's lookups overlap the second one's arrival.
+constexpr int kOptSoloTail = 33554432;
+//  kOptDiagTailLut (diagnostic only, with kOptDiagTail): the last step keeps its 64 lookups per
+//    round but drops their dependency chain (independent lookups of the data words): separates
+//    the tail's LDS work from its latency.
+constexpr int kOptDiagTailLut = 67108864;
+//  kOptSoloHalf (with kOptSoloTail): the wave's very last round as two interleaved 32-byte half
+//    chains joined in VALU (x = M_32(x_a) ^ x_b): half the dependent lookups after the last data.
+constexpr int kOptSoloHalf = 134217728;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
@@ -972,8 +986,9 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         const uint64_t u = uk(k);
         const uint32_t c = ~y;
         if constexpr (VERIFY) {
-            const bool bad = (OPT & (kOptNoHbm | kOptNoFill | kOptNoMath | kOptFakeLut)) != 0 ? __builtin_bswap32(want) == ~c
-                                                                               : __builtin_bswap32(want) != c;
+            const bool bad = (OPT & (kOptNoHbm | kOptNoFill | kOptNoMath | kOptFakeLut | kOptDiagTail)) != 0
+                                   ? __builtin_bswap32(want) == ~c
+                                   : __builtin_bswap32(want) != c;
             if (bad) atomicMax(a.result, ~(unsigned long long)key_of(u, lane / G));
         } else if constexpr ((OPT & kOptNoStore) != 0) {
             if (c == 0x9E3779B9u) *reinterpret_cast<uint32_t *>(word_ptr(u, lane / G)) = c;
@@ -1004,7 +1019,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         }
     } else {
         constexpr int PF = (OPT & kOptPf2) != 0 ? 2 : 1;  // steps of loads in flight
-        auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint64_t k, auto do_pf) {
+        auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint64_t k, auto do_pf, auto do_math) {
             constexpr bool kPf = decltype(do_pf)::value;
             const uint32_t w0 = want_of(k), w1 = want_of(k + 1);
             constexpr bool kLate = (OPT & kOptLate) != 0 || !kPf, kSplit = (OPT & kOptSplit) != 0;
@@ -1020,7 +1035,17 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                 __builtin_amdgcn_sched_barrier(0);
             }
             uint32_t x0 = init ^ word(c0, 0), x1 = init ^ word(c1, 0);
-            if constexpr ((OPT & kOptNoMath) != 0) {
+            if constexpr ((OPT & kOptDiagTailLut) != 0 && !decltype(do_math)::value) {
+                // diagnostic: the same 64 lookups per round with no dependency chain
+                uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    a0 ^= combine(lookups(t, word(c0, i)), 0u);
+                    a1 ^= combine(lookups(t, word(c1, i)), 0u);
+                }
+                x0 ^= a0;
+                x1 ^= a1;
+            } else if constexpr ((OPT & kOptNoMath) != 0 || !decltype(do_math)::value) {
 #pragma unroll
                 for (int i = 1; i < 16; ++i) {
                     x0 ^= word(c0, i);
@@ -1074,6 +1099,8 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         };
         using pf_on = std::integral_constant<bool, true>;
         using pf_off = std::integral_constant<bool, false>;
+        using math_on = std::integral_constant<bool, true>;
+        using math_off = std::integral_constant<bool, false>;
         // kFastTail: the wave's last step, no prefetch, four half-round chains
         auto tail = [&](Round &c0, Round &c1, uint64_t k) {
             const uint32_t w0 = want_of(k), w1 = want_of(k + 1);
@@ -1112,43 +1139,117 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
                     tail(b[0], b[1], k);
                     break;
                 }
-                step(b[0], b[1], b[2], b[3], k, pf_on{});
+                step(b[0], b[1], b[2], b[3], k, pf_on{}, math_on{});
                 if (k == 0) stamp(2);
                 if (k + 4 >= K) {
                     tail(b[2], b[3], k + 2);
                     break;
                 }
-                step(b[2], b[3], b[0], b[1], k + 2, pf_on{});
+                step(b[2], b[3], b[0], b[1], k + 2, pf_on{}, math_on{});
             }
         } else if constexpr (kHead2) {
             // step 0 consumes b0/b1 without a prefetch (b2/b3 already hold step 1), then the
             // usual one-step-ahead rotation from step 1 on
             if (K > 0) {
-                step(b[0], b[1], b[2], b[3], 0, pf_off{});
+                step(b[0], b[1], b[2], b[3], 0, pf_off{}, math_on{});
                 stamp(2);
             }
             for (uint64_t k = 2; k < K; k += 4) {
-                step(b[2], b[3], b[0], b[1], k, pf_on{});
+                step(b[2], b[3], b[0], b[1], k, pf_on{}, math_on{});
                 if (k + 2 >= K) break;
-                step(b[0], b[1], b[2], b[3], k + 2, pf_on{});
+                step(b[0], b[1], b[2], b[3], k + 2, pf_on{}, math_on{});
+            }
+        } else if constexpr (PF == 1 && (OPT & kOptSoloTail) != 0) {
+            // the wave's last two rounds one after the other, each as a single chain: round k's
+            // chain runs while round k + 1 is still arriving, and only one round's lookups
+            // remain once the wave's last data has landed
+            auto solo = [&](Round &c, uint64_t k) {
+                const uint32_t w = want_of(k);
+                __builtin_amdgcn_sched_barrier(0);
+                regroup(c);
+                uint32_t x = init ^ word(c, 0);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x = combine(lookups(t, x), i < 15 ? word(c, i < 15 ? i + 1 : 15) : 0u);
+                finish(k, group_xor<G>(fold(x)), w);
+            };
+            // kOptSoloHalf: the very last round as two 32-byte half chains, interleaved, joined by
+            // x = M_32(x_a) ^ x_b with M_32 as a 32-column GF(2) product in VALU (columns read once
+            // from the ctx's M_32 nibble image: word (i / 4) * 16 + (1 << i % 4) = M_32(1 << i))
+            uint32_t m32c[(OPT & kOptSoloHalf) != 0 ? 32 : 1];
+            if constexpr ((OPT & kOptSoloHalf) != 0) {
+#pragma unroll
+                for (int i = 0; i < 32; ++i) m32c[i] = a.m32[(i >> 2) * 16 + (1u << (i & 3))];
+            }
+            auto solo_last = [&](Round &c, uint64_t k) {
+                if constexpr ((OPT & kOptSoloHalf) != 0) {
+                    const uint32_t w = want_of(k);
+                    __builtin_amdgcn_sched_barrier(0);
+                    regroup(c);
+                    uint32_t xa = init ^ word(c, 0), xb = word(c, 8);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const Look la = lookups(t, xa), lb = lookups(t, xb);
+                        xa = combine(la, i < 7 ? word(c, i < 7 ? i + 1 : 7) : 0u);
+                        xb = combine(lb, i < 7 ? word(c, i < 7 ? i + 9 : 15) : 0u);
+                    }
+                    finish(k, group_xor<G>(fold(gf2_apply4(m32c, xa) ^ xb)), w);
+                } else {
+                    solo(c, k);
+                }
+            };
+            for (uint64_t k = 0; k < K; k += 4) {
+                if (k + 2 >= K) {
+                    if (k + 1 < K) {
+                        solo(b[0], k);
+                        solo_last(b[1], k + 1);
+                    } else {
+                        solo_last(b[0], k);
+                    }
+                    break;
+                }
+                step(b[0], b[1], b[2], b[3], k, pf_on{}, math_on{});
+                if (k + 4 >= K) {
+                    if (k + 3 < K) {
+                        solo(b[2], k + 2);
+                        solo_last(b[3], k + 3);
+                    } else {
+                        solo_last(b[2], k + 2);
+                    }
+                    break;
+                }
+                step(b[2], b[3], b[0], b[1], k + 2, pf_on{}, math_on{});
+            }
+        } else if constexpr (PF == 1 && (OPT & kOptDiagTail) != 0) {
+            // diagnostic: a wave's last step skips the table CRC (wrong results on purpose)
+            for (uint64_t k = 0; k < K; k += 4) {
+                if (k + 2 >= K) {
+                    step(b[0], b[1], b[2], b[3], k, pf_on{}, math_off{});
+                    break;
+                }
+                step(b[0], b[1], b[2], b[3], k, pf_on{}, math_on{});
+                if (k + 4 >= K) {
+                    step(b[2], b[3], b[0], b[1], k + 2, pf_on{}, math_off{});
+                    break;
+                }
+                step(b[2], b[3], b[0], b[1], k + 2, pf_on{}, math_on{});
             }
         } else if constexpr (PF == 1) {
             for (uint64_t k = 0; k < K; k += 4) {
                 prio(k);
-                step(b[0], b[1], b[2], b[3], k, pf_on{});
+                step(b[0], b[1], b[2], b[3], k, pf_on{}, math_on{});
                 if (k == 0) stamp(2);
                 if (k + 2 >= K) break;
                 prio(k + 2);
-                step(b[2], b[3], b[0], b[1], k + 2, pf_on{});
+                step(b[2], b[3], b[0], b[1], k + 2, pf_on{}, math_on{});
             }
         } else {
             for (uint64_t k = 0; k < K; k += 6) {
-                step(b[0], b[1], b[4], b[5], k, pf_on{});
+                step(b[0], b[1], b[4], b[5], k, pf_on{}, math_on{});
                 if (k == 0) stamp(2);
                 if (k + 2 >= K) break;
-                step(b[2], b[3], b[0], b[1], k + 2, pf_on{});
+                step(b[2], b[3], b[0], b[1], k + 2, pf_on{}, math_on{});
                 if (k + 4 >= K) break;
-                step(b[4], b[5], b[2], b[3], k + 4, pf_on{});
+                step(b[4], b[5], b[2], b[3], k + 4, pf_on{}, math_on{});
             }
         }
     }
@@ -1841,7 +1942,7 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         const uint64_t units = (OPT & kOptPitch) != 0 ? ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes
                                                       : a.len / kRoundBytes;
         ChunkLaunch la = a;
-        if constexpr ((OPT & kOptFastTail) != 0) la.m32 = fold + kFoldM32Off;
+        if constexpr ((OPT & (kOptFastTail | kOptSoloHalf)) != 0) la.m32 = fold + kFoldM32Off;
         const uint64_t need = (units + PAIR * kWavesPerBlock - 1) / (PAIR * kWavesPerBlock);
         int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
         if (grid < 1) grid = 1;

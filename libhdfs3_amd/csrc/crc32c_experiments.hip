@@ -136,6 +136,21 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptFastTail>(a, tab, fold, grid_cap, s);
     case 73:  // production + uneven work per workgroup (kOptSkew)
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptSkew>(a, tab, fold, grid_cap, s);
+    case 76:  // diagnostic: production with the last step's table CRC skipped (kOptDiagTail)
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptDiagTail>(a, tab, fold, grid_cap, s);
+    case 78:  // production + the last two rounds as single chains, one after the other (kOptSoloTail)
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptSoloTail>(a, tab, fold, grid_cap, s);
+    case 79:  // 78 with held compute stores (compute at 512: the production store path)
+        return launch_wave<BPC, V, 2, true, true, false, false, false,
+                           kOptLeanFill | kOptSoloTail | (!V && BPC == 512 ? kOptHoldStore : 0)>(a, tab, fold, grid_cap, s);
+    case 80:  // diagnostic: 76, but the last step's lookups are issued without their chain
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptDiagTail | kOptDiagTailLut>(
+            a, tab, fold, grid_cap, s);
+    case 82:  // 78 + the very last round as two half chains joined in VALU (kOptSoloHalf)
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptSoloTail | kOptSoloHalf>(
+            a, tab, fold, grid_cap, s);
+    case 77:  // diagnostic: production with every step's table CRC skipped (lean-fill variant 24)
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOptLeanFill | kOptNoMath>(a, tab, fold, grid_cap, s);
     case 74:    // two 512-thread workgroups per CU, slice-by-2 tables (crc32c_wave2.h)
     case 75: {  // the same kernel, one workgroup per CU per launch (grid = CUs)
         if constexpr (BPC <= 2048) {

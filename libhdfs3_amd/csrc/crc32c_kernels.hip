@@ -12,6 +12,8 @@ uint64_t *g_trace = nullptr;  // timestamp buffer of the traced variants
 
 namespace {
 
+constexpr uint64_t kSoloTailMaxBytes = uint64_t(256) << 20;
+
 template <int BPC, bool V>
 hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                     hipStream_t s) {
@@ -28,8 +30,20 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
     if (g_variant != 0) return launch_experiment(g_variant, a, V, tab, fold, grid_cap, s);
 #endif
     constexpr int kOpt = (BPC <= kRoundBytes ? kOptLeanFill : 0) | (!V && BPC == 512 ? kOptHoldStore : 0);
-    if (a.overlap_previous)
+    if (a.overlap_previous) {
+        // Overlapped verifies up to 256 MiB per launch end with the wave's last two rounds as
+        // single chains one after the other (kOptSoloTail, variant 78): a CU's workgroup frees
+        // its slot for the next launch sooner when less lookup work is left after its last data
+        // landed. 128 MiB: 21.94 -> 21.34 us per launch at bpc 512, 22.37 -> 21.60 at 2048; at
+        // 1 GiB per launch it is 1 % slower, and barriered launches lose 0.9 us, so both keep
+        // the interleaved last step (profiles/r02_kernel_study/r02_ab_solo_*.jsonl).
+        if constexpr (V && BPC <= kRoundBytes) {
+            if (a.len <= kSoloTailMaxBytes)
+                return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt | kOptSoloTail>(a, tab, fold,
+                                                                                                  grid_cap, s);
+        }
         return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
+    }
     return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
 }
 

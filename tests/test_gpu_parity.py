@@ -242,7 +242,7 @@ def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
 # every bit-exact variant (diagnostic variants 9-13, 15, 19, 21-25, 29, 34, 35, 37, 38, 41 time
 # or trace and give wrong results on purpose)
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 14, 16, 18, 20, 26, 27, 28, 30, 31, 32, 33, 36, 40, 42, 43, 44, 46, 47, 48,
-                                     60, 61, 70, 72, 73, 74, 75])
+                                     60, 61, 70, 72, 73, 74, 75, 78, 79, 82])
 @pytest.mark.parametrize("bpc", [512, 1024, 2048, 4096, 8192])
 def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
     """All kernel designs kept for A/B (hdfs3x_set_variant) are parity-checked too:
