@@ -1175,13 +1175,13 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
             // kOptSoloHalf: the very last round as two 32-byte half chains, interleaved, joined by
             // x = M_32(x_a) ^ x_b with M_32 as a 32-column GF(2) product in VALU (columns read once
             // from the ctx's M_32 nibble image: word (i / 4) * 16 + (1 << i % 4) = M_32(1 << i))
-            uint32_t m32c[(OPT & kOptSoloHalf) != 0 ? 32 : 1];
-            if constexpr ((OPT & kOptSoloHalf) != 0) {
-#pragma unroll
-                for (int i = 0; i < 32; ++i) m32c[i] = a.m32[(i >> 2) * 16 + (1u << (i & 3))];
-            }
             auto solo_last = [&](Round &c, uint64_t k) {
                 if constexpr ((OPT & kOptSoloHalf) != 0) {
+                    // wave-uniform columns, loaded here so they are live only in the last round
+                    uint32_t m32c[32];
+#pragma unroll
+                    for (int i = 0; i < 32; ++i)
+                        m32c[i] = __builtin_amdgcn_readfirstlane(a.m32[(i >> 2) * 16 + (1u << (i & 3))]);
                     const uint32_t w = want_of(k);
                     __builtin_amdgcn_sched_barrier(0);
                     regroup(c);
