@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Clock / power during sustained loads: is the 128 MiB verify launch rate set by the GPU's
+clocks under its power limit?
+
+Launch-level kernel traces of the driver's bench command (K=20 after an idle gap) show
+single 128 MiB verifies at 19.2-19.7 us, the same-shape plain-read rate, while the same
+launches sustained over thousands of steps average ~21 us. This tool runs phases of
+back-to-back overlapped launches (verify, then the plain-read kernel of the lab library, the
+same arena and launch shape as bench.py's ceiling), each `--seconds` long with idle gaps
+between, and records
+  * the per-launch time of every batch of 100 launches (HIP events), against time;
+  * `amd-smi metric` samples (clocks, power) from a sampler thread, raw JSON per sample.
+One JSON line per batch and per sample on stdout.
+
+    python tools/clock_probe.py --seconds 3
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def sampler(stop, t0, out, period):
+    cmds = [["amd-smi", "metric", "-g", "0", "--json"], ["rocm-smi", "-d", "0", "--showclocks", "--showpower", "--json"]]
+    cmd = None
+    for c in cmds:
+        try:
+            r = subprocess.run(c, capture_output=True, text=True, timeout=10)
+            if r.returncode == 0 and r.stdout.strip():
+                cmd = c
+                break
+        except Exception:
+            continue
+    if cmd is None:
+        out.append({"smi": "unavailable"})
+        return
+    while not stop.is_set():
+        ts = time.perf_counter() - t0
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=10)
+            raw = r.stdout
+            try:
+                val = json.loads(raw)
+            except Exception:
+                val = raw[-4000:]
+            out.append({"t": round(ts, 3), "t_end": round(time.perf_counter() - t0, 3), "tool": cmd[0], "smi": val})
+        except Exception as e:  # noqa: BLE001 - recorded
+            out.append({"t": round(ts, 3), "error": str(e)})
+        stop.wait(period)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=3.0)
+    ap.add_argument("--idle", type=float, default=1.0)
+    ap.add_argument("--period", type=float, default=0.1)
+    args = ap.parse_args()
+
+    import torch
+    import bench
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import CrcContext
+
+    dev = torch.device("cuda", 0)
+    ctx = CrcContext(0)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    work = bench.Workload(torch, ctx, dev, 128 << 20, 8, 512, seed=1234)
+    lab = bench.lab_context(work, stream)
+    lib = _native.lab()
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    result = torch.zeros(100, dtype=torch.int64, device=dev)
+
+    def verify_batch(i0, n):
+        for i in range(n):
+            b = (i0 + i) % work.blocks
+            ctx.verify_dev_async(work.data_ptr(b), work.block_bytes, 512, work.crc_ptr(b),
+                                 result.data_ptr() + 8 * (i % 100), overlap_previous=i > 0)
+
+    def read_batch(i0, n):
+        for i in range(n):
+            b = (i0 + i) % work.blocks
+            lib.hdfs3x_stream_read_ex(lab.ctx, work.data_ptr(b), work.block_bytes, 256, sink.data_ptr(), int(i > 0))
+
+    lines, samples = [], []
+    stop = threading.Event()
+    t0 = time.perf_counter()
+    th = threading.Thread(target=sampler, args=(stop, t0, samples, args.period), daemon=True)
+    th.start()
+    time.sleep(args.idle)
+    for phase, fn in (("verify", verify_batch), ("plain_read", read_batch), ("verify2", verify_batch)):
+        end = time.perf_counter() + args.seconds
+        i = 0
+        while time.perf_counter() < end:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn(i, 100)
+            e1.record(stream)
+            e1.synchronize()
+            lines.append({"phase": phase, "t": round(time.perf_counter() - t0, 4), "batch": i // 100,
+                          "us_per_launch": round(e0.elapsed_time(e1) * 1e3 / 100, 3)})
+            i += 100
+        if phase == "verify" or phase == "verify2":
+            if bool((result != 0).any().item()):
+                raise SystemExit("clean blocks reported bad")
+        time.sleep(args.idle)
+    stop.set()
+    th.join(timeout=15)
+    for ln in lines:
+        print(json.dumps(ln))
+    for s in samples:
+        print(json.dumps({"sample": s}))
+
+
+if __name__ == "__main__":
+    main()
