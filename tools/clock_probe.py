@@ -5,8 +5,8 @@ clocks under its power limit?
 Launch-level kernel traces of the driver's bench command (K=20 after an idle gap) show
 single 128 MiB verifies at 19.2-19.7 us, the same-shape plain-read rate, while the same
 launches sustained over thousands of steps average ~21 us. This tool runs phases of
-back-to-back overlapped launches (verify, then the plain-read kernel of the lab library, the
-same arena and launch shape as bench.py's ceiling), each `--seconds` long with idle gaps
+back-to-back overlapped launches (verify kernel variants of the lab library, the plain-read
+kernel: the same arena and launch shape as bench.py's ceiling), each `--seconds` long with idle gaps
 between, and records
   * the per-launch time of every batch of 100 launches (HIP events), against time;
   * `amd-smi metric` samples (clocks, power) from a sampler thread, raw JSON per sample.
@@ -61,6 +61,10 @@ def main():
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--idle", type=float, default=1.0)
     ap.add_argument("--period", type=float, default=0.1)
+    ap.add_argument("--phases", default="v0,read,v0",
+                    help="comma list: vN = verify through the lab library with kernel variant N "
+                         "(0 = production; diagnostic variants give wrong results on purpose), "
+                         "read / readnt = the plain-read kernel, default / non-temporal loads")
     args = ap.parse_args()
 
     import torch
@@ -82,13 +86,13 @@ def main():
     def verify_batch(i0, n):
         for i in range(n):
             b = (i0 + i) % work.blocks
-            ctx.verify_dev_async(work.data_ptr(b), work.block_bytes, 512, work.crc_ptr(b),
+            lab.verify_dev_async(work.data_ptr(b), work.block_bytes, 512, work.crc_ptr(b),
                                  result.data_ptr() + 8 * (i % 100), overlap_previous=i > 0)
 
-    def read_batch(i0, n):
+    def read_batch(i0, n, grid=256):
         for i in range(n):
             b = (i0 + i) % work.blocks
-            lib.hdfs3x_stream_read_ex(lab.ctx, work.data_ptr(b), work.block_bytes, 256, sink.data_ptr(), int(i > 0))
+            lib.hdfs3x_stream_read_ex(lab.ctx, work.data_ptr(b), work.block_bytes, grid, sink.data_ptr(), int(i > 0))
 
     lines, samples = [], []
     stop = threading.Event()
@@ -96,7 +100,12 @@ def main():
     th = threading.Thread(target=sampler, args=(stop, t0, samples, args.period), daemon=True)
     th.start()
     time.sleep(args.idle)
-    for phase, fn in (("verify", verify_batch), ("plain_read", read_batch), ("verify2", verify_batch)):
+    for k, phase in enumerate(args.phases.split(",")):
+        fn = (read_batch if phase == "read" else
+              (lambda i0, n: read_batch(i0, n, -256)) if phase == "readnt" else verify_batch)
+        if not phase.startswith("read"):
+            lib.hdfs3x_set_variant(int(phase[1:]))
+        result.zero_()
         end = time.perf_counter() + args.seconds
         i = 0
         while time.perf_counter() < end:
@@ -105,12 +114,12 @@ def main():
             fn(i, 100)
             e1.record(stream)
             e1.synchronize()
-            lines.append({"phase": phase, "t": round(time.perf_counter() - t0, 4), "batch": i // 100,
+            lines.append({"phase": phase, "k": k, "t": round(time.perf_counter() - t0, 4), "batch": i // 100,
                           "us_per_launch": round(e0.elapsed_time(e1) * 1e3 / 100, 3)})
             i += 100
-        if phase == "verify" or phase == "verify2":
-            if bool((result != 0).any().item()):
-                raise SystemExit("clean blocks reported bad")
+        if phase == "v0" and bool((result != 0).any().item()):
+            raise SystemExit("clean blocks reported bad")
+        lib.hdfs3x_set_variant(0)
         time.sleep(args.idle)
     stop.set()
     th.join(timeout=15)
