@@ -109,6 +109,16 @@ int hdfs3_input_available(hdfs3_input_stream *s);
 int64_t hdfs3_input_length(hdfs3_input_stream *s);
 /* replica failovers and block readers opened so far (diagnostics) */
 int hdfs3_input_stats(hdfs3_input_stream *s, uint64_t *failovers, uint64_t *readers_opened);
+/* Block read-ahead (opt-in; not in the reference, which reads one block at a time): while
+ * hdfs3_input_read consumes block i, blocks i+1 .. i+blocks are read by background threads,
+ * each over its own connection and pooled GPU context, verified exactly as on demand, into
+ * host buffers of up to max_bytes_per_block (0 = the whole block). read() still returns the
+ * same bytes, at most to the block end per call; a prefetch that hit a ChecksumException or
+ * I/O error hands back the bytes it verified and the stream fails that replica over from
+ * there (readOneBlock). pread is unaffected. blocks = 0 turns it off. 0 or -errno. */
+int hdfs3_input_set_readahead(hdfs3_input_stream *s, int blocks, int64_t max_bytes_per_block);
+/* block readers the read-ahead threads opened so far (diagnostics) */
+int hdfs3_input_readahead_stats(hdfs3_input_stream *s, uint64_t *prefetch_readers_opened);
 int hdfs3_input_close(hdfs3_input_stream *s);
 
 /* ------------------------------------------------------------------------------------

@@ -85,6 +85,10 @@ int hdfs3_fs_set_sink(hdfsFS fs, const char *path, hdfs3_packet_sink sink, void 
  * hdfsOpenFile(O_RDONLY)/hdfsRead read back what was written. Takes precedence over a sink.
  * 0, or -1 with errno (EINVAL). */
 int hdfs3_fs_set_pipeline(hdfsFS fs, const char *path, const hdfs3_located_block *blocks, int n_blocks);
+/* block read-ahead for files opened for reading from now on (hdfs3_input_set_readahead in
+ * hdfs3_client.h; 0 blocks = off, the reference's one-block-at-a-time reading). 0, or -1 with
+ * errno (EINVAL). */
+int hdfs3_fs_set_readahead(hdfsFS fs, int blocks, int64_t max_bytes_per_block);
 
 #ifdef __cplusplus
 }

@@ -197,6 +197,8 @@ CLIENT_API = {
     "hdfs3_input_length": (c_int64, [c_void_p]),
     "hdfs3_input_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "hdfs3_input_close": (c_int, [c_void_p]),
+    "hdfs3_input_set_readahead": (c_int, [c_void_p, c_int, c_int64]),
+    "hdfs3_input_readahead_stats": (c_int, [c_void_p, POINTER(c_uint64)]),
     "hdfs3_local_reader_open": (c_int, [ctypes.c_char_p, ctypes.c_char_p, c_int64, c_int64, POINTER(LocalOpts),
                                         POINTER(c_void_p)]),
     "hdfs3_local_reader_read": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),
@@ -243,6 +245,7 @@ HDFS_API = {
     "hdfs3_fs_add_file": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_int]),
     "hdfs3_fs_set_sink": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_void_p]),
     "hdfs3_fs_set_pipeline": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_int]),
+    "hdfs3_fs_set_readahead": (c_int, [c_void_p, c_int, c_int64]),
 }
 
 # measurement hooks (libhdfs3_crc_lab.so only; not in any public header)

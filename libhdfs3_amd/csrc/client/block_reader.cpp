@@ -1,7 +1,8 @@
 // hdfs3_block_reader: RemoteBlockReader (src/client/RemoteBlockReader.cpp) with the
 // per-packet CPU verify replaced by batched GPU verification (include/hdfs3_client.h).
 //
-// Pipeline (three stages on a ring of kSlots pinned arenas):
+// Pipeline (three stages on a ring of pinned arenas, kSlots unless the input stream's block
+// read-ahead asks for a deeper ring):
 //   receiver thread  socket -> arena (readNextPacket, up to batch_packets packets; each
 //                    packet's data region 16-byte aligned) -> async H2D + packet kernel +
 //                    result D2H + event on the ctx stream -> `ready` queue
@@ -42,6 +43,7 @@ constexpr int kDefaultBatchPackets = 64;
 constexpr int kDefaultTimeoutMs = 60000;  // input.read.timeout default (SessionConfig.cpp)
 constexpr size_t kMaxResponse = 10u << 20;  // RemoteBlockReader.cpp:116
 constexpr int kSlots = 3;                  // receiving / verifying / delivering
+constexpr int kMaxSlots = 64;              // deepest ring (read-ahead of a whole block)
 constexpr int32_t kMaxPacketData = 16 << 20;  // PacketReceiver.MAX_PACKET_SIZE (Hadoop)
 constexpr size_t kArenaCacheMax = 6;       // arenas a ctx keeps for its next reader
 constexpr size_t kPacketGuess = 64 * 1024 + 16 * 1024;  // 64 KiB payload + CRCs + alignment
@@ -151,7 +153,7 @@ struct hdfs3_block_reader {
     // shared between receiver and caller, under mu
     std::mutex mu;
     std::condition_variable cv;
-    Batch slot[kSlots];
+    std::vector<Batch> slot;   // the ring (kSlots, or deeper for a read-ahead reader)
     std::deque<int> ready;     // launched batches in order, front = delivering
     std::deque<int> free_slots;
     bool recv_done = false;    // the receiver has finished (range complete or failed)
@@ -353,7 +355,7 @@ struct hdfs3_block_reader {
     }
 
     void start_receiver() {
-        for (int i = 0; i < kSlots; ++i) free_slots.push_back(i);
+        for (int i = 0; i < int(slot.size()); ++i) free_slots.push_back(i);
         rx = std::thread([this] { receiver(); });
     }
 
@@ -470,12 +472,15 @@ struct hdfs3_block_reader {
             rx.join();
         }
         if (ctx) (void)hipStreamSynchronize(ctx->stream);
+        // a borrowed ctx keeps up to a ring's worth of arenas for its next reader (a read-ahead
+        // reader's deep ring included: the stream's next read-ahead takes them back)
+        const size_t cache_max = std::max(kArenaCacheMax, slot.size());
         for (Batch &b : slot) {
             if (!b.a.h) continue;
             bool cached = false;
             if (ctx && !own_ctx) {
                 std::lock_guard<std::mutex> lk(ctx->arena_mu);
-                if (ctx->arena_cache.size() < kArenaCacheMax) {
+                if (ctx->arena_cache.size() < cache_max) {
                     ctx->arena_cache.push_back(b.a);
                     cached = true;
                 }
@@ -492,13 +497,19 @@ namespace hdfs3crc {
 
 bool block_reader_local_fault(const hdfs3_block_reader *r) { return r && r->local_fault.load(); }
 
+int64_t block_reader_batch_bytes(const hdfs3_reader_opts *opts) {
+    const int bp = opts && opts->batch_packets > 0 ? opts->batch_packets : kDefaultBatchPackets;
+    return int64_t(bp) * 64 * 1024;  // payload of a batch of 64 KiB datanode packets
+}
+
 int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int64_t start, int64_t len,
                       const char *client_name, const hdfs3_reader_opts *opts, hdfs3_crc_ctx *shared_ctx,
-                      hdfs3_block_reader **out) {
+                      hdfs3_block_reader **out, int slots) {
     if (!out || !host || !blk || start < 0 || len < 0) return fail(-EINVAL, "invalid argument");
     *out = nullptr;
     hdfs3_block_reader *r = new (std::nothrow) hdfs3_block_reader();
     if (!r) return fail(-ENOMEM, "reader allocation");
+    r->slot.resize(size_t(std::min(std::max(slots > 0 ? slots : kSlots, kSlots), kMaxSlots)));
     const int device = opts ? opts->device : 0;
     r->verify = opts ? opts->verify != 0 : true;
     if (opts && opts->batch_packets > 0) r->batch_packets = opts->batch_packets;

@@ -93,6 +93,8 @@ struct HdfsFileSystemInternalWrapper {
     std::string client_name;
     hdfs3_reader_opts ropts{0, 1, 64, 0};
     hdfs3_writer_opts wopts{0, 512, 65536, int64_t(128) << 20, 64};
+    int readahead_blocks = 0;         // hdfs3_fs_set_readahead: for files opened for reading
+    int64_t readahead_bytes = 0;
     std::mutex mu;
     std::map<std::string, FileEntry> files;
 };
@@ -167,6 +169,14 @@ int hdfs3_fs_set_sink(hdfsFS fs, const char *path, hdfs3_packet_sink sink, void 
     return 0;
 }
 
+int hdfs3_fs_set_readahead(hdfsFS fs, int blocks, int64_t max_bytes_per_block) {
+    PARAMETER_ASSERT(fs && blocks >= 0 && max_bytes_per_block >= 0, -1, EINVAL);
+    std::lock_guard<std::mutex> lk(fs->mu);
+    fs->readahead_blocks = blocks;
+    fs->readahead_bytes = max_bytes_per_block;
+    return 0;
+}
+
 int hdfsDisconnect(hdfsFS fs) {
     delete fs;  // Hdfs.cpp:629-636: a null fs is not an error
     return 0;
@@ -222,6 +232,12 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
         } else {
             rc = hdfs3_input_open(e.located_blocks.blocks.data(), int(e.located_blocks.blocks.size()),
                                   fs->client_name.c_str(), &fs->ropts, &file->in);
+            if (rc == 0 && fs->readahead_blocks > 0)
+                rc = hdfs3_input_set_readahead(file->in, fs->readahead_blocks, fs->readahead_bytes);
+            if (rc < 0 && file->in) {
+                hdfs3_input_close(file->in);
+                file->in = nullptr;
+            }
         }
     }
     if (rc < 0) {

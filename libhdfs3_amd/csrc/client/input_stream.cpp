@@ -1,9 +1,17 @@
 // hdfs3_input_stream: InputStreamImpl's read/pread/seek over located blocks with replica
 // failover (src/client/InputStreamImpl.cpp), every block read through the GPU-verifying
 // hdfs3_block_reader. The C entry points keep hdfs.h's -1/errno convention (Hdfs.cpp:826-862).
+//
+// Block read-ahead (opt-in, hdfs3_input_set_readahead; the reference opens a block's reader
+// only when the cursor reaches the block): entering block i opens the readers of blocks
+// i+1 .. i+D as well, each on its own pooled GPU context and with a ring deep enough for
+// max_bytes of the block, so their receiver threads read and verify ahead while block i is
+// consumed. When the cursor reaches block i+1 its reader simply becomes the current one:
+// read(), failover and EIO behave exactly as for a reader opened on demand.
 #include <algorithm>
 #include <cerrno>
 #include <cstring>
+#include <deque>
 #include <new>
 #include <string>
 #include <vector>
@@ -32,6 +40,14 @@ struct Block {
     std::vector<Node> replicas;
 };
 
+// a reader opened ahead of the cursor (block read-ahead) and the pooled ctx it verifies on
+struct Ahead {
+    int block;
+    hdfs3_block_reader *reader;
+    hdfs3_crc_ctx *ctx;
+    Node node;
+};
+
 // hdfs.h convention: errno + -1; the message goes where hdfs3_crc_last_error reads it
 int posix_fail(int err, const std::string &msg) {
     fail(-err, "%s", msg.c_str());
@@ -55,8 +71,14 @@ struct hdfs3_input_stream {
     std::vector<Node> failed;  // failedNodes
     uint64_t failovers = 0, opened = 0;
     std::string last_error;
+    int ahead_blocks = 0;           // hdfs3_input_set_readahead
+    int64_t ahead_bytes = 0;
+    std::deque<Ahead> ahead;        // readers of blocks after `cur`, by block
+    hdfs3_crc_ctx *reader_ctx = nullptr;  // the current reader's own ctx when it came from `ahead`
+    uint64_t ahead_opened = 0;
 
     ~hdfs3_input_stream() {
+        drop_ahead(-1);
         drop_reader();
         if (ctx) ctx_release(ctx);
     }
@@ -64,6 +86,63 @@ struct hdfs3_input_stream {
     void drop_reader() {
         if (reader) hdfs3_block_reader_close(reader);
         reader = nullptr;
+        if (reader_ctx) ctx_release(reader_ctx);  // after the reader: its arenas go back into it
+        reader_ctx = nullptr;
+    }
+
+    static void close_ahead(Ahead &a) {
+        hdfs3_block_reader_close(a.reader);
+        ctx_release(a.ctx);
+    }
+
+    // close the read-ahead readers not in (keep_from, keep_from + ahead_blocks]
+    void drop_ahead(int keep_from) {
+        for (auto it = ahead.begin(); it != ahead.end();) {
+            if (keep_from >= 0 && it->block > keep_from && it->block <= keep_from + ahead_blocks) {
+                ++it;
+                continue;
+            }
+            close_ahead(*it);
+            it = ahead.erase(it);
+        }
+    }
+
+    // entering block i: its read-ahead reader (if any) becomes the current reader; readers
+    // of i+1 .. i+ahead_blocks are opened where missing. A block whose reader cannot be
+    // opened ahead is left to the on-demand path, which owns replica choice and failover.
+    void schedule_ahead(int i) {
+        for (auto it = ahead.begin(); it != ahead.end(); ++it) {
+            if (it->block != i) continue;
+            reader = it->reader;
+            reader_ctx = it->ctx;
+            cur_node = it->node;
+            ahead.erase(it);
+            break;
+        }
+        drop_ahead(i);
+        if (ahead_blocks <= 0) return;
+        const int64_t unit = block_reader_batch_bytes(&opts);
+        for (int j = i + 1; j <= i + ahead_blocks && j < int(blocks.size()); ++j) {
+            auto at = std::find_if(ahead.begin(), ahead.end(), [&](const Ahead &a) { return a.block >= j; });
+            if (at != ahead.end() && at->block == j) continue;
+            const Block &b = blocks[size_t(j)];
+            if (b.length <= 0 || b.replicas.empty()) continue;
+            const int64_t want = std::min<int64_t>(b.length, ahead_bytes > 0 ? ahead_bytes : b.length);
+            const int slots = int(std::min<int64_t>((want + unit - 1) / unit + 1, 64));
+            hdfs3_crc_ctx *c = nullptr;
+            if (ctx_acquire(opts.device, &c)) break;  // no context to spare: read on demand
+            hdfs3_block_id id = b.id;
+            id.pool_id = b.pool.c_str();
+            hdfs3_block_reader *r = nullptr;
+            const Node &n = b.replicas.front();  // choseBestNode with a fresh failed list
+            if (open_block_reader(n.host.c_str(), n.port, &id, 0, b.length, client_name.c_str(), &opts, c, &r,
+                                  slots)) {
+                ctx_release(c);
+                continue;
+            }
+            ++ahead_opened;
+            ahead.insert(at, Ahead{j, r, c, n});
+        }
     }
 
     int find_block(int64_t pos) const {  // LocatedBlocks::findBlock
@@ -114,6 +193,9 @@ struct hdfs3_input_stream {
         cur = i;
         end_of_cur_block = blocks[i].offset + blocks[i].length;
         failed.clear();
+        // a read-ahead reader starts at the block's first byte: usable on sequential entry
+        if ((ahead_blocks > 0 || !ahead.empty()) && cursor == blocks[i].offset) schedule_ahead(i);
+        else if (!ahead.empty()) drop_ahead(i);
     }
 
     // readOneBlock (:616-712)
@@ -311,6 +393,20 @@ int hdfs3_input_stats(hdfs3_input_stream *s, uint64_t *failovers, uint64_t *read
     if (!s) return fail(-EINVAL, "null stream");
     if (failovers) *failovers = s->failovers;
     if (readers_opened) *readers_opened = s->opened;
+    return 0;
+}
+
+int hdfs3_input_set_readahead(hdfs3_input_stream *s, int blocks, int64_t max_bytes_per_block) {
+    if (!s || blocks < 0 || max_bytes_per_block < 0) return fail(-EINVAL, "invalid argument");
+    s->ahead_blocks = blocks;
+    s->ahead_bytes = max_bytes_per_block;
+    if (blocks == 0) s->drop_ahead(-1);
+    return 0;
+}
+
+int hdfs3_input_readahead_stats(hdfs3_input_stream *s, uint64_t *prefetch_readers_opened) {
+    if (!s) return fail(-EINVAL, "null stream");
+    if (prefetch_readers_opened) *prefetch_readers_opened = s->ahead_opened;
     return 0;
 }
 

@@ -480,9 +480,15 @@ class InputStream:
 
     def stats(self):
         from ctypes import c_uint64
-        f, o = c_uint64(), c_uint64()
+        f, o, a = c_uint64(), c_uint64(), c_uint64()
         check("hdfs3_input_stats", self._lib.hdfs3_input_stats(self.s, byref(f), byref(o)))
-        return {"failovers": f.value, "readers_opened": o.value}
+        check("hdfs3_input_readahead_stats", self._lib.hdfs3_input_readahead_stats(self.s, byref(a)))
+        return {"failovers": f.value, "readers_opened": o.value, "prefetch_readers_opened": a.value}
+
+    def set_readahead(self, blocks: int, max_bytes_per_block: int = 0) -> None:
+        """hdfs3_input_set_readahead: blocks i+1 .. i+blocks read by background threads while
+        block i is consumed (0 turns it off)."""
+        check("hdfs3_input_set_readahead", self._lib.hdfs3_input_set_readahead(self.s, blocks, max_bytes_per_block))
 
     def close(self):
         if self.s:

@@ -257,6 +257,30 @@ int main(int argc, char **argv) {
     CHECK(off >= c.len[0] && off <= c.len[0] + flip, "error surfaced at %lld", (long long)off);
     CHECK(inb && hdfsCloseFile(fs, inb) == 0, "close bad");
 
+    /* ---- the same read with block read-ahead (hdfs3_fs_set_readahead): same bytes, same
+     * failover off the corrupt replica, read-ahead readers opened for every later block ---- */
+    CHECK(hdfs3_fs_set_readahead(fs, 2, 0) == 0, "set_readahead");
+    hdfsFile ina = hdfsOpenFile(fs, "/tmp/f", O_RDONLY, 0, 0, 0);
+    CHECK(ina != NULL, "open for read-ahead: %s", hdfsGetLastError());
+    off = 0;
+    const double ta0 = now_s();
+    while (ina && off < size) {
+        const tSize want = (tSize)(size - off < (int64_t)rchunk ? size - off : (int64_t)rchunk);
+        const tSize g = hdfsRead(fs, ina, rbuf, want);
+        CHECK(g > 0, "read-ahead hdfsRead at %lld returned %d (%s)", (long long)off, g, hdfsGetLastError());
+        if (g <= 0) break;
+        if (!check_buffer(rbuf, (size_t)g, (size_t)off)) {
+            CHECK(0, "read-ahead CheckBuffer at %lld", (long long)off);
+            break;
+        }
+        off += g;
+    }
+    const double ta = now_s() - ta0;
+    CHECK(off == size, "read-ahead read %lld of %lld bytes", (long long)off, (long long)size);
+    CHECK(ina && hdfsRead(fs, ina, rbuf, 10) == 0, "read-ahead EOF");
+    CHECK(ina && hdfsCloseFile(fs, ina) == 0, "close read-ahead file");
+    CHECK(hdfs3_fs_set_readahead(fs, 0, 0) == 0, "read-ahead off");
+
     /* through datanodes: hdfsWrite -> GPU CRCs -> OP_WRITE_BLOCK pipeline of 3 loopback
      * nodes (acks per packet, the last node verifies every word) -> hdfsCloseFile registers the
      * file at the acked lengths -> hdfsOpenFile(O_RDONLY) / hdfsRead back from the nodes */
@@ -319,8 +343,9 @@ int main(int argc, char **argv) {
         return 1;
     }
     printf("{\"hdfs_consumer\": \"ok\", \"bytes\": %lld, \"blocks\": %lld, \"packets\": %lld, "
-           "\"hdfsWrite_GiBps\": %.3f, \"hdfsRead_GiBps\": %.3f, \"hdfsWrite_3node_pipeline_GiBps\": %.3f}\n",
+           "\"hdfsWrite_GiBps\": %.3f, \"hdfsRead_GiBps\": %.3f, \"hdfsRead_readahead2_GiBps\": %.3f, "
+           "\"hdfsWrite_3node_pipeline_GiBps\": %.3f}\n",
            (long long)size, (long long)c.nblocks, (long long)c.packets, (double)size / tw / (1 << 30),
-           (double)size / tr / (1 << 30), (double)size / tp / (1 << 30));
+           (double)size / tr / (1 << 30), (double)size / ta / (1 << 30), (double)size / tp / (1 << 30));
     return 0;
 }

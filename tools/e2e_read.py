@@ -6,6 +6,7 @@
                 hdfs3_block_reader: socket -> pinned arena -> H2D -> packet-kernel verify ->
                 caller buffer), verify on vs off
   parallel      8 concurrent streams, one hdfsPread of one whole block each
+  readahead     hdfsRead on one stream with block read-ahead (hdfs3_input_set_readahead D)
   local         short-circuit read (hdfs3_local_reader, LocalBlockReader): 8 block files of
                 128 MiB + .meta in a temp dir (page-cache resident after writing), 4 MiB reads,
                 verify on vs off; 1 stream, and 8 concurrent readers (one block each)
@@ -174,6 +175,8 @@ def main():
     ap.add_argument("--read-mib", type=int, default=4, help="hdfsRead request size")
     ap.add_argument("--diag", action="store_true", help="per-phase timing of the block reader only")
     ap.add_argument("--local-only", action="store_true", help="only the short-circuit reader lines")
+    ap.add_argument("--readahead", default="1,2,3,7",
+                    help="block read-ahead depths of the extra single-stream hdfsRead lines ('' = none)")
     args = ap.parse_args()
 
     from libhdfs3_amd import _native
@@ -253,6 +256,27 @@ def main():
                 print(json.dumps({**line, "mode": mode, "verify": verify, "streams": 1 if mode == "hdfsRead"
                                   else args.blocks, "batch_packets": args.batch, "packet_kib": args.packet_kib,
                                   "gib_s": round(best, 2)}), flush=True)
+        # single-stream hdfsRead with block read-ahead (hdfs3_input_set_readahead): blocks
+        # i+1 .. i+D read and verified by background threads while block i is consumed
+        for ahead in [int(x) for x in args.readahead.split(",") if x]:
+            best = 0.0
+            for _ in range(args.reps):
+                t0 = time.perf_counter()
+                with InputStream([(b, n, [("127.0.0.1", dn.port)]) for b, n in blocks], verify=True,
+                                 batch_packets=args.batch) as s:
+                    s.set_readahead(ahead)
+                    pos = 0
+                    while pos < total:
+                        got = s.read_into(out, pos, min(args.read_mib << 20, total - pos))
+                        assert got > 0
+                        pos += got
+                dt = time.perf_counter() - t0
+                best = max(best, total / dt / GIB)
+            assert np.array_equal(out, data)
+            out[:] = 0
+            print(json.dumps({**line, "mode": "hdfsRead_readahead", "verify": True, "streams": 1,
+                              "readahead_blocks": ahead, "batch_packets": args.batch,
+                              "packet_kib": args.packet_kib, "gib_s": round(best, 2)}), flush=True)
     finally:
         dn.stop()
     local_reads(data, crc, args, line)
