@@ -61,6 +61,11 @@ def main():
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--idle", type=float, default=1.0)
     ap.add_argument("--period", type=float, default=0.1)
+    ap.add_argument("--burst", type=int, default=100,
+                    help="launches per HIP-event batch; with --gap-ms > 0 the GPU idles between batches")
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="idle time between batches (duty-cycled load: average power below the limit)")
+    ap.add_argument("--barriered", action="store_true", help="every verify launch keeps the AQL barrier bit")
     ap.add_argument("--phases", default="v0,read,v0",
                     help="comma list: vN = verify through the lab library with kernel variant N "
                          "(0 = production; diagnostic variants give wrong results on purpose), "
@@ -81,18 +86,19 @@ def main():
     lab = bench.lab_context(work, stream)
     lib = _native.lab()
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
-    result = torch.zeros(100, dtype=torch.int64, device=dev)
+    result = torch.zeros(max(100, args.burst), dtype=torch.int64, device=dev)
 
     def verify_batch(i0, n):
         for i in range(n):
             b = (i0 + i) % work.blocks
             lab.verify_dev_async(work.data_ptr(b), work.block_bytes, 512, work.crc_ptr(b),
-                                 result.data_ptr() + 8 * (i % 100), overlap_previous=i > 0)
+                                 result.data_ptr() + 8 * (i % result.numel()), overlap_previous=i > 0 and not args.barriered)
 
     def read_batch(i0, n, grid=256):
         for i in range(n):
             b = (i0 + i) % work.blocks
-            lib.hdfs3x_stream_read_ex(lab.ctx, work.data_ptr(b), work.block_bytes, grid, sink.data_ptr(), int(i > 0))
+            lib.hdfs3x_stream_read_ex(lab.ctx, work.data_ptr(b), work.block_bytes, grid, sink.data_ptr(),
+                                      int(i > 0 and not args.barriered))
 
     lines, samples = [], []
     stop = threading.Event()
@@ -111,12 +117,14 @@ def main():
         while time.perf_counter() < end:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            fn(i, 100)
+            fn(i, args.burst)
             e1.record(stream)
             e1.synchronize()
-            lines.append({"phase": phase, "k": k, "t": round(time.perf_counter() - t0, 4), "batch": i // 100,
-                          "us_per_launch": round(e0.elapsed_time(e1) * 1e3 / 100, 3)})
-            i += 100
+            lines.append({"phase": phase, "k": k, "t": round(time.perf_counter() - t0, 4), "batch": i // args.burst,
+                          "us_per_launch": round(e0.elapsed_time(e1) * 1e3 / args.burst, 3)})
+            i += args.burst
+            if args.gap_ms > 0:
+                time.sleep(args.gap_ms * 1e-3)
         if phase == "v0" and bool((result != 0).any().item()):
             raise SystemExit("clean blocks reported bad")
         lib.hdfs3x_set_variant(0)
