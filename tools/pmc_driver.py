@@ -15,6 +15,8 @@ def main():
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--launches", type=int, default=16)
     ap.add_argument("--mode", default="verify")
+    ap.add_argument("--overlap", action="store_true",
+                    help="launches after the first overlap their predecessor (the bench's timed mode)")
     args = ap.parse_args()
     import torch
     from libhdfs3_amd import _native
@@ -35,7 +37,7 @@ def main():
     for i in range(args.launches):
         if args.mode == "verify":
             ctx.verify_dev_async(data[i % blocks].data_ptr(), bb, args.bpc, crc[i % blocks].data_ptr(),
-                                 res.data_ptr() + 8 * i)
+                                 res.data_ptr() + 8 * i, overlap_previous=args.overlap and i > 0)
         else:
             ctx.compute_dev(data[i % blocks].data_ptr(), bb, args.bpc, crc[i % blocks].data_ptr())
     ctx.synchronize()
