@@ -40,6 +40,7 @@
 #include <thread>
 #include <vector>
 
+#include "../copy_pool.h"
 #include "../ctx.h"
 #include "hdfs3_client.h"
 #include "hdfs3_crc.h"
@@ -64,22 +65,6 @@ int hip_err(hipError_t e, const char *what) {
         hipError_t e_ = (expr);                           \
         if (e_ != hipSuccess) return hip_err(e_, #expr);  \
     } while (0)
-
-int pread_fully(int fd, void *buf, size_t n, int64_t off) {
-    uint8_t *p = static_cast<uint8_t *>(buf);
-    while (n) {
-        const ssize_t r = ::pread(fd, p, n, off);
-        if (r < 0) {
-            if (errno == EINTR) continue;
-            return -errno;
-        }
-        if (r == 0) return -EIO;  // file shorter than the block / meta says
-        p += r;
-        n -= size_t(r);
-        off += r;
-    }
-    return 0;
-}
 
 // Reader resources — a ctx (stream, table images) and kSlots pinned + device windows —
 // are pooled per process. The reference opens one LocalBlockReader per block
@@ -122,93 +107,9 @@ void give_back(LocalResources r) {
     free_resources(r);
 }
 
-// Copies out of a verified window are the single-stream limit of this reader (one thread
-// copies ~11 GiB/s; the loader preads at ~20). Large copies are split over a small
-// process-wide pool of helper threads. The pool is leaked on purpose: its threads block on
-// its condition variable until the process exits.
-class CopyPool {
-  public:
-    static CopyPool &get() {
-        static CopyPool *p = new CopyPool();
-        return *p;
-    }
-    void copy(uint8_t *dst, const uint8_t *src, size_t n) { split(dst, src, -1, 0, n); }
-    // pread of [off, off + n) of fd into dst, in parallel pieces; 0 or -errno
-    int pread(int fd, uint8_t *dst, size_t n, int64_t off) { return split(dst, nullptr, fd, off, n); }
-
-  private:
-    static constexpr size_t kHelpers = 3;
-    struct Job {
-        uint8_t *dst = nullptr;
-        const uint8_t *src = nullptr;  // memcpy source, or null: pread from fd at off
-        int fd = -1;
-        int64_t off = 0;
-        size_t n = 0;
-        std::atomic<int> *pending = nullptr;
-        std::atomic<int> *err = nullptr;
-    };
-    static void run(const Job &j) {
-        if (j.src) {
-            std::memcpy(j.dst, j.src, j.n);
-        } else if (int rc = pread_fully(j.fd, j.dst, j.n, j.off)) {
-            j.err->store(rc, std::memory_order_relaxed);
-        }
-        j.pending->fetch_sub(1, std::memory_order_release);
-    }
-    int split(uint8_t *dst, const uint8_t *src, int fd, int64_t foff, size_t n) {
-        constexpr size_t kMin = 2u << 20;
-        std::atomic<int> pending{0}, err{0};
-        if (n < kMin) {
-            run(Job{dst, src, fd, foff, n, &pending, &err});
-            return err.load();
-        }
-        const size_t parts = kHelpers + 1;
-        const size_t piece = (n / parts + 4095) & ~size_t(4095);
-        size_t off = piece;
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            for (size_t i = 1; i < parts && off < n; ++i, off += piece) {
-                jobs_.push_back(Job{dst + off, src ? src + off : nullptr, fd, foff + int64_t(off), std::min(piece, n - off),
-                                    &pending, &err});
-                pending.fetch_add(1, std::memory_order_relaxed);
-            }
-        }
-        cv_.notify_all();
-        pending.fetch_add(1, std::memory_order_relaxed);
-        run(Job{dst, src, fd, foff, std::min(piece, n), &pending, &err});
-        // help with pieces no helper has taken yet, then wait for the rest
-        for (;;) {
-            Job j;
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                if (jobs_.empty()) break;
-                j = jobs_.back();
-                jobs_.pop_back();
-            }
-            run(j);
-        }
-        while (pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
-        return err.load();
-    }
-    CopyPool() {
-        for (size_t i = 0; i < kHelpers; ++i)
-            std::thread([this] {
-                for (;;) {
-                    Job j;
-                    {
-                        std::unique_lock<std::mutex> lk(mu_);
-                        cv_.wait(lk, [this] { return !jobs_.empty(); });
-                        j = jobs_.front();
-                        jobs_.pop_front();
-                    }
-                    run(j);
-                }
-            }).detach();
-    }
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::deque<Job> jobs_;
-};
+// Copies out of a verified window (one thread ~11 GiB/s) and the window preads (one thread
+// ~9-12 GiB/s) are this reader's single-stream limits: both go through the process-wide
+// CopyPool (copy_pool.h).
 
 struct Window {
     PacketArena a;            // h/d: [data (cap_data)][crc words]

@@ -1,0 +1,182 @@
+// Internal: a small process-wide pool of host threads for the large CPU copies around the GPU
+// work — staging pageable caller buffers into pinned memory (hdfs3_crc32c_verify/compute),
+// copying verified bytes out of pinned arenas into caller buffers (block reader, local
+// reader) and preading block files (local reader). One thread copies ~11-28 GiB/s depending
+// on the memory involved, below the PCIe and socket rates these paths feed, so copies of 2 MiB
+// or more are split over the caller and the helpers (3; HDFS3_COPY_HELPERS=n sets n, 0 copies
+// on the calling thread only). The pool is leaked on purpose: its threads block on its
+// condition variable until the process exits. Not installed.
+#pragma once
+
+#include <unistd.h>
+
+#include <cstdlib>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+
+namespace hdfs3crc {
+
+inline int pread_fully(int fd, void *buf, size_t n, int64_t off) {
+    uint8_t *p = static_cast<uint8_t *>(buf);
+    while (n) {
+        const ssize_t r = ::pread(fd, p, n, off);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return -errno;
+        }
+        if (r == 0) return -EIO;  // file shorter than the block / meta says
+        p += r;
+        n -= size_t(r);
+        off += r;
+    }
+    return 0;
+}
+
+class CopyPool {
+  public:
+    struct Range {
+        uint8_t *dst;
+        const uint8_t *src;
+        size_t n;
+    };
+
+    static CopyPool &get() {
+        static CopyPool *p = new CopyPool();
+        return *p;
+    }
+    void copy(void *dst, const void *src, size_t n) {
+        split(static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), -1, 0, n);
+    }
+    // pread of [off, off + n) of fd into dst, in parallel pieces; 0 or -errno
+    int pread(int fd, void *dst, size_t n, int64_t off) { return split(static_cast<uint8_t *>(dst), nullptr, fd, off, n); }
+    // many independent ranges (e.g. the data regions of consecutive packets): split into
+    // groups of consecutive ranges of about equal bytes, one group per thread
+    void copy_ranges(const Range *r, size_t count) {
+        size_t total = 0;
+        for (size_t i = 0; i < count; ++i) total += r[i].n;
+        if (total < kMin || count < 2 || helpers_ == 0) {
+            for (size_t i = 0; i < count; ++i) std::memcpy(r[i].dst, r[i].src, r[i].n);
+            return;
+        }
+        std::atomic<int> pending{0}, err{0};
+        const size_t target = total / (helpers_ + 1) + 1;
+        Job mine{};
+        bool have_mine = false;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            size_t i = 0;
+            while (i < count) {
+                size_t j = i, bytes = 0;
+                while (j < count && (bytes < target || j == i)) bytes += r[j++].n;
+                Job g{};
+                g.ranges = r + i;
+                g.nranges = j - i;
+                g.pending = &pending;
+                g.err = &err;
+                pending.fetch_add(1, std::memory_order_relaxed);
+                if (!have_mine) {
+                    mine = g;
+                    have_mine = true;
+                } else {
+                    jobs_.push_back(g);
+                }
+                i = j;
+            }
+        }
+        cv_.notify_all();
+        run(mine);
+        help_and_wait(pending);
+    }
+
+  private:
+    static constexpr size_t kMin = 2u << 20;
+    size_t helpers_ = 3;
+    struct Job {
+        uint8_t *dst = nullptr;
+        const uint8_t *src = nullptr;  // memcpy source, or null: pread from fd at off
+        int fd = -1;
+        int64_t off = 0;
+        size_t n = 0;
+        const Range *ranges = nullptr;  // set: copy these ranges instead
+        size_t nranges = 0;
+        std::atomic<int> *pending = nullptr;
+        std::atomic<int> *err = nullptr;
+    };
+    static void run(const Job &j) {
+        if (j.ranges) {
+            for (size_t i = 0; i < j.nranges; ++i) std::memcpy(j.ranges[i].dst, j.ranges[i].src, j.ranges[i].n);
+        } else if (j.src) {
+            std::memcpy(j.dst, j.src, j.n);
+        } else if (int rc = pread_fully(j.fd, j.dst, j.n, j.off)) {
+            j.err->store(rc, std::memory_order_relaxed);
+        }
+        j.pending->fetch_sub(1, std::memory_order_release);
+    }
+    // help with pieces no helper has taken yet, then wait for the rest
+    void help_and_wait(std::atomic<int> &pending) {
+        for (;;) {
+            Job j;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (jobs_.empty()) break;
+                j = jobs_.back();
+                jobs_.pop_back();
+            }
+            run(j);
+        }
+        while (pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    }
+    int split(uint8_t *dst, const uint8_t *src, int fd, int64_t foff, size_t n) {
+        std::atomic<int> pending{0}, err{0};
+        if (n < kMin || helpers_ == 0) {
+            pending.fetch_add(1, std::memory_order_relaxed);
+            run(Job{dst, src, fd, foff, n, nullptr, 0, &pending, &err});
+            return err.load();
+        }
+        const size_t parts = helpers_ + 1;
+        const size_t piece = (n / parts + 4095) & ~size_t(4095);
+        size_t off = piece;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (size_t i = 1; i < parts && off < n; ++i, off += piece) {
+                jobs_.push_back(Job{dst + off, src ? src + off : nullptr, fd, foff + int64_t(off), std::min(piece, n - off),
+                                    nullptr, 0, &pending, &err});
+                pending.fetch_add(1, std::memory_order_relaxed);
+            }
+        }
+        cv_.notify_all();
+        pending.fetch_add(1, std::memory_order_relaxed);
+        run(Job{dst, src, fd, foff, std::min(piece, n), nullptr, 0, &pending, &err});
+        help_and_wait(pending);
+        return err.load();
+    }
+    CopyPool() {
+        if (const char *e = getenv("HDFS3_COPY_HELPERS")) helpers_ = size_t(std::min(std::max(atoi(e), 0), 15));
+        for (size_t i = 0; i < helpers_; ++i)
+            std::thread([this] {
+                for (;;) {
+                    Job j;
+                    {
+                        std::unique_lock<std::mutex> lk(mu_);
+                        cv_.wait(lk, [this] { return !jobs_.empty(); });
+                        j = jobs_.front();
+                        jobs_.pop_front();
+                    }
+                    run(j);
+                }
+            }).detach();
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Job> jobs_;
+};
+
+}  // namespace hdfs3crc

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <new>
 
+#include "copy_pool.h"
 #include "crc32c_kernels.h"
 #include "crc32c_tables.h"
 #include "ctx.h"
@@ -174,7 +175,7 @@ int host_pipeline_impl(hdfs3_crc_ctx *ctx, const void *data, size_t len, uint32_
         if (s.done) HIP_TRY(hipEventSynchronize(s.done));
         if (int rc = finish_pending(s)) return rc;
         if (int rc = grow_slot(s, seg, seg_crc)) return rc;
-        if (!direct) std::memcpy(s.h_data, src + off, n);
+        if (!direct) CopyPool::get().copy(s.h_data, src + off, n);  // pageable: staged, split over the pool
         HIP_TRY(hipMemcpyAsync(s.d_data, direct ? src + off : s.h_data, n, hipMemcpyHostToDevice, ctx->stream));
         ChunkLaunch a{};
         a.data = s.d_data;
