@@ -29,7 +29,6 @@
 #include <thread>
 #include <vector>
 
-#include "../copy_pool.h"
 #include "../ctx.h"
 #include "block_reader.h"
 #include "hdfs3_crc.h"
@@ -165,7 +164,6 @@ struct hdfs3_block_reader {
 
     // caller state
     int64_t delivered = 0;
-    std::vector<CopyPool::Range> pieces;  // read(): the copies of one batch
     bool sent_status = false;
     int error = 0;             // sticky failure (-errno)
     std::string error_msg;
@@ -418,14 +416,14 @@ struct hdfs3_block_reader {
             const size_t limit = b.bad_pkt >= 0 ? size_t(b.bad_pkt) : b.pk.size();
             {
                 Timer tm(t_ns[4]);
-                // this call's pieces of the batch (one per packet data region), then one copy
-                // of all of them: split over the copy pool when they add up to MiBs
-                pieces.clear();
+                // (a copy per packet on this thread: splitting a call's copies over the copy
+                // pool gained nothing on a single TCP-bound stream and cost 8 concurrent
+                // streams ~20 %, profiles/r02/e2e_read_copy_pool_ab.jsonl)
                 while (total < len && b.dpkt < limit) {
                     const PacketRef &p = b.pk[b.dpkt];
                     const size_t avail = p.deliver - b.doff;
                     const size_t n = std::min<size_t>(avail, size_t(len - total));
-                    pieces.push_back(CopyPool::Range{out + total, b.a.h + p.data_off + p.skip + b.doff, n});
+                    std::memcpy(out + total, b.a.h + p.data_off + p.skip + b.doff, n);
                     total += int32_t(n);
                     b.doff += n;
                     delivered += int64_t(n);
@@ -434,7 +432,6 @@ struct hdfs3_block_reader {
                         b.doff = 0;
                     }
                 }
-                CopyPool::get().copy_ranges(pieces.data(), pieces.size());
             }
             if (b.dpkt == limit) {
                 if (b.bad_pkt >= 0) {

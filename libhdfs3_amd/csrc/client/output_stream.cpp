@@ -269,15 +269,18 @@ struct hdfs3_output_stream {
         while (todo > 0) {
             if (!cur)
                 if (int rc = open_packet()) return rc;
-            const uint32_t n = uint32_t(std::min<int64_t>(bpc - position, todo));
+            // the chunks of one packet are contiguous in its data region, so everything up to the
+            // packet's or the block's end is one copy; appendChunkToPacket's per-chunk
+            // bookkeeping (bytesWritten advances by whole chunks, position is the partial one)
+            // is then applied for all the chunks it completed
+            const int64_t pkt_room = int64_t(chunks_per_packet) * bpc - cur->data_len;
+            const int64_t blk_room = block_size - bytes_written - position;
+            const uint32_t n = uint32_t(std::min({todo, pkt_room, blk_room}));
             std::memcpy(batch[cur_batch].a.h + cur->data_off + cur->data_len, buf + (size - todo), n);
             cur->data_len += n;
-            position += n;
             todo -= n;
-            if (position == bpc) {  // appendChunkToPacket
-                position = 0;
-                bytes_written += bpc;
-            }
+            bytes_written += int64_t((position + n) / bpc) * bpc;
+            position = (position + n) % bpc;
             const bool full = cur->data_len == uint32_t(chunks_per_packet) * bpc;
             if (full || bytes_written == block_size) {
                 send_current();

@@ -1,11 +1,13 @@
 // Internal: a small process-wide pool of host threads for the large CPU copies around the GPU
 // work — staging pageable caller buffers into pinned memory (hdfs3_crc32c_verify/compute),
-// copying verified bytes out of pinned arenas into caller buffers (block reader, local
-// reader) and preading block files (local reader). One thread copies ~11-28 GiB/s depending
-// on the memory involved, below the PCIe and socket rates these paths feed, so copies of 2 MiB
-// or more are split over the caller and the helpers (3; HDFS3_COPY_HELPERS=n sets n, 0 copies
-// on the calling thread only). The pool is leaked on purpose: its threads block on its
-// condition variable until the process exits. Not installed.
+// copying verified windows out to the caller and preading block files (local reader). One
+// thread copies ~11-28 GiB/s depending on the memory involved, below the PCIe rate these
+// paths feed, so copies of 2 MiB or more are split over the caller and the helpers (3;
+// HDFS3_COPY_HELPERS=n sets n, 0 copies on the calling thread only). A caller always copies
+// its own first piece and then takes queued pieces itself, so concurrent callers (a local
+// reader's loader and its consumer) share the helpers without waiting on each other. The pool
+// is leaked on purpose: its threads block on its condition variable until the process exits.
+// Not installed.
 #pragma once
 
 #include <unistd.h>
@@ -42,12 +44,6 @@ inline int pread_fully(int fd, void *buf, size_t n, int64_t off) {
 
 class CopyPool {
   public:
-    struct Range {
-        uint8_t *dst;
-        const uint8_t *src;
-        size_t n;
-    };
-
     static CopyPool &get() {
         static CopyPool *p = new CopyPool();
         return *p;
@@ -57,45 +53,6 @@ class CopyPool {
     }
     // pread of [off, off + n) of fd into dst, in parallel pieces; 0 or -errno
     int pread(int fd, void *dst, size_t n, int64_t off) { return split(static_cast<uint8_t *>(dst), nullptr, fd, off, n); }
-    // many independent ranges (e.g. the data regions of consecutive packets): split into
-    // groups of consecutive ranges of about equal bytes, one group per thread
-    void copy_ranges(const Range *r, size_t count) {
-        size_t total = 0;
-        for (size_t i = 0; i < count; ++i) total += r[i].n;
-        if (total < kMin || count < 2 || helpers_ == 0) {
-            for (size_t i = 0; i < count; ++i) std::memcpy(r[i].dst, r[i].src, r[i].n);
-            return;
-        }
-        std::atomic<int> pending{0}, err{0};
-        const size_t target = total / (helpers_ + 1) + 1;
-        Job mine{};
-        bool have_mine = false;
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            size_t i = 0;
-            while (i < count) {
-                size_t j = i, bytes = 0;
-                while (j < count && (bytes < target || j == i)) bytes += r[j++].n;
-                Job g{};
-                g.ranges = r + i;
-                g.nranges = j - i;
-                g.pending = &pending;
-                g.err = &err;
-                pending.fetch_add(1, std::memory_order_relaxed);
-                if (!have_mine) {
-                    mine = g;
-                    have_mine = true;
-                } else {
-                    jobs_.push_back(g);
-                }
-                i = j;
-            }
-        }
-        cv_.notify_all();
-        run(mine);
-        help_and_wait(pending);
-    }
-
   private:
     static constexpr size_t kMin = 2u << 20;
     size_t helpers_ = 3;
@@ -105,15 +62,11 @@ class CopyPool {
         int fd = -1;
         int64_t off = 0;
         size_t n = 0;
-        const Range *ranges = nullptr;  // set: copy these ranges instead
-        size_t nranges = 0;
         std::atomic<int> *pending = nullptr;
         std::atomic<int> *err = nullptr;
     };
     static void run(const Job &j) {
-        if (j.ranges) {
-            for (size_t i = 0; i < j.nranges; ++i) std::memcpy(j.ranges[i].dst, j.ranges[i].src, j.ranges[i].n);
-        } else if (j.src) {
+        if (j.src) {
             std::memcpy(j.dst, j.src, j.n);
         } else if (int rc = pread_fully(j.fd, j.dst, j.n, j.off)) {
             j.err->store(rc, std::memory_order_relaxed);
@@ -138,23 +91,24 @@ class CopyPool {
         std::atomic<int> pending{0}, err{0};
         if (n < kMin || helpers_ == 0) {
             pending.fetch_add(1, std::memory_order_relaxed);
-            run(Job{dst, src, fd, foff, n, nullptr, 0, &pending, &err});
+            run(Job{dst, src, fd, foff, n, &pending, &err});
             return err.load();
         }
         const size_t parts = helpers_ + 1;
-        const size_t piece = (n / parts + 4095) & ~size_t(4095);
+        // ceil(n / parts), rounded up to 4 KiB: the parts pieces cover all n bytes
+        const size_t piece = ((n + parts - 1) / parts + 4095) & ~size_t(4095);
         size_t off = piece;
         {
             std::lock_guard<std::mutex> lk(mu_);
             for (size_t i = 1; i < parts && off < n; ++i, off += piece) {
                 jobs_.push_back(Job{dst + off, src ? src + off : nullptr, fd, foff + int64_t(off), std::min(piece, n - off),
-                                    nullptr, 0, &pending, &err});
+                                    &pending, &err});
                 pending.fetch_add(1, std::memory_order_relaxed);
             }
         }
         cv_.notify_all();
         pending.fetch_add(1, std::memory_order_relaxed);
-        run(Job{dst, src, fd, foff, std::min(piece, n), nullptr, 0, &pending, &err});
+        run(Job{dst, src, fd, foff, std::min(piece, n), &pending, &err});
         help_and_wait(pending);
         return err.load();
     }

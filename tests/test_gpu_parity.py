@@ -374,3 +374,18 @@ def test_overlapped_chain_at_bench_size(gpu_ctx):
     words = gpu_ctx.download(res, 8 * nblk * passes).view(np.uint64)
     got = [gpu_ctx.decode_result(int(w)) for w in words]
     assert got == [last if i % nblk == 5 else -1 for i in range(nblk * passes)]
+
+
+@pytest.mark.parametrize("n", [(2 << 20) + 1, (4 << 20) + 3, (16 << 20) + (4 << 20) + 2])
+def test_host_api_pageable_staging_every_byte(gpu_ctx, n):
+    """The host-buffer API stages pageable buffers through the host copy pool (split for copies
+    of 2 MiB or more): lengths that split unevenly must compute and verify every chunk,
+    including the last, exactly as the oracle does."""
+    data = splitmix_bytes(n, n)
+    for bpc in (512, 4096):
+        want = oracle_compute(data, bpc)
+        assert np.array_equal(gpu_ctx.compute(data, bpc), want), (n, bpc)
+        assert gpu_ctx.verify(data, bpc, want, True) == -1
+        bad = data.copy()
+        bad[-1] ^= 0x80  # the very last byte lives in the piece that used to be dropped
+        assert gpu_ctx.verify(bad, bpc, want, True) == oracle_verify(bad, bpc, want, True) == (n - 1) // bpc

@@ -210,3 +210,23 @@ def test_local_buffer_above_1gib_is_rejected(tmp_path):
     with pytest.raises(Hdfs3CrcError) as ei:
         read(d, m, buffer_size=(1 << 30) + 1)
     assert ei.value.rc == -errno.EINVAL
+
+
+@pytest.mark.parametrize("piece", [(2 << 20) + 1, (2 << 20) + 3, (4 << 20) + 2, (3 << 20) + 5])
+def test_read_sizes_that_split_unevenly(tmp_path, piece, staging):
+    """Copies of 2 MiB or more are split over the host copy pool (csrc/copy_pool.h). Sizes whose
+    quarter is a whole number of 4 KiB pages plus 1-3 bytes once lost their last bytes (the
+    pieces were sized from the floor); every byte of every read must be the file's."""
+    from libhdfs3_amd.engine import LocalBlockReader
+
+    data = splitmix_bytes(9 * (1 << 20) + 17, piece)
+    d, m = write_block(tmp_path, "blk_uneven", data)
+    for verify in (True, False):
+        with LocalBlockReader(d, m, verify=verify, buffer_size=1 << 20, window_buffers=8) as r:
+            out = np.full(data.nbytes, 0xEE, np.uint8)
+            pos = 0
+            while pos < data.nbytes:
+                got = r.read_into(out, pos, min(piece, data.nbytes - pos))
+                assert got > 0
+                pos += got
+            assert pos == data.nbytes and np.array_equal(out, data), verify
