@@ -524,6 +524,8 @@ namespace {
 std::mutex g_ctx_pool_mu;
 std::vector<hdfs3_crc_ctx *> g_ctx_pool;
 constexpr size_t kCtxPoolMax = 32;
+constexpr size_t kArenaCacheKeep = 6;  // arenas any pooled ctx keeps (block_reader.cpp kArenaCacheMax)
+constexpr size_t kDeepCtxMax = 4;      // pooled contexts allowed to keep a read-ahead ring's worth
 }  // namespace
 
 int ctx_acquire(int device, hdfs3_crc_ctx **out) {
@@ -558,6 +560,19 @@ void ctx_release(hdfs3_crc_ctx *ctx) {
     if (ok) {
         std::lock_guard<std::mutex> lk(g_ctx_pool_mu);
         if (g_ctx_pool.size() < kCtxPoolMax) {
+            // a read-ahead reader's deep ring leaves up to a block's worth of pinned arenas in
+            // its ctx (block_reader.cpp); at most kDeepCtxMax pooled contexts keep that much,
+            // the others go back to the usual few arenas, so the pool's pinned memory is bounded
+            size_t deep = 0;
+            for (hdfs3_crc_ctx *c : g_ctx_pool) deep += c->arena_cache.size() > kArenaCacheKeep;
+            if (deep >= kDeepCtxMax && ctx->arena_cache.size() > kArenaCacheKeep) {
+                DeviceGuard g(ctx->device);
+                std::lock_guard<std::mutex> alk(ctx->arena_mu);
+                while (ctx->arena_cache.size() > kArenaCacheKeep) {
+                    ctx->arena_cache.back().release();
+                    ctx->arena_cache.pop_back();
+                }
+            }
             g_ctx_pool.push_back(ctx);
             return;
         }
