@@ -130,7 +130,7 @@ struct hdfs3_input_stream {
             const int64_t want = std::min<int64_t>(b.length, ahead_bytes > 0 ? ahead_bytes : b.length);
             const int slots = int(std::min<int64_t>((want + unit - 1) / unit + 1, 64));
             hdfs3_crc_ctx *c = nullptr;
-            if (ctx_acquire(opts.device, &c)) break;  // no context to spare: read on demand
+            if (ctx_acquire(opts.device, &c, true)) break;  // no context to spare: read on demand
             hdfs3_block_id id = b.id;
             id.pool_id = b.pool.c_str();
             hdfs3_block_reader *r = nullptr;

@@ -77,7 +77,8 @@ namespace hdfs3crc {
 // (stream, table uploads, device query) and its pinned arenas costs milliseconds, more than
 // reading a small file. A released ctx keeps its arena cache and goes back to the pool.
 // acquire: a pooled ctx of `device` (stream reset to its own, type CRC32C) or a new one.
-int ctx_acquire(int device, hdfs3_crc_ctx **out);
+// deep = true: prefer the pooled ctx holding the most cached arenas (block read-ahead rings).
+int ctx_acquire(int device, hdfs3_crc_ctx **out, bool deep = false);
 // release: synchronizes the ctx's stream; pooled when that succeeds and the pool has room.
 void ctx_release(hdfs3_crc_ctx *ctx);
 }  // namespace hdfs3crc

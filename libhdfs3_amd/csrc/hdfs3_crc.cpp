@@ -525,17 +525,25 @@ std::mutex g_ctx_pool_mu;
 std::vector<hdfs3_crc_ctx *> g_ctx_pool;
 constexpr size_t kCtxPoolMax = 32;
 constexpr size_t kArenaCacheKeep = 6;  // arenas any pooled ctx keeps (block_reader.cpp kArenaCacheMax)
-constexpr size_t kDeepCtxMax = 4;      // pooled contexts allowed to keep a read-ahead ring's worth
+constexpr size_t kDeepCtxMax = 8;      // pooled contexts allowed to keep a read-ahead ring's worth
 }  // namespace
 
-int ctx_acquire(int device, hdfs3_crc_ctx **out) {
+int ctx_acquire(int device, hdfs3_crc_ctx **out, bool deep) {
     if (!out) return fail(-EINVAL, "null out");
     {
         std::lock_guard<std::mutex> lk(g_ctx_pool_mu);
+        // deep: the pooled ctx with the most cached arenas (a read-ahead reader's ring);
+        // otherwise the one with the fewest, which keeps the deep ones for read-ahead
+        long best = -1;
         for (size_t i = 0; i < g_ctx_pool.size(); ++i) {
-            hdfs3_crc_ctx *ctx = g_ctx_pool[i];
-            if (ctx->device != device) continue;
-            g_ctx_pool.erase(g_ctx_pool.begin() + long(i));
+            if (g_ctx_pool[i]->device != device) continue;
+            if (best < 0 || (deep ? g_ctx_pool[i]->arena_cache.size() > g_ctx_pool[size_t(best)]->arena_cache.size()
+                                  : g_ctx_pool[i]->arena_cache.size() < g_ctx_pool[size_t(best)]->arena_cache.size()))
+                best = long(i);
+        }
+        if (best >= 0) {
+            hdfs3_crc_ctx *ctx = g_ctx_pool[size_t(best)];
+            g_ctx_pool.erase(g_ctx_pool.begin() + best);
             ctx->stream = ctx->own_stream;
             ctx->checksum_type = HDFS3_CHECKSUM_TYPE_CRC32C;
             ctx->d_tables = ctx->d_tables_by[0];
