@@ -719,7 +719,7 @@ int hdfs3_crc32c_verify_packets(hdfs3_crc_ctx *ctx, const void *arena, size_t ar
     if (s.done) HIP_TRY(hipEventSynchronize(s.done));
     if (int rc = finish_pending(s)) return rc;
     if (int rc = grow_slot(s, arena_len, 4)) return rc;
-    std::memcpy(s.h_data, arena, arena_len);
+    CopyPool::get().copy(s.h_data, arena, arena_len);  // split over the pool from 2 MiB up
     HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, arena_len, hipMemcpyHostToDevice, ctx->stream));
     return packets_common(ctx, s.d_data, arena_len, pk, n, bpc, true, check_short_tail, bad_packet,
                           bad_chunk);

@@ -163,6 +163,22 @@ def test_packets_api(gpu_ctx, bpc):
     assert np.array_equal(gpu_ctx.download(d2, arena.nbytes), arena)
 
 
+@pytest.mark.parametrize("n_pkts", [33, 70])
+def test_packets_api_large_host_arena(gpu_ctx, n_pkts):
+    """A host packet arena of MiBs (odd length: a short last packet) is staged through the host
+    copy pool: a flip in the arena's very last byte must still be found, in the last packet's
+    last chunk (local semantics check the short tail)."""
+    rng = np.random.default_rng(n_pkts)
+    arena, pk = _wire_arena(n_pkts, 512, rng)
+    assert arena.nbytes > (2 << 20)
+    assert gpu_ctx.verify_packets(arena, pk, 512, True) == (-1, -1)
+    bad = arena.copy()
+    bad[-1] ^= 0x01
+    data_off, crc_off, data_len = pk[-1]
+    assert data_off + data_len == arena.nbytes
+    assert gpu_ctx.verify_packets(bad, pk, 512, True) == (n_pkts - 1, (data_len - 1) // 512)
+
+
 @pytest.mark.parametrize("bpc", [512, 2048, 4096])
 def test_full_size_stream_1gib_roundtrip(gpu_ctx, bpc):
     """Config 3: 1 GiB stream, compute (write) then verify (read); every CRC word checked."""
