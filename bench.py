@@ -238,7 +238,8 @@ def run_steps(work, ctx, mode, n, result, events=None, base=0, overlap=False):
                                  result.data_ptr() + 8 * (s % result.numel()),
                                  overlap_previous=overlap and i > 0 and events is None)
         else:
-            ctx.compute_dev(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b))
+            ctx.compute_dev(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b),
+                            overlap_previous=overlap and i > 0 and events is None)
         if events is not None:
             events[2 * i + 1].record()
 
@@ -532,7 +533,7 @@ def main():
     torch.cuda.synchronize()
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the roofline pass")
-    overlap = args.mode == "verify" and not args.no_overlap
+    overlap = not args.no_overlap
     alg_bytes = work.nchunks * (args.bpc + 4)  # verify reads data + CRC; compute reads data, writes CRC
     # (0b) barriered pass (reported beside the overlapped `value`, first-class: it is what a
     # caller issuing one plain hdfs3_crc32c_verify_dev_async per block gets): max(D - K, 1000)

@@ -139,6 +139,13 @@ int64_t hdfs3_crc_decode_result(uint64_t result_word);
 int hdfs3_crc32c_verify_dev_async_ex(hdfs3_crc_ctx *ctx, const void *d_data, size_t len,
                                      uint32_t bpc, const void *d_crc_be, int check_short_tail,
                                      uint64_t *d_result, uint32_t flags);
+/* hdfs3_crc32c_compute_dev with launch flags (compute-on-write over resident blocks).
+ * HDFS3_LAUNCH_OVERLAP_PREVIOUS, under the same rule: the previous operation enqueued on
+ * the stream is a compute or verify launch of this library, this launch's data was ready
+ * before that one was enqueued, and neither launch reads what the other writes (each
+ * compute writes only its own CRC array). 0 = exactly hdfs3_crc32c_compute_dev. */
+int hdfs3_crc32c_compute_dev_async_ex(hdfs3_crc_ctx *ctx, const void *d_data, size_t len, uint32_t bpc,
+                                      void *d_crc_be_out, uint32_t flags);
 
 /* ---- batch of independent device-resident blocks -------------------------------
  * n blocks (each its own data, CRC array and length; chunk counts < 2^32) verified or

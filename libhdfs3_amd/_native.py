@@ -60,6 +60,7 @@ PUBLIC_API = {
     "hdfs3_crc32c_verify": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p, c_int,
                                     POINTER(c_int64)]),
     "hdfs3_crc32c_compute_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p]),
+    "hdfs3_crc32c_compute_dev_async_ex": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p, c_uint32]),
     "hdfs3_crc32c_verify_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p, c_int,
                                         POINTER(c_int64)]),
     "hdfs3_crc32c_verify_dev_async": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, c_void_p,

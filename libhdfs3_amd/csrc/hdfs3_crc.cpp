@@ -664,6 +664,22 @@ int hdfs3_crc32c_compute_dev(hdfs3_crc_ctx *ctx, const void *d_data, size_t len,
     return launch(ctx, a, false);
 }
 
+int hdfs3_crc32c_compute_dev_async_ex(hdfs3_crc_ctx *ctx, const void *d_data, size_t len, uint32_t bpc,
+                                      void *d_crc_be_out, uint32_t flags) {
+    if (int rc = check_args(ctx, bpc)) return rc;
+    if (flags & ~HDFS3_LAUNCH_OVERLAP_PREVIOUS) return fail(-EINVAL, "unknown launch flags 0x%x", flags);
+    if (len == 0) return 0;
+    if (!d_data || !d_crc_be_out) return fail(-EINVAL, "null buffer");
+    DeviceGuard g(ctx->device);
+    ChunkLaunch a{};
+    a.data = static_cast<const uint8_t *>(d_data);
+    a.len = len;
+    a.bpc = bpc;
+    a.out_be = static_cast<uint8_t *>(d_crc_be_out);
+    a.overlap_previous = (flags & HDFS3_LAUNCH_OVERLAP_PREVIOUS) != 0;
+    return launch(ctx, a, false);
+}
+
 int hdfs3_crc32c_verify_dev_async(hdfs3_crc_ctx *ctx, const void *d_data, size_t len,
                                   uint32_t bpc, const void *d_crc_be, int check_short_tail,
                                   uint64_t *d_result) {

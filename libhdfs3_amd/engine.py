@@ -144,7 +144,13 @@ class CrcContext:
         return bad.value
 
     # -- device-resident API --------------------------------------------------------
-    def compute_dev(self, d_data: int, nbytes: int, bpc: int, d_out: int) -> None:
+    def compute_dev(self, d_data: int, nbytes: int, bpc: int, d_out: int, overlap_previous: bool = False) -> None:
+        """overlap_previous: HDFS3_LAUNCH_OVERLAP_PREVIOUS (hdfs3_crc32c_compute_dev_async_ex; the
+        caller's guarantee is in include/hdfs3_crc.h)."""
+        if overlap_previous:
+            self._check("hdfs3_crc32c_compute_dev_async_ex",
+                  self._lib.hdfs3_crc32c_compute_dev_async_ex(self.ctx, d_data, nbytes, bpc, d_out, 1))
+            return
         self._check("hdfs3_crc32c_compute_dev",
               self._lib.hdfs3_crc32c_compute_dev(self.ctx, d_data, nbytes, bpc, d_out))
 

@@ -365,6 +365,33 @@ def test_overlapped_verify_chain_matches_oracle(gpu_ctx, bpc):
             assert got == (bad_chunk if i == bad_blk else -1), (r, i, got)
 
 
+@pytest.mark.parametrize("bpc", [512, 2048, 4096])
+def test_overlapped_compute_chain_matches_oracle(gpu_ctx, bpc):
+    """hdfs3_crc32c_compute_dev_async_ex with HDFS3_LAUNCH_OVERLAP_PREVIOUS: a chain of compute
+    launches over resident blocks (ragged lengths, each writing its own CRC array, then the
+    chain once more into fresh arrays) gives every block exactly the oracle's words."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    nblk = 6
+    lens = [(8 << 20) + (i * 4099 if i % 2 else 0) for i in range(nblk)]
+    blocks = []
+    for i, n in enumerate(lens):
+        data = splitmix_bytes(n, 0xC0DE + i + bpc)
+        want = oracle_compute(data, bpc)
+        outs = [DeviceBuffer(want.nbytes) for _ in range(2)]
+        for o in outs:
+            gpu_ctx.memset(o, 0xA5, want.nbytes)
+        blocks.append((gpu_ctx.upload(data), outs, n, want))
+    gpu_ctx.synchronize()
+    for r in range(2):
+        for i, (d, outs, n, _) in enumerate(blocks):
+            gpu_ctx.compute_dev(d.ptr, n, bpc, outs[r].ptr, overlap_previous=(r, i) != (0, 0))
+    gpu_ctx.synchronize()
+    for i, (_, outs, _, want) in enumerate(blocks):
+        for r in range(2):
+            assert np.array_equal(gpu_ctx.download(outs[r], want.nbytes), want), (i, r)
+
+
 def test_overlapped_chain_at_bench_size(gpu_ctx):
     """BASELINE configs[1] size through the bench's launch mode: 8 x 128 MiB blocks verified by
     overlapped single-block launches, three passes; a flipped bit in the LAST chunk of block 5
