@@ -365,11 +365,12 @@ def test_overlapped_verify_chain_matches_oracle(gpu_ctx, bpc):
             assert got == (bad_chunk if i == bad_blk else -1), (r, i, got)
 
 
-@pytest.mark.parametrize("bpc", [512, 2048, 4096])
+@pytest.mark.parametrize("bpc", [512, 2048, 4096, 516, 8192])
 def test_overlapped_compute_chain_matches_oracle(gpu_ctx, bpc):
     """hdfs3_crc32c_compute_dev_async_ex with HDFS3_LAUNCH_OVERLAP_PREVIOUS: a chain of compute
     launches over resident blocks (ragged lengths, each writing its own CRC array, then the
-    chain once more into fresh arrays) gives every block exactly the oracle's words."""
+    chain once more into fresh arrays) gives every block exactly the oracle's words. Chunk sizes
+    the wave kernel does not take (516, 8192) accept the flag and launch barriered."""
     from libhdfs3_amd.engine import DeviceBuffer
 
     nblk = 6
