@@ -433,3 +433,22 @@ def test_host_api_pageable_staging_every_byte(gpu_ctx, n):
         bad = data.copy()
         bad[-1] ^= 0x80  # the very last byte lives in the piece that used to be dropped
         assert gpu_ctx.verify(bad, bpc, want, True) == oracle_verify(bad, bpc, want, True) == (n - 1) // bpc
+
+
+def test_host_api_random_sizes_and_offsets(gpu_ctx):
+    """Host-buffer API over random lengths (1-40 MiB: one to three 16 MiB staging segments,
+    copies split over the copy pool) at random offsets into pageable numpy buffers, random
+    chunk sizes: every word the oracle's, and a flip at a random position found at its chunk."""
+    rng = np.random.default_rng(20261017)
+    base = splitmix_bytes((41 << 20) + 64, 0x5151)
+    for _ in range(12):
+        n = int(rng.integers(1 << 20, 40 << 20))
+        off = int(rng.integers(0, 64))
+        bpc = int(rng.choice([512, 1024, 2048, 4096, 516]))
+        data = base[off:off + n]
+        want = oracle_compute(data, bpc)
+        assert np.array_equal(gpu_ctx.compute(data, bpc), want), (n, off, bpc)
+        pos = int(rng.integers(0, n))
+        bad = data.copy()
+        bad[pos] ^= 0x02
+        assert gpu_ctx.verify(bad, bpc, want, True) == pos // bpc, (n, off, bpc, pos)
