@@ -230,3 +230,27 @@ def test_read_sizes_that_split_unevenly(tmp_path, piece, staging):
                 assert got > 0
                 pos += got
             assert pos == data.nbytes and np.array_equal(out, data), verify
+
+
+def test_random_offsets_and_read_sizes(tmp_path):
+    """Short-circuit reads with random block sizes, start offsets and read sizes (1 KiB to
+    6 MiB, so copies both below and above the copy pool's 2 MiB split): every byte returned is
+    the file's, verification on and off."""
+    from libhdfs3_amd.engine import LocalBlockReader
+
+    rng = np.random.default_rng(1017)
+    for case in range(6):
+        n = int(rng.integers(1 << 20, 12 << 20))
+        data = splitmix_bytes(n, 4000 + case)
+        d, m = write_block(tmp_path, f"blk_rand{case}", data)
+        start = int(rng.integers(0, n // 2))
+        for verify in (True, False):
+            with LocalBlockReader(d, m, offset=start, verify=verify) as r:
+                out = np.full(n - start, 0xEE, np.uint8)
+                pos = 0
+                while pos < out.nbytes:
+                    want = int(rng.integers(1 << 10, 6 << 20))
+                    got = r.read_into(out, pos, min(want, out.nbytes - pos))
+                    assert got > 0
+                    pos += got
+                assert np.array_equal(out, data[start:]), (case, verify, start)
