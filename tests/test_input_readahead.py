@@ -193,3 +193,38 @@ def test_readahead_off_again_and_pread_unaffected(cluster):
         assert s.pread_into(pos, out) == out.nbytes and np.array_equal(out, whole[pos:pos + out.nbytes])
         got, _ = _read_all(s, whole.nbytes - SIZES[0])
         assert np.array_equal(got, whole[SIZES[0]:])
+
+
+@pytest.mark.parametrize("ahead", [0, 2, 5])
+def test_random_walk_of_reads_seeks_and_preads(cluster, ahead):
+    """A seeded random walk of hdfsRead (1 B to 3 MiB), hdfsSeek (anywhere, block starts
+    included) and hdfsPread over the 6-block file, with and without read-ahead: every byte
+    equals the file's, read never crosses a block, tell follows the cursor."""
+    a, b, blocks, whole = cluster
+    starts = np.cumsum([0] + SIZES)
+    rng = np.random.default_rng(ahead + 77)
+    with _stream(blocks, [("127.0.0.1", a.port)], ahead) as s:
+        pos = 0
+        for _ in range(80):
+            op = rng.integers(0, 10)
+            if op < 6:
+                n = int(rng.integers(1, 3 << 20))
+                buf = np.zeros(n, np.uint8)
+                got = s.read_into(buf)
+                if pos >= whole.nbytes:
+                    assert got == 0
+                    continue
+                blk = np.searchsorted(starts, pos, side="right") - 1
+                assert 0 < got <= n and pos + got <= starts[blk + 1]
+                assert np.array_equal(buf[:got], whole[pos:pos + got])
+                pos += got
+            elif op < 8:
+                pos = int(rng.choice([rng.integers(0, whole.nbytes), starts[rng.integers(0, len(SIZES))]]))
+                s.seek(pos)
+            else:
+                p = int(rng.integers(0, whole.nbytes))
+                n = int(rng.integers(1, 3 << 20))
+                buf = np.zeros(n, np.uint8)
+                got = s.pread_into(p, buf)
+                assert got == min(n, whole.nbytes - p) and np.array_equal(buf[:got], whole[p:p + got])
+            assert s.tell() == pos
