@@ -63,6 +63,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
+    p.add_argument("--no-compute", action="store_true", help="skip the compute-on-write block of the line")
     p.add_argument("--sweep", action="store_true", help="extra diagnostics on stderr")
     p.add_argument("--graph", action="store_true",
                    help="replay the K steps from captured HIP graphs instead of launching them eagerly "
@@ -307,6 +308,55 @@ class StepGraphs:
             self.graphs[1].replay()
 
 
+def compute_block(torch, work, ctx, K, warm, stream, read_ceilings):
+    """Compute-on-write at the bench's shape (BASELINE.json configs[2]'s write half at configs[1]'s
+    block): `hdfs3_crc32c_compute_dev` over the same rotated blocks, one 128 MiB block per launch,
+    on the same clock as `value` (HIP events on the launch stream around K launches), overlapped
+    (HDFS3_LAUNCH_OVERLAP_PREVIOUS after the first) and barriered. The words go to fresh arrays
+    (poisoned before the timed run) and every word of every block is checked against the oracle
+    after the timed region. read_ceilings: (overlapped, barriered) same-shape plain-read GB/s."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from util import oracle_compute  # test infrastructure: the checker only, after timing
+
+    out = torch.full_like(work.crc, 0xA5)
+    alg = work.nchunks * (work.bpc + 4)  # reads C, writes 4 per chunk
+
+    def launches(n, overlap):
+        for i in range(n):
+            b = i % work.blocks
+            ctx.compute_dev(work.data_ptr(b), work.block_bytes, work.bpc, out[b].data_ptr(),
+                            overlap_previous=overlap and i > 0)
+
+    res = {"api": "hdfs3_crc32c_compute_dev", "alg_bytes_per_launch": alg,
+           "timing": "HIP events on the launch stream around K launches (the clock of value)"}
+    for name, overlap in (("overlapped", True), ("barriered", False)):
+        launches(warm, overlap)
+        out.fill_(0xA5)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        launches(K, overlap)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) * 1e-3 / K
+        r = {"value": round(work.block_bytes / t / 2**30, 2), "unit": "GiB/s", "avg_launch_us": round(t * 1e6, 2),
+             "achieved_GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}
+        ceil = read_ceilings[0 if overlap else 1] if read_ceilings else None
+        if ceil:
+            r["frac_of_achievable_per_block"] = round(alg / t / 1e9 / (ceil * alg / work.block_bytes), 4)
+        res[name] = r
+    # every word the timed launches wrote (the last K launches covered all blocks when K >= blocks)
+    host = out.cpu().numpy()
+    for b in range(min(K, work.blocks)):
+        want = oracle_compute(work.data[b].cpu().numpy(), work.bpc)
+        if not np.array_equal(host[b], want):
+            bad = int(np.nonzero(host[b] != want)[0][0]) // 4
+            raise SystemExit(f"PARITY FAILURE: compute block {b} chunk {bad} differs from the oracle")
+    res["checked"] = f"every CRC word of {min(K, work.blocks)} blocks against the oracle after the timed region"
+    return res
+
+
 def lab_context(work, stream):
     """A context of the measurement library (libhdfs3_crc_lab.so) on the bench's device and
     stream: the plain-read ceiling kernels live there, not in the product library."""
@@ -408,7 +458,9 @@ def cpu_baseline(work, seconds, bpc):
            "sample": f"{reps} x verify of one {data.nbytes >> 20} MiB block ({bpc} B chunks, "
                      f"RemoteBlockReader::verifyChecksum loop) split over {threads} threads "
                      f"(= len(os.sched_getaffinity(0))), {t:.1f} s; engine: {engine}",
-           "nproc": os.cpu_count(), "cgroup_cpu_quota_cores": quota}
+           "nproc": os.cpu_count(), "cgroup_cpu_quota_cores": quota,
+           # the threads share the cgroup's CPU quota: the rate is that many cores' worth of CPU time
+           "effective_cores": min(threads, quota) if quota else threads}
     g1, r1, t1 = timed(1, seconds / 3)
     out["one_core"] = {"value": round(g1, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
                        "sample": f"{r1} x verify of the same block on 1 thread, {t1:.1f} s"}
@@ -584,8 +636,9 @@ def main():
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the timed region")
     my_rate = block_bytes * K / elapsed / 2**30
-    rows = gather_per_rank(dist, world, rank, [rank, local % ndev, rank_seed(rank), elapsed, host_elapsed, my_rate],
-                           coll_device)
+    rows = gather_per_rank(dist, world, rank, [rank, torch.cuda.current_device(), rank_seed(rank), elapsed,
+                                               host_elapsed, my_rate], coll_device)
+    dist_world = dist.get_world_size() if dist.is_initialized() else 1
     elapsed_max = max(r[3] for r in rows)
     host_max = max(r[4] for r in rows)
     value = aggregate_rate(block_bytes * K, world, elapsed_max)
@@ -607,6 +660,7 @@ def main():
                 "eager_per_launch_us": round(eager_launch_s * 1e6, 2)}
     extra = {}
     lab = None
+    ceilings = None
     if world == 1:
         try:
             lab = lab_context(work, stream)
@@ -616,8 +670,10 @@ def main():
             # the same launch mode (overlapped or barriered)
             roofline["achievable_read_per_block_launch_GBps"] = round(per_block, 1)
             roofline["frac_of_achievable_per_block"] = round(achieved / (per_block * alg_bytes / block_bytes), 4)
+            ceilings = [per_block, None]
             if barriered is not None:
                 _, per_block_b = stream_read_ceiling(torch, work, lab, overlap=False)
+                ceilings[1] = per_block_b
                 barriered["achievable_read_per_block_launch_GBps"] = round(per_block_b, 1)
                 barriered["frac_of_achievable_per_block"] = round(
                     barriered["achieved_GBps"] / (per_block_b * alg_bytes / block_bytes), 4)
@@ -625,6 +681,12 @@ def main():
             log("stream ceiling failed:", e)
         if barriered is not None:
             extra["barriered"] = barriered
+        if args.mode == "verify" and not args.no_compute:
+            extra["compute"] = compute_block(torch, work, ctx, K, max(W, 500), stream, ceilings)
+            for m in ("overlapped", "barriered"):
+                v = roofline["frac"] if m == "overlapped" else (barriered or {}).get("frac")
+                if v:
+                    extra["compute"][m]["frac_vs_verify"] = round(extra["compute"][m]["frac"] / v, 4)
         try:
             extra["batched"] = batched_rate(torch, work, ctx, args.mode)
         except SystemExit:
@@ -657,16 +719,23 @@ def main():
                    "bpc": args.bpc, "block_bytes": block_bytes, "chunks_per_block": work.nchunks,
                    "blocks_rotated_per_gpu": args.blocks, "mode": args.mode,
                    "parallelism": f"{world} GPU(s), independent blocks one set per GPU, no collectives"},
+        "world_size": dist_world, "backend": backend if world > 1 else None,
         "roofline": roofline, "cpu_baseline": cpu,
-        "per_rank": [{"rank": int(r[0]), "device": int(r[1]), "seed": int(r[2]), "ms_per_step": round(r[3] / K * 1e3, 4),
+        "per_rank": [{"rank": int(r[0]), "current_device": int(r[1]), "seed": int(r[2]),
+                      "ms_per_step": round(r[3] / K * 1e3, 4),
                       "value": round(r[5], 2)} for r in rows],
     }
     if "barriered" in extra:
         line["barriered"] = extra["barriered"]
     if "batched" in extra:
         line["batched"] = extra["batched"]
+    if "compute" in extra:
+        line["compute"] = extra["compute"]
     if cpu:
         line["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        line["gpu_over_cpu_note"] = (f"against {cpu['effective_cores']} effective cores "
+                                     f"({cpu['cores']} threads under a cgroup quota of {cpu['cgroup_cpu_quota_cores']})"
+                                     if cpu.get("cgroup_cpu_quota_cores") else f"against {cpu['cores']} cores")
         if "pcl_port" in cpu and "all_cores" in cpu["pcl_port"]:
             line["gpu_over_cpu_pcl"] = round(value / cpu["pcl_port"]["all_cores"]["value"], 1)
     print(json.dumps(line), flush=True)

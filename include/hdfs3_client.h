@@ -202,6 +202,20 @@ typedef struct hdfs3_writer_opts {
  * not a multiple of it (OutputStreamImpl.cpp:258-273) */
 int hdfs3_output_open(const hdfs3_writer_opts *opts, hdfs3_packet_sink sink, void *user,
                       hdfs3_output_stream **out);
+/* Append (hdfsOpenFile with O_APPEND; OutputStreamImpl::initAppend, OutputStreamImpl.cpp:172-230):
+ * what the namenode's append() returns, supplied by the caller (the namenode is out of scope).
+ * The stream's tell() starts at file_length; the appended block's packets start at
+ * offsetInBlock = last_block_bytes. A file ending mid-chunk gets a first packet of ONE chunk of
+ * chunkSize - file_length % chunkSize bytes with its CRC over those bytes only; a file ending on a
+ * chunk boundary gets a first packet capped at the block's free space; the configured sizes return
+ * after the first full packet (:332-337). -EIO when the last block is already full (:191-196). */
+typedef struct hdfs3_append_info {
+    int64_t file_length;       /* FileStatus::getLength                                          */
+    int64_t last_block_bytes;  /* the last block's getNumBytes; -1 when append() returned no last
+                                  block (the file ends on a block boundary: writes start a new one) */
+} hdfs3_append_info;
+int hdfs3_output_open_append(const hdfs3_writer_opts *opts, const hdfs3_append_info *append, hdfs3_packet_sink sink,
+                             void *user, hdfs3_output_stream **out);
 int32_t hdfs3_output_write(hdfs3_output_stream *s, const void *buf, int32_t len);  /* hdfsWrite: len or -1 */
 int hdfs3_output_flush(hdfs3_output_stream *s);    /* hdfsFlush / hdfsHFlush: flushInternal(false) */
 int hdfs3_output_sync(hdfs3_output_stream *s);     /* hdfsSync: flushInternal(true)               */
@@ -239,6 +253,17 @@ typedef struct hdfs3_pipeline_opts {
 
 int hdfs3_pipeline_open(const hdfs3_located_block *blocks, int n_blocks, const char *client_name,
                         uint32_t bytes_per_checksum, const hdfs3_pipeline_opts *opts, hdfs3_pipeline **out);
+/* PipelineImpl(append = true) (Pipeline.cpp:58-81): blocks[0] is the file's last block as append()
+ * returned it (id, generation stamp, num_bytes = its length, its replicas as the pipeline nodes);
+ * its pipeline is set up with stage PIPELINE_SETUP_APPEND, minBytesRcvd = maxBytesRcvd = num_bytes
+ * and latestGenerationStamp = new_generation_stamp (updateBlockForPipeline's, :274-276), after
+ * which the block carries that stamp (lastBlock = lb, :327-334). blocks[1..] are the blocks
+ * addBlock allocates once it is full (PIPELINE_SETUP_CREATE). */
+int hdfs3_pipeline_open_append(const hdfs3_located_block *blocks, int n_blocks, uint64_t new_generation_stamp,
+                               const char *client_name, uint32_t bytes_per_checksum,
+                               const hdfs3_pipeline_opts *opts, hdfs3_pipeline **out);
+/* block i's generation stamp as the pipeline left it (the new stamp for an appended block) */
+int hdfs3_pipeline_generation_stamp(hdfs3_pipeline *p, int block, uint64_t *gs);
 /* an hdfs3_packet_sink (pass the pipeline as `user`): PipelineImpl::send, or ::close for a
  * block's last packet (waits for every ack of the block, then closes its connection) */
 int hdfs3_pipeline_send(void *pipeline, const void *packet, size_t len, const hdfs3_packet_info *info);
@@ -258,6 +283,10 @@ int hdfs3_pipeline_close(hdfs3_pipeline *p);
  * opts->bytes_per_checksum (-EINVAL). The stream does not own the pipeline. */
 int hdfs3_output_open_pipeline(const hdfs3_writer_opts *opts, hdfs3_pipeline *pipeline,
                                hdfs3_output_stream **out);
+/* the same over a pipeline opened by hdfs3_pipeline_open_append (or hdfs3_pipeline_open when
+ * append->last_block_bytes < 0) */
+int hdfs3_output_open_pipeline_append(const hdfs3_writer_opts *opts, const hdfs3_append_info *append,
+                                      hdfs3_pipeline *pipeline, hdfs3_output_stream **out);
 
 /* ------------------------------------------------------------------------------------
  * OP_BLOCK_CHECKSUM client (DataTransferProtocolSender::blockChecksum, a TODO in the

@@ -2,21 +2,27 @@
  * hdfs3_hdfs.h — libhdfs3's C file-I/O surface (src/client/hdfs.h) over the GPU-verified
  * streams of hdfs3_client.h.
  *
- * Every function below has exactly the prototype of the reference's hdfs.h (cited per
- * line), with the same argument checks, return values and errno convention as
- * src/client/Hdfs.cpp: a caller written against hdfs.h links against libhdfs3_crc.so and
- * runs unchanged. tests/test_reference_headers.py compiles the implementation
- * (csrc/client/hdfs_shim.cpp) with the reference's own hdfs.h force-included, so the
- * compiler checks that every definition matches the reference's declaration.
+ * The file-I/O functions below (hdfsOpenFile ... hdfsAvailable) have exactly the prototypes
+ * of the reference's hdfs.h (cited per line), with the same argument checks, return values and
+ * errno convention as src/client/Hdfs.cpp: code that reads and writes through an hdfsFS/hdfsFile
+ * compiles and links against libhdfs3_crc.so unchanged. tests/test_reference_headers.py compiles
+ * the implementation (csrc/client/hdfs_shim.cpp) with the reference's own hdfs.h force-included,
+ * so the compiler checks that every definition matches the reference's declaration.
  *
- * What stays outside the checksum path is the namenode: hdfsConnect/hdfsOpenFile resolve
- * a path through ClientProtocol RPC (getBlockLocations, create/addBlock) and a write
- * pipeline to datanodes (Pipeline.cpp). Here an hdfsFS is an in-process table that holds,
- * per path, what the namenode and the pipeline would provide:
- *   - for reading: the file's LocatedBlocks (hdfs3_fs_add_file), read through
- *     hdfs3_input_* (datanode OP_READ_BLOCK, GPU verify, replica failover);
- *   - for writing: a packet sink (hdfs3_fs_set_sink), fed by hdfs3_output_* with
- *     packets byte-identical to Packet::getBuffer whose CRCs the GPU computed.
+ * NOT provided: hdfsConnect / hdfsConnectAsUser / hdfsBuilderConnect and the rest of the
+ * namespace API (hdfsDelete, hdfsRename, hdfsListDirectory, hdfsGetPathInfo, ...). They are
+ * ClientProtocol RPC to the namenode, outside the checksum path. A caller obtains its hdfsFS
+ * from hdfs3_fs_new instead of hdfsConnect, and registers per path what the namenode would
+ * answer:
+ *   - getBlockLocations (for O_RDONLY, and append()'s file length and last block):
+ *     hdfs3_fs_add_file — read through hdfs3_input_* (datanode OP_READ_BLOCK, GPU verify,
+ *     replica failover);
+ *   - create/addBlock (for O_WRONLY): hdfs3_fs_set_pipeline (datanodes, OP_WRITE_BLOCK) or
+ *     hdfs3_fs_set_sink (a packet sink), fed by hdfs3_output_* with packets byte-identical to
+ *     Packet::getBuffer whose CRCs the GPU computed;
+ *   - updateBlockForPipeline's new generation stamp (for O_APPEND): hdfs3_fs_set_append_stamp.
+ * Those two lines of setup (hdfs3_fs_new + the registrations) replace hdfsConnect; everything
+ * after hdfsOpenFile runs as written against hdfs.h.
  */
 #ifndef HDFS3_HDFS_H
 #define HDFS3_HDFS_H
@@ -47,9 +53,13 @@ int hdfsFileIsOpenForRead(hdfsFile file);                               /* hdfs.
 int hdfsFileIsOpenForWrite(hdfsFile file);                              /* hdfs.h:96  */
 int hdfsDisconnect(hdfsFS fs);                                          /* hdfs.h:303 */
 /* O_RDONLY: the registered LocatedBlocks (ENOENT if none); O_WRONLY [| O_CREAT | O_SYNC]:
- * the registered sink (ENOENT if none), blocksize 0 = the fs's writer default, which must
- * be a multiple of the chunk size (EINVAL); O_RDWR, O_EXCL|O_CREAT: ENOTSUP (Hdfs.cpp:653);
- * O_APPEND (append to a partial last block, Pipeline recovery): ENOTSUP. */
+ * the registered pipeline or sink (ENOENT if none), blocksize 0 = the fs's writer default, which
+ * must be a multiple of the chunk size (EINVAL); O_RDWR, O_EXCL|O_CREAT: ENOTSUP (Hdfs.cpp:653);
+ * O_WRONLY|O_APPEND: append to the registered file (ENOENT if none): OutputStreamImpl::initAppend
+ * (OutputStreamImpl.cpp:172-230) with the file's length and, when it ends inside a block, its last
+ * block (file_length % blocksize != 0, blocksize as for O_WRONLY): written through a
+ * PIPELINE_SETUP_APPEND pipeline to that block's replicas (or the registered sink), further blocks
+ * through hdfs3_fs_set_pipeline's; a clean close registers the whole file for reading again. */
 hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, short replication,
                       tOffset blocksize);                                /* hdfs.h:319 */
 int hdfsCloseFile(hdfsFS fs, hdfsFile file);                            /* hdfs.h:332 */
@@ -85,6 +95,9 @@ int hdfs3_fs_set_sink(hdfsFS fs, const char *path, hdfs3_packet_sink sink, void 
  * hdfsOpenFile(O_RDONLY)/hdfsRead read back what was written. Takes precedence over a sink.
  * 0, or -1 with errno (EINVAL). */
 int hdfs3_fs_set_pipeline(hdfsFS fs, const char *path, const hdfs3_located_block *blocks, int n_blocks);
+/* the generation stamp updateBlockForPipeline would give `path`'s last block when it is next
+ * opened O_APPEND (Pipeline.cpp:274-276); unset: that block's stamp + 1. 0, or -1 with errno. */
+int hdfs3_fs_set_append_stamp(hdfsFS fs, const char *path, uint64_t new_generation_stamp);
 /* block read-ahead for files opened for reading from now on (hdfs3_input_set_readahead in
  * hdfs3_client.h; 0 blocks = off, the reference's one-block-at-a-time reading). 0, or -1 with
  * errno (EINVAL). */

@@ -165,6 +165,12 @@ class WriterOpts(ctypes.Structure):
                 ("block_size", c_int64), ("batch_packets", c_int)]
 
 
+class AppendInfo(ctypes.Structure):
+    """hdfs3_append_info (include/hdfs3_client.h)."""
+
+    _fields_ = [("file_length", c_int64), ("last_block_bytes", c_int64)]
+
+
 class PipelineOpts(ctypes.Structure):
     """hdfs3_pipeline_opts (include/hdfs3_client.h)."""
 
@@ -222,6 +228,13 @@ CLIENT_API = {
     "hdfs3_pipeline_error": (ctypes.c_char_p, [c_void_p]),
     "hdfs3_pipeline_close": (c_int, [c_void_p]),
     "hdfs3_output_open_pipeline": (c_int, [POINTER(WriterOpts), c_void_p, POINTER(c_void_p)]),
+    "hdfs3_output_open_append": (c_int, [POINTER(WriterOpts), POINTER(AppendInfo), PACKET_SINK, c_void_p,
+                                         POINTER(c_void_p)]),
+    "hdfs3_output_open_pipeline_append": (c_int, [POINTER(WriterOpts), POINTER(AppendInfo), c_void_p,
+                                                  POINTER(c_void_p)]),
+    "hdfs3_pipeline_open_append": (c_int, [POINTER(LocatedBlock), c_int, c_uint64, ctypes.c_char_p, c_uint32,
+                                           POINTER(PipelineOpts), POINTER(c_void_p)]),
+    "hdfs3_pipeline_generation_stamp": (c_int, [c_void_p, c_int, POINTER(c_uint64)]),
 }
 
 # every symbol include/hdfs3_hdfs.h declares (hdfs.h prototypes + the namenode stand-in)
@@ -247,6 +260,7 @@ HDFS_API = {
     "hdfs3_fs_set_sink": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_void_p]),
     "hdfs3_fs_set_pipeline": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_int]),
     "hdfs3_fs_set_readahead": (c_int, [c_void_p, c_int, c_int64]),
+    "hdfs3_fs_set_append_stamp": (c_int, [c_void_p, ctypes.c_char_p, c_uint64]),
 }
 
 # measurement hooks (libhdfs3_crc_lab.so only; not in any public header)
@@ -318,7 +332,8 @@ def loopback() -> ctypes.CDLL:
                               ("set_store_written", [c_int, c_int], c_int),
                               ("write_stats", [c_int] + [POINTER(c_uint64)] * 4, c_int),
                               ("get_block", [c_int, c_uint64, POINTER(c_void_p), POINTER(c_uint64), POINTER(c_void_p),
-                                             POINTER(c_uint32)], c_int)]:
+                                             POINTER(c_uint32)], c_int),
+                              ("block_gs", [c_int, c_uint64, POINTER(c_uint64)], c_int)]:
             f = getattr(lb, "hdfs3_loopback_" + fn)
             f.argtypes, f.restype = args, res
         _LOOPBACK = lb

@@ -85,6 +85,7 @@ struct FileEntry {
     void *user = nullptr;
     BlockTable pipeline_blocks;  // hdfs3_fs_set_pipeline: the blocks addBlock would allocate
     bool pipeline = false;
+    uint64_t append_gs = 0;      // hdfs3_fs_set_append_stamp (0: the last block's stamp + 1)
 };
 
 }  // namespace
@@ -105,6 +106,7 @@ struct HdfsFileInternalWrapper {
     hdfs3_output_stream *out = nullptr;
     hdfs3_pipeline *pipe = nullptr;  // writes through datanodes (hdfs3_fs_set_pipeline)
     BlockTable written;              // the pipeline's blocks, for completeFile
+    BlockTable prefix;               // append: the file's blocks before the pipeline's first one
     std::string path;
 };
 
@@ -160,6 +162,13 @@ int hdfs3_fs_set_pipeline(hdfsFS fs, const char *path, const hdfs3_located_block
     return 0;
 }
 
+int hdfs3_fs_set_append_stamp(hdfsFS fs, const char *path, uint64_t new_generation_stamp) {
+    PARAMETER_ASSERT(fs && path && std::strlen(path) > 0 && new_generation_stamp > 0, -1, EINVAL);
+    std::lock_guard<std::mutex> lk(fs->mu);
+    fs->files[path].append_gs = new_generation_stamp;
+    return 0;
+}
+
 int hdfs3_fs_set_sink(hdfsFS fs, const char *path, hdfs3_packet_sink sink, void *user) {
     PARAMETER_ASSERT(fs && path && std::strlen(path) > 0 && sink, -1, EINVAL);
     std::lock_guard<std::mutex> lk(fs->mu);
@@ -187,9 +196,8 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
     PARAMETER_ASSERT(fs && path && std::strlen(path) > 0, nullptr, EINVAL);
     PARAMETER_ASSERT(bufferSize >= 0 && replication >= 0 && blocksize >= 0, nullptr, EINVAL);
     PARAMETER_ASSERT(!(flags & O_RDWR) && !((flags & O_EXCL) && (flags & O_CREAT)), nullptr, ENOTSUP);
-    // appending to a block's partial last chunk needs the pipeline's recovery path
-    PARAMETER_ASSERT(!(flags & O_APPEND), nullptr, ENOTSUP);
-    const bool write = (flags & O_CREAT) || (flags & O_WRONLY);
+    const bool append = (flags & O_APPEND) != 0;
+    const bool write = (flags & O_CREAT) || (flags & O_WRONLY) || append;
     hdfsFile file = new (std::nothrow) HdfsFileInternalWrapper();
     if (!file) {
         set_msg("Out of memory");
@@ -202,9 +210,17 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
         // held across the open: hdfs3_input_open copies the located blocks out of the table
         std::lock_guard<std::mutex> lk(fs->mu);
         auto it = fs->files.find(path);
-        if (it == fs->files.end() || (write ? !it->second.sink && !it->second.pipeline : !it->second.located)) {
+        // append() needs the file (its located blocks stand in for the namenode's reply); a new file
+        // needs somewhere to write (a sink or the blocks addBlock would allocate)
+        const bool exists = it != fs->files.end() && it->second.located;
+        const bool missing = append ? !exists
+                             : write ? it == fs->files.end() || (!it->second.sink && !it->second.pipeline)
+                                     : !exists;
+        if (missing) {
             delete file;
-            set_msg((std::string(write ? "no write pipeline registered for " : "file does not exist: ") + path).c_str());
+            set_msg((std::string(write && !append ? "no write pipeline registered for " : "file does not exist: ") +
+                     path)
+                        .c_str());
             errno = ENOENT;  // FileNotFoundException -> ENOENT (Hdfs.cpp:243-327)
             return nullptr;
         }
@@ -220,14 +236,39 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
                 errno = EINVAL;
                 return nullptr;
             }
-            if (e.pipeline) {  // datanodes: PipelineImpl behind the stream
-                file->written = e.pipeline_blocks;
+            // append (OutputStreamImpl::initAppend, OutputStreamImpl.cpp:172-230): the file's located
+            // blocks play append()'s reply — its length, and its last block when that is partial
+            hdfs3_append_info ai{0, -1};
+            const hdfs3_located_block *last = nullptr;
+            if (append) {
+                const auto &lbs = e.located_blocks.blocks;
+                for (const hdfs3_located_block &b : lbs) ai.file_length += int64_t(b.block.num_bytes);
+                if (!lbs.empty() && ai.file_length % o.block_size != 0) {
+                    last = &lbs.back();
+                    ai.last_block_bytes = int64_t(last->block.num_bytes);
+                }
+            }
+            if (e.pipeline || (last && !e.sink)) {  // datanodes: PipelineImpl behind the stream
                 file->path = path;
-                rc = hdfs3_pipeline_open(file->written.blocks.data(), int(file->written.blocks.size()),
-                                         fs->client_name.c_str(), o.bytes_per_checksum, nullptr, &file->pipe);
-                if (rc == 0) rc = hdfs3_output_open_pipeline(&o, file->pipe, &file->out);
+                BlockTable t;
+                std::vector<hdfs3_located_block> pb;
+                if (last) pb.push_back(*last);  // its replicas are the append pipeline's nodes
+                if (e.pipeline) pb.insert(pb.end(), e.pipeline_blocks.blocks.begin(), e.pipeline_blocks.blocks.end());
+                t.assign(pb.data(), int(pb.size()));
+                file->written = t;
+                if (append) file->prefix.assign(e.located_blocks.blocks.data(),
+                                                int(e.located_blocks.blocks.size()) - (last ? 1 : 0));
+                if (last) {
+                    const uint64_t gs = e.append_gs ? e.append_gs : last->block.generation_stamp + 1;
+                    rc = hdfs3_pipeline_open_append(file->written.blocks.data(), int(file->written.blocks.size()), gs,
+                                                    fs->client_name.c_str(), o.bytes_per_checksum, nullptr, &file->pipe);
+                } else {
+                    rc = hdfs3_pipeline_open(file->written.blocks.data(), int(file->written.blocks.size()),
+                                             fs->client_name.c_str(), o.bytes_per_checksum, nullptr, &file->pipe);
+                }
+                if (rc == 0) rc = hdfs3_output_open_pipeline_append(&o, append ? &ai : nullptr, file->pipe, &file->out);
             } else {
-                rc = hdfs3_output_open(&o, e.sink, e.user, &file->out);
+                rc = hdfs3_output_open_append(&o, append ? &ai : nullptr, e.sink, e.user, &file->out);
             }
         } else {
             rc = hdfs3_input_open(e.located_blocks.blocks.data(), int(e.located_blocks.blocks.size()),
@@ -257,17 +298,21 @@ namespace {
 void complete_written_file(hdfsFS fs, hdfsFile file) {
     std::vector<int64_t> acked(file->written.blocks.size(), 0);
     hdfs3_pipeline_stats(file->pipe, acked.data(), int(acked.size()), nullptr, nullptr);
-    BlockTable t = file->written;
+    // an appended file keeps its earlier blocks; the appended one carries its new stamp
+    std::vector<hdfs3_located_block> all(file->prefix.blocks.begin(), file->prefix.blocks.end());
     int64_t off = 0;
-    size_t n = 0;
-    for (; n < acked.size() && acked[n] > 0; ++n) {
-        t.blocks[n].block.num_bytes = uint64_t(acked[n]);
-        t.blocks[n].offset = off;
+    for (const hdfs3_located_block &b : all) off += int64_t(b.block.num_bytes);
+    for (size_t n = 0; n < acked.size() && acked[n] > 0; ++n) {
+        hdfs3_located_block b = file->written.blocks[n];
+        b.block.num_bytes = uint64_t(acked[n]);
+        b.offset = off;
+        (void)hdfs3_pipeline_generation_stamp(file->pipe, int(n), &b.block.generation_stamp);
         off += acked[n];
+        all.push_back(b);
     }
     std::lock_guard<std::mutex> lk(fs->mu);
     FileEntry &slot = fs->files[file->path];
-    slot.located_blocks.assign(t.blocks.data(), int(n));
+    slot.located_blocks.assign(all.data(), int(all.size()));
     slot.located = true;
 }
 }  // namespace

@@ -91,6 +91,12 @@ struct hdfs3_output_stream {
     // OutputStreamImpl state
     int64_t cursor = 0, last_flushed = 0, bytes_written = 0, next_seqno = 0, block_index = 0;
     uint32_t position = 0;           // bytes of the current partial chunk
+    // initAppend (OutputStreamImpl.cpp:172-230): until the first packet has been sent full, the
+    // chunk size (chunkSize = freeInCksum when the file ends mid-chunk) and chunks per packet
+    // (1 then, or what the last block's free space allows) differ from the configured ones
+    bool is_append = false;
+    uint32_t chunk_cur = 512;        // chunkSize (buffer.size())
+    int cpp_cur = 0;                 // chunksPerPacket
     std::vector<uint8_t> carry;      // a flushed partial chunk, re-sent by the next packet
     bool pipeline_open = false;      // a packet of the current block has been sent
     int error = 0;
@@ -125,6 +131,8 @@ struct hdfs3_output_stream {
         crc_region = stride * uint64_t(batch_packets);
         arena_bytes = crc_region + 4ull * chunks_per_packet * batch_packets;
         carry.resize(bpc);
+        chunk_cur = bpc;
+        cpp_cur = chunks_per_packet;
         for (WBatch &b : batch) {
             HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&b.a.h), arena_bytes, hipHostMallocDefault));
             HIP_OK(hipMalloc(reinterpret_cast<void **>(&b.a.d), arena_bytes));
@@ -273,22 +281,55 @@ struct hdfs3_output_stream {
             // packet's or the block's end is one copy; appendChunkToPacket's per-chunk
             // bookkeeping (bytesWritten advances by whole chunks, position is the partial one)
             // is then applied for all the chunks it completed
-            const int64_t pkt_room = int64_t(chunks_per_packet) * bpc - cur->data_len;
+            const uint32_t cs = chunk_cur;
+            const int64_t pkt_room = int64_t(cpp_cur) * cs - cur->data_len;
             const int64_t blk_room = block_size - bytes_written - position;
             const uint32_t n = uint32_t(std::min({todo, pkt_room, blk_room}));
             std::memcpy(batch[cur_batch].a.h + cur->data_off + cur->data_len, buf + (size - todo), n);
             cur->data_len += n;
             todo -= n;
-            bytes_written += int64_t((position + n) / bpc) * bpc;
-            position = (position + n) % bpc;
-            const bool full = cur->data_len == uint32_t(chunks_per_packet) * bpc;
+            bytes_written += int64_t((position + n) / cs) * cs;
+            position = (position + n) % cs;
+            const bool full = cur->data_len == uint32_t(cpp_cur) * cs;
             if (full || bytes_written == block_size) {
                 send_current();
+                if (is_append) {  // back to the configured chunk and packet sizes (:332-337)
+                    is_append = false;
+                    chunk_cur = bpc;
+                    cpp_cur = chunks_per_packet;
+                }
                 if (bytes_written == block_size)
                     if (int rc = close_block()) return rc;
             }
         }
         cursor += size;
+        return 0;
+    }
+
+    // initAppend (:172-230) for a file of file_length bytes whose last block holds last_block_bytes
+    // (< 0: append() returned no last block, the next write starts a new block). The appended
+    // block's packets start at offsetInBlock = last_block_bytes; a file ending mid-chunk gets a
+    // first packet of ONE chunk of chunkSize - file_length % chunkSize bytes, its CRC over those
+    // bytes only (the datanode merges it with the partial chunk it holds).
+    int init_append(int64_t file_length, int64_t last_block_bytes) {
+        cursor = last_flushed = file_length;
+        if (last_block_bytes < 0) return 0;
+        const int64_t free_in_block = block_size - file_length % block_size;
+        if (free_in_block == block_size)
+            return fail(-EIO, "OutputStreamImpl: the last block for the file is full.");
+        is_append = true;
+        bytes_written = last_block_bytes;
+        const uint32_t used_in_cksum = uint32_t(file_length % bpc);
+        int64_t psize = packet_size;
+        if (used_in_cksum > 0) {
+            psize = 0;
+            chunk_cur = bpc - used_in_cksum;
+        } else {
+            psize = std::min<int64_t>(psize, free_in_block);
+        }
+        // computePacketChunkSize (:161-170), C++ division truncating toward zero
+        const int64_t with_sum = int64_t(chunk_cur) + 4;
+        cpp_cur = int(std::max<int64_t>(1, (psize - kHeader + with_sum - 1) / with_sum));
         return 0;
     }
 
@@ -324,19 +365,31 @@ extern "C" {
 
 int hdfs3_output_open_pipeline(const hdfs3_writer_opts *opts, hdfs3_pipeline *pipeline,
                                hdfs3_output_stream **out) {
+    return hdfs3_output_open_pipeline_append(opts, nullptr, pipeline, out);
+}
+
+int hdfs3_output_open_pipeline_append(const hdfs3_writer_opts *opts, const hdfs3_append_info *append,
+                                      hdfs3_pipeline *pipeline, hdfs3_output_stream **out) {
     if (!pipeline || !out) return fail(-EINVAL, "invalid argument");
     const uint32_t bpc = opts && opts->bytes_per_checksum ? opts->bytes_per_checksum : 512;
     if (bpc != pipeline_bpc(pipeline))
         return fail(-EINVAL, "the pipeline's bytes per checksum differ from the stream's");
-    if (int rc = hdfs3_output_open(opts, hdfs3_pipeline_send, pipeline, out)) return rc;
+    if (int rc = hdfs3_output_open_append(opts, append, hdfs3_pipeline_send, pipeline, out)) return rc;
     (*out)->pipeline = pipeline;
     return 0;
 }
 
 int hdfs3_output_open(const hdfs3_writer_opts *opts, hdfs3_packet_sink sink, void *user,
                       hdfs3_output_stream **out) {
+    return hdfs3_output_open_append(opts, nullptr, sink, user, out);
+}
+
+int hdfs3_output_open_append(const hdfs3_writer_opts *opts, const hdfs3_append_info *append, hdfs3_packet_sink sink,
+                             void *user, hdfs3_output_stream **out) {
     if (!out || !sink) return fail(-EINVAL, "invalid argument");
     *out = nullptr;
+    if (append && (append->file_length < 0 || append->last_block_bytes > append->file_length))
+        return fail(-EINVAL, "invalid append position");
     hdfs3_output_stream *s = new (std::nothrow) hdfs3_output_stream();
     if (!s) return fail(-ENOMEM, "output stream allocation");
     s->sink = sink;
@@ -360,7 +413,9 @@ int hdfs3_output_open(const hdfs3_writer_opts *opts, hdfs3_packet_sink sink, voi
     }
     // arenas, events and launches belong to the ctx's device, whatever is current here
     DeviceGuard g(device);
-    if (int rc = s->init()) {
+    int rc = s->init();
+    if (!rc && append) rc = s->init_append(append->file_length, append->last_block_bytes);
+    if (rc) {
         delete s;
         return rc;
     }

@@ -5,8 +5,10 @@
 // more than max_unacked packets are outstanding (:631-633, waitForAcks(false)) and at
 // flush / block close (waitForAcks(true), :755-813, :823-841).
 //
-// Per block: connect to the first node, OP_WRITE_BLOCK {PIPELINE_SETUP_CREATE, the other
-// nodes as targets, ChecksumProto{type, bpc}} and the BlockOpResponseProto check
+// Per block: connect to the first node, OP_WRITE_BLOCK {PIPELINE_SETUP_CREATE (or, for the
+// appended last block of hdfs3_pipeline_open_append, PIPELINE_SETUP_APPEND with the block's length
+// and the new generation stamp), the other nodes as targets, ChecksumProto{type, bpc}} and the
+// BlockOpResponseProto check
 // (createBlockOutputStream, :529-608); then [31 B header][BE32 CRC words][data] packets
 // exactly as the output stream built them (their CRCs computed on the GPU), each acked by a
 // PipelineAckProto carrying one status per node (processAck, :680-722).
@@ -41,6 +43,9 @@ struct BlockTarget {
     wire::ExtendedBlock id;
     std::vector<std::pair<std::string, int>> nodes;  // pipeline order
     int64_t acked = 0;                               // lastBlock->setNumBytes(bytesAcked)
+    bool append = false;        // PIPELINE_SETUP_APPEND: the file's last block, `base` bytes long
+    int64_t base = 0;
+    uint64_t new_gs = 0;        // updateBlockForPipeline's generation stamp
 };
 
 struct Outstanding {
@@ -91,14 +96,15 @@ struct hdfs3_pipeline {
         return n.first + ":" + std::to_string(n.second);
     }
 
-    // createBlockOutputStream (:529-608) for block b, stage PIPELINE_SETUP_CREATE
+    // createBlockOutputStream (:529-608) for block b: stage PIPELINE_SETUP_CREATE for a new block,
+    // PIPELINE_SETUP_APPEND for the appended last block (buildForAppendOrRecovery, :214-335)
     int setup(int64_t b) {
         if (b < 0 || b >= int64_t(blocks.size()))
             return sticky(-EIO, "Pipeline: no block allocated for block " + std::to_string(b) +
                                     " of the file (addBlock returned " + std::to_string(blocks.size()) + ")");
         cur = b;
-        bytes_sent = bytes_acked = 0;
         BlockTarget &t = blocks[size_t(b)];
+        bytes_sent = bytes_acked = t.append ? t.base : 0;  // PipelineImpl(bytesSent = offsetInBlock)
         const int s = net::connect_tcp(t.nodes[0].first.c_str(), t.nodes[0].second, timeout_ms);
         if (s < 0)
             return sticky(-EIO, "Cannot create block output stream for block " + block_name(t.id) +
@@ -106,7 +112,7 @@ struct hdfs3_pipeline {
         fd = s;
         wire::WriteBlockRequest req;
         req.block = t.id;
-        req.block.num_bytes = 0;  // lastBlock->getNumBytes() of a new block
+        req.block.num_bytes = t.append ? uint64_t(t.base) : 0;  // lastBlock->getNumBytes()
         req.client_name = client_name;
         for (size_t i = 1; i < t.nodes.size(); ++i) {
             wire::DatanodeAddr d;
@@ -114,7 +120,12 @@ struct hdfs3_pipeline {
             d.xfer_port = uint32_t(t.nodes[i].second);
             req.targets.push_back(d);
         }
-        req.stage = wire::kPipelineSetupCreate;
+        req.stage = t.append ? wire::kPipelineSetupAppend : wire::kPipelineSetupCreate;
+        if (t.append) {  // writeBlock(..., lastBlock->getNumBytes(), bytesSent, gs, ...) (:545-547)
+            req.min_bytes_rcvd = uint64_t(t.base);
+            req.max_bytes_rcvd = uint64_t(bytes_sent);
+            req.latest_generation_stamp = t.new_gs;
+        }
         req.pipeline_size = uint32_t(req.targets.size());
         req.checksum_type = checksum_type;
         req.bytes_per_checksum = bpc;
@@ -132,6 +143,7 @@ struct hdfs3_pipeline {
         if (resp.status != wire::kSuccess)
             return sticky(-EIO, "Bad connect ack with firstBadLink as " + resp.first_bad_link + " for block " +
                                     block_name(t.id));
+        if (t.append) t.id.generation_stamp = t.new_gs;  // lastBlock = lb (:327-334)
         return 0;
     }
 
@@ -266,6 +278,26 @@ int hdfs3_pipeline_open(const hdfs3_located_block *blocks, int n_blocks, const c
         p->blocks.push_back(std::move(t));
     }
     *out = p;
+    return 0;
+}
+
+int hdfs3_pipeline_open_append(const hdfs3_located_block *blocks, int n_blocks, uint64_t new_generation_stamp,
+                               const char *client_name, uint32_t bytes_per_checksum,
+                               const hdfs3_pipeline_opts *opts, hdfs3_pipeline **out) {
+    if (blocks && n_blocks > 0 && new_generation_stamp <= blocks[0].block.generation_stamp)
+        return fail(-EINVAL, "Pipeline: the new generation stamp must be above the last block's");
+    if (int rc = hdfs3_pipeline_open(blocks, n_blocks, client_name, bytes_per_checksum, opts, out)) return rc;
+    BlockTarget &t = (*out)->blocks[0];
+    t.append = true;
+    t.base = int64_t(blocks[0].block.num_bytes);
+    t.acked = t.base;
+    t.new_gs = new_generation_stamp;
+    return 0;
+}
+
+int hdfs3_pipeline_generation_stamp(hdfs3_pipeline *p, int block, uint64_t *gs) {
+    if (!p || !gs || block < 0 || block >= int(p->blocks.size())) return fail(-EINVAL, "invalid argument");
+    *gs = p->blocks[size_t(block)].id.generation_stamp;
     return 0;
 }
 

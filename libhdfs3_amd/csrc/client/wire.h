@@ -129,7 +129,13 @@ struct DatanodeAddr {              // DatanodeInfoProto.id (hdfs.proto:49-60,72-
     uint32_t info_port = 0;
     uint32_t ipc_port = 0;
 };
-enum BlockConstructionStage : int { kPipelineSetupCreate = 6, kPipelineClose = 4, kDataStreaming = 2 };
+// BlockConstructionStage (Pipeline.h:50-70)
+enum BlockConstructionStage : int {
+    kPipelineSetupAppend = 0,
+    kDataStreaming = 2,
+    kPipelineClose = 4,
+    kPipelineSetupCreate = 6
+};
 struct WriteBlockRequest {
     ExtendedBlock block;
     std::string client_name;

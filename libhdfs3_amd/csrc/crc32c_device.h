@@ -402,7 +402,9 @@ __device__ __forceinline__ uint32_t gf2_apply4(const uint32_t (&col)[32], uint32
 
 template <int DPP>
 __device__ __forceinline__ uint32_t dpp_xor(uint32_t v) {
-    return v ^ uint32_t(__builtin_amdgcn_update_dpp(0, int(v), DPP, 0xF, 0xF, false));
+    // bound_ctrl: every lane of these patterns has a source; it lets the DPP combiner fold the
+    // move into the xor (v_xor_b32_dpp), row_half_mirror included
+    return v ^ uint32_t(__builtin_amdgcn_update_dpp(0, int(v), DPP, 0xF, 0xF, true));
 }
 
 // XOR-reduce over aligned groups of G lanes; the group total lands in (at least) the
@@ -745,7 +747,7 @@ constexpr int kOptSoloHalf = 134217728;
 
 template <int BPC, bool VERIFY, int PAIR, bool NT = false, bool BUF = true, bool TRACE = false, bool PRIO = false,
           int OPT = 0>
-__global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a,
+__global__ __launch_bounds__(kBlockThreads) void crc32c_wave_r2_kernel(ChunkLaunch a,
                                                                     const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes, "one-round units only");
@@ -1947,10 +1949,10 @@ hipError_t launch_wave(const ChunkLaunch &a, const uint32_t *tab, const uint32_t
         int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
         if (grid < 1) grid = 1;
         if (ANY_ORDER || a.overlap_previous)  // AQL packet without the barrier bit (variant 16, opt-in flag)
-            hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
+            hipExtLaunchKernelGGL((crc32c_wave_r2_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
                                   dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, la, tab, nib);
         else
-            hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
+            hipLaunchKernelGGL((crc32c_wave_r2_kernel<BPC, V, PAIR, NT, BUF, TRACE, PRIO, OPT>), dim3(grid),
                                dim3(kBlockThreads), 0, s, la, tab, nib);
         return hipGetLastError();
     }

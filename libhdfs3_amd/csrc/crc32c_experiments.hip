@@ -5,6 +5,7 @@
 // (no HBM / no math / fake lookups / timestamps) give wrong results on purpose.
 #include "crc32c_block.h"
 #include "crc32c_wave2.h"
+#include "crc32c_wave.h"
 
 namespace hdfs3crc {
 namespace {
@@ -25,7 +26,7 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
         constexpr int G = BPC <= kRoundBytes ? BPC / 64 : 64;
         constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
         if constexpr (BPC <= kRoundBytes)
-            hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, 1>), dim3(grid_cap), dim3(kBlockThreads), 0, s, e,
+            hipLaunchKernelGGL((crc32c_wave_r2_kernel<BPC, V, 1>), dim3(grid_cap), dim3(kBlockThreads), 0, s, e,
                                tab, fold + kFoldWords + set * kFoldNibbleWords);
         return hipGetLastError();
     }
@@ -171,6 +172,28 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
         }
     }
+    case 90:
+    case 91: {  // the round-2 production kernel (before crc32c_wave.h): solo tail when overlapped
+        constexpr int kOpt = (BPC <= kRoundBytes ? kOptLeanFill : 0) | (!V && BPC == 512 ? kOptHoldStore : 0);
+        if (a.overlap_previous) {
+            if constexpr (V && BPC <= kRoundBytes) {
+                if (a.len <= (uint64_t(256) << 20))
+                    return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt | kOptSoloTail>(a, tab, fold,
+                                                                                                      grid_cap, s);
+            }
+            return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
+        }
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
+    }
+    case 92:  // the round-3 kernel with its prefetch issued at the start of each step (early)
+        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, false>(a, tab, fold, grid_cap, s);
+        return hipErrorInvalidValue;
+    case 93:  // the round-3 kernel, solo last step when overlapped (as the round-2 production)
+        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, true, true>(a, tab, fold, grid_cap, s);
+        return hipErrorInvalidValue;
+    case 94:  // 92 + solo last step when overlapped
+        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, false, true>(a, tab, fold, grid_cap, s);
+        return hipErrorInvalidValue;
     case 34: {  // 24 (no table math) with timestamps
         if (!g_trace) return hipErrorInvalidValue;
         ChunkLaunch e = a;

@@ -1,7 +1,7 @@
 // gfx950 (CDNA4) CRC32C kernels for libhdfs3's per-chunk checksum path: production
 // launchers. The device code (kernels, design notes) is in crc32c_device.h; the kernel
 // variants kept for A/B are in crc32c_experiments.hip.
-#include "crc32c_device.h"
+#include "crc32c_wave.h"
 
 namespace hdfs3crc {
 
@@ -12,39 +12,18 @@ uint64_t *g_trace = nullptr;  // timestamp buffer of the traced variants
 
 namespace {
 
-constexpr uint64_t kSoloTailMaxBytes = uint64_t(256) << 20;
-
 template <int BPC, bool V>
 hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                     hipStream_t s) {
-    // Production path: the wave kernel with the LDS nibble fold, two software-pipelined
-    // chains per lane and non-temporal data loads for bpc <= 4096 (the round kernel above
-    // that); an opted-in overlapped launch (HDFS3_LAUNCH_OVERLAP_PREVIOUS) goes out as an
-    // AQL packet without the barrier bit (the same kernel). Non-zero variants select the
-    // designs kept for in-process A/B (crc32c_experiments.hip, tools/ab.py).
-    // The table fill is the lean one (one slice-table word per thread; for bpc <= 2048 also
-    // the half fold image): variant 44 in the A/B, 1-1.5 % per 128 MiB launch. Compute at
-    // bpc 512 holds its CRC words in VGPRs and stores them in bursts (variant 47: -2.8 % per
-    // GiB, -0.8 % per 128 MiB; profiles/r01_kernel_study/ab_holdstore.jsonl).
+    // Production path: the round kernel of crc32c_wave.h for bpc <= 4096 (the multi-round kernel
+    // above that). An opted-in overlapped launch (HDFS3_LAUNCH_OVERLAP_PREVIOUS) goes out as an AQL
+    // packet without the barrier bit. Non-zero variants select the designs kept for in-process A/B
+    // (crc32c_experiments.hip, tools/ab.py; variant 90 = the round-2 production kernel).
 #if HDFS3_LAB
     if (g_variant != 0) return launch_experiment(g_variant, a, V, tab, fold, grid_cap, s);
 #endif
-    constexpr int kOpt = (BPC <= kRoundBytes ? kOptLeanFill : 0) | (!V && BPC == 512 ? kOptHoldStore : 0);
-    if (a.overlap_previous) {
-        // Overlapped verifies up to 256 MiB per launch end with the wave's last two rounds as
-        // single chains one after the other (kOptSoloTail, variant 78): a CU's workgroup frees
-        // its slot for the next launch sooner when less lookup work is left after its last data
-        // landed. 128 MiB: 21.94 -> 21.34 us per launch at bpc 512, 22.37 -> 21.60 at 2048; at
-        // 1 GiB per launch it is 1 % slower, and barriered launches lose 0.9 us, so both keep
-        // the interleaved last step (profiles/r02_kernel_study/r02_ab_solo_*.jsonl).
-        if constexpr (V && BPC <= kRoundBytes) {
-            if (a.len <= kSoloTailMaxBytes)
-                return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt | kOptSoloTail>(a, tab, fold,
-                                                                                                  grid_cap, s);
-        }
-        return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
-    }
-    return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
+    if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false>(a, tab, fold, grid_cap, s);
+    return launch_wave<BPC, V, 2, true>(a, tab, fold, grid_cap, s);
 }
 
 template <int BPC>
@@ -54,13 +33,18 @@ hipError_t launch_rv(const ChunkLaunch &a, bool verify, const uint32_t *tab, con
                   : launch_r<BPC, false>(a, tab, fold, grid_cap, s);
 }
 
-// packet streams at a constant pitch: the production wave kernel with kOptPitch
+// packet streams at a constant pitch: the production round kernel's pitch walk
 template <int BPC, bool V>
 hipError_t launch_p(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
-    constexpr int kOpt = kOptLeanFill | kOptPitch | (!V && BPC == 512 ? kOptHoldStore : 0);
-    if (a.overlap_previous)
-        return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
-    return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
+#if HDFS3_LAB
+    if (g_variant == 91) {  // A/B: the round-2 kernel's pitch mode
+        constexpr int kOpt = kOptLeanFill | kOptPitch | (!V && BPC == 512 ? kOptHoldStore : 0);
+        if (a.overlap_previous)
+            return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
+        return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
+    }
+#endif
+    return launch_wave3<BPC, V, true>(a, tab, fold, grid_cap, s);
 }
 
 template <int BPC>

@@ -1,0 +1,363 @@
+// The production round kernel (bpc 512 / 1024 / 2048 / 4096) of libhdfs3's per-chunk
+// CRC32C: verify-on-read (RemoteBlockReader::verifyChecksum, src/client/RemoteBlockReader.cpp:306-326;
+// LocalBlockReader::readAndVerify, src/client/LocalBlockReader.cpp:138-163) and compute-on-write
+// (OutputStreamImpl::appendInternal, src/client/OutputStreamImpl.cpp:298-359) over a whole block,
+// a constant-pitch packet stream or a list of segments in one launch. Internal; not installed.
+//
+// Work unit: a ROUND = 4 KiB of contiguous data, one wave at a time (crc32c_device.h: load_round_buf,
+// regroup, Lut, fold_half, group_xor). A wave consumes two rounds per STEP as two software-pipelined
+// lookup chains and has the next step's two rounds in flight while it does (8 KiB per wave, 128 KiB
+// per CU). The round -> data mapping is a WALK:
+//   BlockWalk   one contiguous block (unit u at data + 4096 u);
+//   PitchWalk   a packet stream at a constant pitch, or equal blocks of one 2-D tensor
+//               (unit u = round u & (upp - 1) of packet u >> log2(upp));
+//   SegWalk     a list of independent segments (ragged batches, packets in descriptor lists),
+//               the prefetch stream's current segment cached in scalar registers.
+// Every view a walk returns (data pointer, the round's CRC-word pointer, the key of its first chunk)
+// is wave-uniform, so its arithmetic is SALU and the word loads/stores take the saddr form.
+//
+// Loop shape (round 3). The buffers rotate A -> B -> A by unrolling, and the loop has ONE exit, at
+// its bottom: full steps (the ones with something to prefetch) run in pairs, then one more full step
+// if their count is odd, then the LAST step, which prefetches nothing. The round-2 kernel left its
+// loop from the middle of the body into two inlined tails; the register allocator then kept the
+// second step's rounds in two places and copied them (32 v_mov per step, +11 % VALU per round in the
+// PMC of the bench launch) and drained every load at the loop head (vmcnt(0)).
+#pragma once
+
+#include "crc32c_device.h"
+
+namespace hdfs3crc {
+namespace {
+
+typedef __attribute__((address_space(1))) const uint32_t gcu32;
+typedef __attribute__((address_space(1))) const uint8_t gcu8;
+typedef __attribute__((address_space(1))) uint8_t gu8;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// A round's view: data, CRC words of its first chunk (stored words when verifying, the output when
+// computing), result key of its first chunk.
+struct WView {
+    const uint8_t *p;
+    uint8_t *w;
+    uint64_t key;
+};
+
+// Rounds of one contiguous block: the wave's rounds are units wave, wave + W, ... (W = waves).
+template <int CPU>
+struct BlockWalk {
+    const uint8_t *data;
+    uint8_t *words;
+    uint64_t key0, first, stride;
+    uint32_t K;            // rounds of this wave (< 2^32: 16 TiB per launch); 32-bit so k < K is SALU
+    const uint8_t *dummy;  // the cache-resident 4 KiB table image: reads past the wave's last round
+    __device__ __forceinline__ WView view(uint32_t k) const {
+        const uint64_t u = first + uint64_t(k) * stride;
+        const bool in = k < K;
+        return WView{in ? data + u * kRoundBytes : dummy, in ? words + 4 * CPU * u : const_cast<uint8_t *>(dummy),
+                     key0 + CPU * u};
+    }
+};
+
+// A packet stream at one pitch: every packet but the last holds 1 << L whole rounds; its words sit
+// at words + packet * wpitch (the wire layout: in the packet; a [blocks, words] tensor: their own
+// pitch). Keys are (packet << 32) | chunk.
+template <int CPU>
+struct PitchWalk {
+    const uint8_t *data;
+    uint8_t *words;
+    uint64_t dpitch, wpitch, first, stride;
+    uint32_t K, L;
+    const uint8_t *dummy;
+    __device__ __forceinline__ WView view(uint32_t k) const {
+        const uint64_t u = first + uint64_t(k) * stride;
+        const uint64_t pk = u >> L, r = u & ((uint64_t(1) << L) - 1);
+        const bool in = k < K;
+        return WView{in ? data + pk * dpitch + r * kRoundBytes : dummy,
+                     in ? words + pk * wpitch + 4 * CPU * r : const_cast<uint8_t *>(dummy), (pk << 32) | (CPU * r)};
+    }
+};
+
+// The core: prologue, steps, last step. VERIFY: compare with the stored words and fold the first bad
+// key into *result; else store the words. SOLO: the last step runs its two rounds as single chains one
+// after the other (overlapped launches: the first chain overlaps the second round's arrival and only
+// one round's lookups remain once the wave's last data landed). HOLD (compute, bpc 512): the words of
+// 8 rounds are transposed into one VGPR and up to 8 such VGPRs are stored in one burst.
+template <int BPC, bool VERIFY, bool SOLO, bool HOLD, bool LATE, class Walk>
+__device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uint32_t *__restrict__ g_tab,
+                                            const uint32_t *__restrict__ g_nib, unsigned long long *result) {
+    constexpr int G = BPC / 64;
+    constexpr bool kHalfFold = G <= 32;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t j = lane % G;
+    const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
+    const uint32_t K = walk.K;
+
+    // lean fill: one slice-table word per thread replicated 32x; for G <= 32 the half fold image
+    const uint32_t tw = g_tab[threadIdx.x];
+    u32x4 n0, n1;
+    if constexpr (kHalfFold) {
+        const uint32_t t = threadIdx.x;
+        const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
+        n0 = *reinterpret_cast<const u32x4 *>(g_nib + (fk * 16 + fe) * 64 + fc);
+    } else {
+        n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
+        n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+    }
+    WView cv0 = walk.view(0), cv1 = walk.view(1);
+    __builtin_amdgcn_sched_barrier(0);
+    Round a0, a1, b0, b1;
+    load_round_buf<true>(a0, cv0.p, lane_off);
+    load_round_buf<true>(a1, cv1.p, lane_off);
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        const uint32_t tt = threadIdx.x, slice = tt >> 8, entry = tt & 255;
+        u32x4 *l4 = reinterpret_cast<u32x4 *>(lds);
+        const uint32_t slot0 = ((slice >> 1) << 16 | entry << 8 | (slice & 1) << 7) / 16;
+        // 32 copies as 8 x b128, rotated by thread so 8 neighbouring threads hit 8 bank groups
+#pragma unroll
+        for (int r = 0; r < 8; ++r) l4[slot0 + ((r + tt) & 7)] = u32x4{tw, tw, tw, tw};
+        if constexpr (kHalfFold) {
+            reinterpret_cast<u32x4 *>(lds + kPoolFoldOff / 4)[tt] = n0;
+        } else {
+            u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * tt;
+            dst[0] = n0;
+            dst[1] = n1;
+        }
+    }
+    lds_barrier();
+    const Lut t(lds);
+    const NibFold nf(lds);
+    auto fold = [&](uint32_t x) -> uint32_t {
+        if constexpr (kHalfFold) return fold_half(reinterpret_cast<const uint8_t *>(lds), x);
+        return nf.apply(x);
+    };
+    const uint32_t woff = 4 * (lane / G);  // this lane's chunk word within a round
+    WView pv0 = walk.view(2), pv1 = walk.view(3);
+
+    // The stored words through a buffer resource on the round's (wave-uniform) word base: the lane's
+    // offset is the only VGPR operand. A 64-bit VGPR address temporary may be allocated on registers
+    // of a round still in flight, and the waitcnt pass then drains every load at the loop head.
+    auto wrsrc = [](const WView &v) {
+        return __builtin_amdgcn_make_buffer_rsrc(v.w, 0, 4 * (kRoundBytes / BPC), 0x00020000);
+    };
+    auto want_of = [&](const WView &v) -> uint32_t {
+        if constexpr (VERIFY) return __builtin_amdgcn_raw_buffer_load_b32(wrsrc(v), woff, 0, 0);
+        return 0;
+    };
+    constexpr bool kHold = HOLD && !VERIFY && G == 8;
+    // kHold: lane 8r + c collects chunk c of round r of the current octet (8 rounds) in `line`; up to
+    // 8 closed octets wait in hold[] (hold[i] = octet hold_base + nheld - 1 - i) and go out in one
+    // burst. Their addresses come from the walk at flush time (lane-varying round index), so holding
+    // costs one VGPR per octet.
+    uint32_t line = 0;
+    uint32_t hold[kHold ? 8 : 1];
+    uint32_t nheld = 0, hold_base = 0;
+    auto flush = [&]() {
+#pragma unroll
+        for (int i = 0; i < (kHold ? 8 : 0); ++i) {
+            if (uint32_t(i) < nheld) {
+                const uint32_t kk = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
+                if (kk < K) *(gu32 *)((gu8 *)walk.view(kk).w + 4 * (lane & 7)) = __builtin_bswap32(hold[i]);
+            }
+        }
+        hold_base += nheld;
+        nheld = 0;
+    };
+    // y: the chunk's finished CRC (the affine fold image carries init and final xor)
+    auto finish = [&](uint32_t k, const WView &v, uint32_t y, uint32_t want) {
+        if constexpr (kHold) {
+            if (k >= K) return;
+            const uint32_t r = k & 7;
+            // group c's lanes all hold chunk c's state (group_xor is a butterfly)
+            const uint32_t got = uint32_t(__builtin_amdgcn_ds_bpermute(int(32 * (lane & 7)), int(y)));
+            line = (lane >> 3) == r ? got : line;
+            if (r == 7 || k + 1 == K) {
+#pragma unroll
+                for (int i = (kHold ? 7 : 0); i > 0; --i) hold[i] = hold[i - 1];
+                hold[0] = line;
+                if (++nheld == 8) flush();
+            }
+            return;
+        }
+        if (k >= K || j != 0) return;
+        const uint32_t c = y;
+        if constexpr (VERIFY) {
+            if (__builtin_bswap32(want) != c)
+                __hip_atomic_fetch_max((gu64 *)result, ~(unsigned long long)(v.key + lane / G), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bswap32(c), wrsrc(v), woff, 0, 0);
+        }
+    };
+    auto word = [](const Round &r, int i) -> uint32_t { return r.w[i >> 2][i & 3]; };
+    // two interleaved chains over c0, c1 (chain 1's 4 reads fly while chain 0 folds)
+    auto chains = [&](Round &c0, Round &c1, uint32_t &x0, uint32_t &x1) {
+        x0 = word(c0, 0);
+        x1 = word(c1, 0);
+        Look l0 = lookups(t, x0), l1;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            l1 = lookups(t, x1);
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = combine(l0, i < 15 ? word(c0, i < 15 ? i + 1 : 15) : 0u);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i < 15) l0 = lookups(t, x0);
+            __builtin_amdgcn_sched_barrier(0);
+            x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    // one round as a single chain. The two solo rounds of a last step end in different asm markers:
+    // identical code otherwise gets tail-merged into one copy that both run (register copies in).
+    auto solo = [&](Round &c, const WView &v, uint32_t k, uint32_t w, auto id) {
+        uint32_t x = word(c, 0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x = combine(lookups(t, x), i < 15 ? word(c, i < 15 ? i + 1 : 15) : 0u);
+        finish(k, v, group_xor<G>(fold(x)), w);
+        if constexpr (decltype(id)::value == 0) asm volatile("; solo round 0" ::: "memory");
+        else asm volatile("; solo round 1" ::: "memory");
+    };
+    // A step: the words of rounds k, k+1 are requested first (older than the prefetch, so waiting for
+    // them never drains it: vmcnt is in-order), then the prefetch of rounds k+2, k+3 into p0, p1 (past
+    // the wave's last round: the cache-resident table image), then the chains over c0, c1. The next
+    // views are resolved at the end. `fin` (wave-uniform) marks the wave's last step: with SOLO its
+    // rounds run as single chains one after the other.
+    auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k, bool fin) {
+        const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
+        if (!LATE) {
+            load_round_buf<true>(p0, pv0.p, lane_off);
+            load_round_buf<true>(p1, pv1.p, lane_off);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (SOLO && fin) {
+            regroup(c0);
+            solo(c0, cv0, k, w0, std::integral_constant<int, 0>{});
+            regroup(c1);
+            solo(c1, cv1, k + 1, w1, std::integral_constant<int, 1>{});
+        } else {
+            regroup(c0);
+            regroup(c1);
+            if constexpr (LATE) {
+                // the prefetch goes out once this step's rounds have landed: at most 8 KiB in
+                // flight per wave (128 KiB per CU), not 16 (more requests in flight lower the
+                // DRAM efficiency; the round-2 kernel got this by accident from
+                // register-reuse waits at its loop head)
+                __builtin_amdgcn_sched_barrier(0);
+                load_round_buf<true>(p0, pv0.p, lane_off);
+                load_round_buf<true>(p1, pv1.p, lane_off);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            uint32_t x0, x1;
+            chains(c0, c1, x0, x1);
+            finish(k, cv0, group_xor<G>(fold(x0)), w0);
+            finish(k + 1, cv1, group_xor<G>(fold(x1)), w1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        cv0 = pv0;
+        cv1 = pv1;
+        pv0 = walk.view(k + 4);
+        pv1 = walk.view(k + 5);
+    };
+
+    // The A -> B -> A rotation by unrolling, every step the same code (a special last step outside
+    // the loop made the register allocator copy the rounds: 32 v_mov per step in round 2).
+    const uint32_t nr = (K + 1) & ~1u;  // rounds rounded up to whole steps
+    for (uint32_t k = 0; k < nr; k += 4) {
+        step(a0, a1, b0, b1, k, k + 2 >= nr);
+        if (k + 2 >= nr) break;
+        step(b0, b1, a0, a1, k + 2, k + 4 >= nr);
+    }
+    if constexpr (kHold) flush();
+}
+
+// Slow region of one contiguous run: the chunks after its last whole round plus its short tail, one
+// chunk per thread of the grid (at most 8 + 1), 128-byte lines (crc_run_lines).
+template <int BPC, bool VERIFY>
+__device__ __forceinline__ void slow_region(const uint32_t *lds, const uint8_t *sdata, uint8_t *sw, uint64_t len,
+                                            uint64_t skey, int check_short_tail, unsigned long long *result) {
+    constexpr int kChunksPerUnit = kRoundBytes / BPC;
+    const Lut t(lds);
+    const uint64_t nfull = len / BPC;
+    const uint64_t first_slow = (len / kRoundBytes) * kChunksPerUnit;
+    const uint64_t nslow = nfull - first_slow + (len % BPC ? 1 : 0);
+    const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
+    const bool crc_al4 = (reinterpret_cast<uintptr_t>(sw) & 3u) == 0;
+    if (gtid < nslow) {
+        const uint64_t chunk = first_slow + gtid;
+        const uint32_t sz = chunk < nfull ? uint32_t(BPC) : uint32_t(len % BPC);
+        const uint32_t c = ~crc_run_lines(t, 0xFFFFFFFFu, sdata + chunk * BPC, sz);
+        if constexpr (VERIFY) {
+            if ((sz == uint32_t(BPC) || check_short_tail) && load_be32(sw + 4 * chunk, crc_al4) != c)
+                atomicMax(result, ~(unsigned long long)(skey + chunk));
+        } else {
+            store_be32(sw + 4 * chunk, c, crc_al4);
+        }
+    }
+}
+
+// One block (PITCH = false) or a constant-pitch stream (PITCH = true, ChunkLaunch::pitch/npk/...).
+template <int BPC, bool VERIFY, bool PITCH, bool SOLO, bool LATE = true>
+__global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
+                                                                    const uint32_t *__restrict__ g_nib) {
+    static_assert(BPC <= kRoundBytes && BPC % 512 == 0, "one-round units");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytesWave / 4];
+    constexpr int kCpu = kRoundBytes / BPC;
+    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
+    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *words = VERIFY ? const_cast<uint8_t *>(a.crc_be) : a.out_be;
+    const uint8_t *dummy = reinterpret_cast<const uint8_t *>(g_tab);
+    constexpr bool kHold = !VERIFY && BPC == 512;
+    if constexpr (PITCH) {
+        const uint64_t nunits = ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes;
+        // the division runs in VALU; readfirstlane puts K back in SGPRs so every k < K below is SALU
+        PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves,
+                          uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), a.upp_log2,
+                          dummy};
+        wave_rounds<BPC, VERIFY, SOLO, kHold, LATE>(w, lds, g_tab, g_nib, a.result);
+        const uint64_t lp = a.npk - 1;
+        slow_region<BPC, VERIFY>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
+                                 a.check_short_tail, a.result);
+    } else {
+        const uint64_t nunits = a.len / kRoundBytes;
+        BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves,
+                          uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), dummy};
+        wave_rounds<BPC, VERIFY, SOLO, kHold, LATE>(w, lds, g_tab, g_nib, a.result);
+        slow_region<BPC, VERIFY>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
+    }
+}
+
+// Overlapped verifies up to 256 MiB per launch end with the solo last step (21.94 -> 21.34 us per
+// 128 MiB launch at bpc 512 in round 2; 1 % slower at 1 GiB per launch, +0.9 us barriered:
+// profiles/r02_kernel_study/r02_ab_solo_*.jsonl).
+constexpr uint64_t kSoloTailMaxBytes = uint64_t(256) << 20;
+
+template <int BPC, bool V, bool PITCH, bool LATE = true, bool SOLO = false>
+hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
+    constexpr int G = BPC / 64;
+    constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
+    const uint32_t *nib = fold + kFoldAffineOff + set * kFoldNibbleWords;
+    const uint64_t units = PITCH ? ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes : a.len / kRoundBytes;
+    const uint64_t need = (units + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock);
+    int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
+    if (grid < 1) grid = 1;
+    if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
+        if constexpr (SOLO && V && !PITCH) {
+            if (units * kRoundBytes <= kSoloTailMaxBytes) {
+                hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LATE>), dim3(grid), dim3(kBlockThreads),
+                                      0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+                return hipGetLastError();
+            }
+        }
+        hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LATE>), dim3(grid), dim3(kBlockThreads), 0, s,
+                              nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+    } else {
+        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LATE>), dim3(grid), dim3(kBlockThreads), 0, s, a,
+                           tab, nib);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace hdfs3crc

@@ -47,10 +47,11 @@ int fail(int code, const char *fmt, ...) {
 namespace hdfs3crc {
 
 // Per polynomial ([0] CRC32C, [1] CRC32): slice tables, then the fold image (kFoldWords
-// matrix columns and 4 nibble-table sets for G = 8, 16, 32, 64), built once per process.
+// matrix columns, 4 nibble-table sets for G = 8, 16, 32, 64, the M_32 image and the 4 affine
+// sets of the production round kernel), built once per process.
 struct HostImage {
     uint32_t t[kSlices][kTableEntries];
-    uint32_t fold[kFoldWords + 4 * kFoldNibbleWords + kM32Words];
+    uint32_t fold[kFoldWords + 4 * kFoldNibbleWords + kM32Words + 4 * kFoldNibbleWords];
 };
 
 const HostImage *host_images() {
@@ -64,6 +65,9 @@ const HostImage *host_images() {
             for (int set = 0; set < 4; ++set)
                 build_fold_nibbles(img[p].fold, set, img[p].fold + kFoldWords + set * kFoldNibbleWords);
             build_m32_nibbles(img[p].t[0], img[p].fold + kFoldM32Off);
+            for (int set = 0; set < 4; ++set)
+                build_fold_affine(img[p].t[0], img[p].fold + kFoldWords + set * kFoldNibbleWords, set,
+                                  img[p].fold + kFoldAffineOff + set * kFoldNibbleWords);
         }
     });
     return img;

@@ -389,18 +389,32 @@ def _located_blocks(blocks, pool_id: bytes, generation_stamp: int):
 class Pipeline:
     """hdfs3_pipeline (include/hdfs3_client.h): PipelineImpl for a file's blocks.
     `blocks` = [(block_id, [(host, port), ...])]: what addBlock would return for each block,
-    pipeline nodes in order."""
+    pipeline nodes in order. append=(last_block_bytes, new_generation_stamp): blocks[0] is the
+    file's last block, appended to (hdfs3_pipeline_open_append, PIPELINE_SETUP_APPEND)."""
 
     def __init__(self, blocks, *, bytes_per_checksum: int = 512, timeout_ms: int = 60000, max_unacked: int = 1024,
-                 pool_id: bytes = b"BP-loopback", generation_stamp: int = 1, client_name: bytes = b"libhdfs3_amd"):
+                 pool_id: bytes = b"BP-loopback", generation_stamp: int = 1, client_name: bytes = b"libhdfs3_amd",
+                 append: tuple[int, int] | None = None):
         self._lib = _native.lib()
         self.n_blocks = len(blocks)
         arr, self._keep = _located_blocks([(bid, 0, nodes) for bid, nodes in blocks], pool_id, generation_stamp)
         opts = _native.PipelineOpts(timeout_ms, max_unacked, 0)
         p = c_void_p()
-        check("hdfs3_pipeline_open", self._lib.hdfs3_pipeline_open(arr, len(blocks), client_name, bytes_per_checksum,
-                                                                   byref(opts), byref(p)))
+        if append is None:
+            check("hdfs3_pipeline_open", self._lib.hdfs3_pipeline_open(arr, len(blocks), client_name,
+                                                                       bytes_per_checksum, byref(opts), byref(p)))
+        else:
+            arr[0].block.num_bytes = append[0]
+            check("hdfs3_pipeline_open_append",
+                  self._lib.hdfs3_pipeline_open_append(arr, len(blocks), append[1], client_name, bytes_per_checksum,
+                                                       byref(opts), byref(p)))
         self.p = p.value
+
+    def generation_stamp(self, block: int) -> int:
+        from ctypes import c_uint64
+        gs = c_uint64()
+        check("hdfs3_pipeline_generation_stamp", self._lib.hdfs3_pipeline_generation_stamp(self.p, block, byref(gs)))
+        return gs.value
 
     @property
     def error(self) -> str:
@@ -521,16 +535,19 @@ class OutputStream:
 
     def __init__(self, *, device: int = 0, bytes_per_checksum: int = 512, packet_size: int = 65536,
                  block_size: int = 64 << 20, batch_packets: int = 64, sink=None, raw_sink=None, raw_user=None,
-                 pipeline: "Pipeline | None" = None):
+                 pipeline: "Pipeline | None" = None, append: tuple[int, int] | None = None):
         """pipeline: write to datanodes through hdfs3_output_open_pipeline (flush/sync wait
-        for every node's ack) instead of a sink."""
+        for every node's ack) instead of a sink. append = (file_length, last_block_bytes): open
+        for append (hdfs3_output_open_append; last_block_bytes -1 = no partial last block)."""
         self._lib = _native.lib()
         self.pipeline = pipeline
+        ap = None if append is None else _native.AppendInfo(append[0], append[1])
         if pipeline is not None:
             opts = _native.WriterOpts(device, bytes_per_checksum, packet_size, block_size, batch_packets)
             p = c_void_p()
-            check("hdfs3_output_open_pipeline",
-                  self._lib.hdfs3_output_open_pipeline(byref(opts), pipeline.p, byref(p)))
+            check("hdfs3_output_open_pipeline_append",
+                  self._lib.hdfs3_output_open_pipeline_append(byref(opts), byref(ap) if ap is not None else None,
+                                                              pipeline.p, byref(p)))
             self.s = p.value
             return
         self.packets: list[tuple[bytes, dict]] = []
@@ -550,7 +567,9 @@ class OutputStream:
         self._cb = _native.PACKET_SINK(_sink) if raw_sink is None else ctypes.cast(raw_sink, _native.PACKET_SINK)
         opts = _native.WriterOpts(device, bytes_per_checksum, packet_size, block_size, batch_packets)
         p = c_void_p()
-        check("hdfs3_output_open", self._lib.hdfs3_output_open(byref(opts), self._cb, raw_user, byref(p)))
+        check("hdfs3_output_open_append",
+              self._lib.hdfs3_output_open_append(byref(opts), byref(ap) if ap is not None else None, self._cb,
+                                                 raw_user, byref(p)))
         self.s = p.value
 
     def _posix(self, fn: str, rc: int) -> int:

@@ -87,6 +87,12 @@ class LoopbackDatanode:
         crc = np.frombuffer(ctypes.string_at(c, 4 * nch), np.uint8).copy() if nch else np.zeros(0, np.uint8)
         return data, crc, bpc.value
 
+    def block_gs(self, block_id: int) -> int | None:
+        """the generation stamp a written block was finalized with (0: added to serve)"""
+        gs = ctypes.c_uint64()
+        rc = self.lb.hdfs3_loopback_block_gs(self.port, block_id, ctypes.byref(gs))
+        return None if rc != 0 else gs.value
+
     def stop(self) -> None:
         if self.port:
             self.lb.hdfs3_loopback_stop(self.port)

@@ -153,3 +153,67 @@ def test_invalid_configuration_rejected():
         OutputStream(block_size=1000)  # not a multiple of 512
     with pytest.raises(Hdfs3CrcError):
         OutputStream(packet_size=100)  # below the chunk size
+
+
+def run_append(ops, data, append, **cfg):
+    """the GPU output stream and the reference model, both opened for append"""
+    from libhdfs3_amd.engine import OutputStream
+
+    model = OutputStreamModel(crc, bpc=cfg.get("bytes_per_checksum", 512), packet_size=cfg.get("packet_size", 65536),
+                              block_size=cfg.get("block_size", 64 << 20), append=append)
+    gpu = OutputStream(append=append, **cfg)
+    assert gpu.tell() == model.cursor == append[0]
+    pos = 0
+    for op, n in ops:
+        if op == "w":
+            model.write(data[pos:pos + n].tobytes())
+            assert gpu.write(data[pos:pos + n]) == n
+            pos += n
+            assert gpu.tell() == model.cursor
+        elif op == "f":
+            model.flush()
+            gpu.flush()
+        elif op == "s":
+            model.sync()
+            gpu.sync()
+    model.close()
+    gpu.close()
+    return model.sent, gpu.packets
+
+
+BS = 1 << 20
+
+
+@pytest.mark.parametrize("append", [
+    (3 * BS + 5 * 512 + 100, 5 * 512 + 100),   # ends mid-chunk: one 412-byte chunk first
+    (3 * BS + 5 * 512 + 511, 5 * 512 + 511),   # one byte short of a chunk
+    (3 * BS + 1, 1),                           # one byte into a block
+    (3 * BS + 7 * 512, 7 * 512),               # on a chunk boundary: packet capped by free space
+    (4 * BS - 512, BS - 512),                  # one chunk short of a block
+    (4 * BS - 1, BS - 1),                      # one byte short of a block
+    (4 * BS, -1),                              # on a block boundary: no last block
+])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_append_packets_identical_to_reference_model(append, seed):
+    """initAppend (OutputStreamImpl.cpp:172-230): the packets of an append, flushes and syncs
+    included, are byte-identical to the reference model's; the partial chunk's CRC covers the
+    appended bytes only."""
+    rng = random.Random(seed * 1000 + append[0] % 997)
+    data = splitmix_bytes(3 << 20, seed + 40)
+    ops = random_ops(rng, data.nbytes, flush_p=0.15)
+    if seed == 2:
+        ops = [("w", 7), ("f", 0)] + ops  # a flush inside the partial chunk first
+    want, got = run_append(ops, data, append, block_size=BS, batch_packets=4)
+    assert len(got) == len(want)
+    for i, ((gp, gi), (wp, wi)) in enumerate(zip(got, want)):
+        assert gi == wi, (i, gi, wi)
+        assert gp == wp, i
+
+
+def test_append_to_full_last_block_is_eio():
+    from libhdfs3_amd.engine import OutputStream
+    from libhdfs3_amd._native import Hdfs3CrcError
+
+    with pytest.raises(Hdfs3CrcError) as ei:
+        OutputStream(append=(2 * BS, BS), block_size=BS)
+    assert ei.value.rc == -errno.EIO

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-3 kernel pass: -m gpu suite on the new round kernel, in-process A/B against the round-2
+# kernel (lab variant 90) in both launch modes and compute, then the default bench line.
+set -o pipefail
+TAG=${1:-r3a}
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    -p no:cacheprovider > gpurun_out/${TAG}_gpu_tests.txt 2>&1 \
+    || { echo "gpu tests failed"; tail -40 gpurun_out/${TAG}_gpu_tests.txt; exit 1; }
+tail -3 gpurun_out/${TAG}_gpu_tests.txt
+timeout -k 10 240 python -u tools/ab.py --variants 0,90 --bpc 512,2048,4096 --overlap --rounds 9 --reps 100 \
+    > gpurun_out/${TAG}_ab_ovl.jsonl 2> gpurun_out/${TAG}_ab_ovl.err || { echo "ab ovl failed"; tail gpurun_out/${TAG}_ab_ovl.err; exit 1; }
+cat gpurun_out/${TAG}_ab_ovl.jsonl
+timeout -k 10 240 python -u tools/ab.py --variants 0,90 --bpc 512,4096 --rounds 9 --reps 100 \
+    > gpurun_out/${TAG}_ab_bar.jsonl 2> gpurun_out/${TAG}_ab_bar.err || { echo "ab bar failed"; tail gpurun_out/${TAG}_ab_bar.err; exit 1; }
+cat gpurun_out/${TAG}_ab_bar.jsonl
+timeout -k 10 240 python -u tools/ab.py --mode compute --variants 0,90 --bpc 512,4096 --rounds 9 --reps 100 \
+    > gpurun_out/${TAG}_ab_cmp.jsonl 2> gpurun_out/${TAG}_ab_cmp.err || { echo "ab cmp failed"; tail gpurun_out/${TAG}_ab_cmp.err; exit 1; }
+cat gpurun_out/${TAG}_ab_cmp.jsonl
+timeout -k 10 300 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
+    || { echo "bench failed"; tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
+cat gpurun_out/${TAG}_bench.json

@@ -15,8 +15,10 @@
 // CRC words when it is the last node of the pipeline (as HDFS's BlockReceiver does), stores
 // the block and acks every packet with PipelineAckProto{seqno, [own status] + downstream
 // statuses} from a responder thread. After the last packet's ack the block is readable
-// through OP_READ_BLOCK. Fault injection: refuse the setup, an error status or a dropped
-// connection at a seqno, bytes corrupted in transit at a seqno.
+// through OP_READ_BLOCK. PIPELINE_SETUP_APPEND continues a replica this node holds (length and
+// stamp checked; the appended block takes the new generation stamp; a packet completing a partial
+// chunk gets that chunk's stored word recomputed over the whole chunk). Fault injection: refuse the
+// setup, an error status or a dropped connection at a seqno, bytes corrupted in transit at a seqno.
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -54,6 +56,7 @@ struct Block {
     uint32_t bpc;
     int type;
     std::shared_ptr<Stored> keep;  // owner of data/crc_be for written blocks
+    uint64_t gs = 0;               // generation stamp (0: not tracked, as for blocks added to serve)
 };
 
 enum WriteFault : int { kNoFault = 0, kRefuseSetup = 1, kAckError = 2, kCorruptInTransit = 3, kDropAt = 4 };
@@ -202,6 +205,35 @@ void serve_write(Server *sv, int fd, const std::string &proto, int version, int 
         net::close_fd(fd);
         return;
     }
+    // PIPELINE_SETUP_APPEND: this node must hold the replica at the client's length and stamp; the
+    // block continues from its bytes and takes the new generation stamp (BlockReceiver append)
+    std::shared_ptr<Stored> base;
+    if (req.stage == wire::kPipelineSetupAppend) {
+        Block b{};
+        bool found = false;
+        {
+            std::lock_guard<std::mutex> lk(sv->mu);
+            auto it = sv->blocks.find(req.block.block_id);
+            if (it != sv->blocks.end()) b = it->second, found = true;
+        }
+        const char *why = !found ? "replica not found"
+                          : b.len != req.min_bytes_rcvd || b.len != req.block.num_bytes ? "replica length mismatch"
+                          : b.gs && b.gs != req.block.generation_stamp ? "replica generation stamp mismatch"
+                          : req.latest_generation_stamp <= req.block.generation_stamp ? "stale new generation stamp"
+                          : b.bpc != req.bytes_per_checksum ? "bytes per checksum mismatch"
+                                                            : nullptr;
+        if (why) {
+            resp.status = wire::kErrorInvalid;
+            resp.message = why;
+            resp.first_bad_link = self;
+            (void)net::write_delimited(fd, wire::encode_block_op_response(resp), to);
+            net::close_fd(fd);
+            return;
+        }
+        base = std::make_shared<Stored>();
+        base->data.assign(b.data, b.data + b.len);
+        base->crc_be.assign(b.crc_be, b.crc_be + 4 * ((b.len + b.bpc - 1) / b.bpc));
+    }
     int down = -1;  // mirror to the next node of the pipeline
     if (!req.targets.empty()) {
         const wire::DatanodeAddr next = req.targets[0];
@@ -232,7 +264,8 @@ void serve_write(Server *sv, int fd, const std::string &proto, int version, int 
     }
     const uint32_t bpc = req.bytes_per_checksum;
     const bool verify = down < 0 && req.checksum_type == wire::kChecksumCrc32c;  // the last node verifies
-    auto stored = std::make_shared<Stored>();
+    auto stored = base ? base : std::make_shared<Stored>();
+    const uint64_t final_gs = base ? req.latest_generation_stamp : req.block.generation_stamp;
 
     std::mutex qmu;
     std::condition_variable qcv;
@@ -275,7 +308,7 @@ void serve_write(Server *sv, int fd, const std::string &proto, int version, int 
                 std::lock_guard<std::mutex> lk(sv->mu);
                 const uint64_t len = stored->data.size();
                 sv->blocks[req.block.block_id] =
-                    Block{stored->data.data(), len, stored->crc_be.data(), bpc, req.checksum_type, stored};
+                    Block{stored->data.data(), len, stored->crc_be.data(), bpc, req.checksum_type, stored, final_gs};
                 ++sv->blocks_finalized;
             }
             if (it.last) return;
@@ -322,13 +355,26 @@ void serve_write(Server *sv, int fd, const std::string &proto, int version, int 
         if (status == wire::kSuccess && h.data_len > 0 && sv->store_written) {
             // a re-sent partial chunk (after hflush) overwrites from offsetInBlock
             const uint64_t off = uint64_t(h.offset_in_block);
-            if (off > stored->data.size() || off % bpc) {
+            if (off > stored->data.size() || (off % bpc && !base)) {
                 status = wire::kErrorInvalid;
-            } else {
+            } else if (off % bpc == 0) {
                 stored->data.resize(off);
                 stored->crc_be.resize(off / bpc * 4);
                 stored->data.insert(stored->data.end(), data, data + h.data_len);
                 stored->crc_be.insert(stored->crc_be.end(), sums, sums + 4 * chunks);
+            } else {
+                // appended bytes that complete a partial chunk: the packet's words cover the new
+                // bytes only, so the stored word of every chunk touched is recomputed over the
+                // whole chunk (the datanode's partial-chunk checksum handling)
+                stored->data.resize(off);
+                stored->data.insert(stored->data.end(), data, data + h.data_len);
+                const uint64_t c0 = off / bpc, n = stored->data.size();
+                stored->crc_be.resize(c0 * 4);
+                for (uint64_t c = c0; c * bpc < n; ++c) {
+                    const uint32_t w = g_crc(stored->data.data() + c * bpc, size_t(std::min<uint64_t>(bpc, n - c * bpc)));
+                    const uint8_t be[4] = {uint8_t(w >> 24), uint8_t(w >> 16), uint8_t(w >> 8), uint8_t(w)};
+                    stored->crc_be.insert(stored->crc_be.end(), be, be + 4);
+                }
             }
         }
         ++sv->write_packets;
@@ -601,6 +647,17 @@ int hdfs3_loopback_get_block(int port, uint64_t block_id, const void **data, uin
     if (len) *len = it->second.len;
     if (crc_be) *crc_be = it->second.crc_be;
     if (bpc) *bpc = it->second.bpc;
+    return 0;
+}
+
+/* the generation stamp a written block was finalized with (0 for blocks added to serve) */
+int hdfs3_loopback_block_gs(int port, uint64_t block_id, uint64_t *gs) {
+    Server *sv = find(port);
+    if (!sv || !gs) return -EINVAL;
+    std::lock_guard<std::mutex> lk(sv->mu);
+    auto it = sv->blocks.find(block_id);
+    if (it == sv->blocks.end()) return -ENOENT;
+    *gs = it->second.gs;
     return 0;
 }
 
