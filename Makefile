@@ -19,7 +19,7 @@ LABLIB   := $(LIBDIR)/libhdfs3_crc_lab.so
 LOOPBACK := $(LIBDIR)/libhdfs3_loopback.so
 
 # device/HIP translation units (built twice: product and lab), host-only ones (shared)
-HIP_SRCS := crc32c_kernels.hip hdfs3_crc.cpp multi_device.cpp client/block_reader.cpp client/input_stream.cpp \
+HIP_SRCS := crc32c_kernels.hip hdfs3_crc.cpp multi_device.cpp numa.cpp client/block_reader.cpp client/input_stream.cpp \
             client/output_stream.cpp client/local_reader.cpp client/block_checksum.cpp client/pipeline.cpp
 HOST_SRCS:= host_crc32c.cpp client/wire.cpp client/net.cpp md5.cpp client/hdfs_shim.cpp
 objname   = $(subst /,_,$(basename $(1))).o

@@ -116,9 +116,13 @@ int hdfs3_input_stats(hdfs3_input_stream *s, uint64_t *failovers, uint64_t *read
  * same bytes, at most to the block end per call; a prefetch that hit a ChecksumException or
  * I/O error hands back the bytes it verified and the stream fails that replica over from
  * there (readOneBlock). pread is unaffected. blocks = 0 turns it off. 0 or -errno. */
+#define HDFS3_READAHEAD_MAX_BLOCKS 8  /* -EINVAL above: each holds a ctx, a socket and a pinned ring */
 int hdfs3_input_set_readahead(hdfs3_input_stream *s, int blocks, int64_t max_bytes_per_block);
-/* block readers the read-ahead threads opened so far (diagnostics) */
-int hdfs3_input_readahead_stats(hdfs3_input_stream *s, uint64_t *prefetch_readers_opened);
+/* block readers the read-ahead threads opened so far, and those dropped on a local (GPU or pinned
+ * memory) fault, whose block was then read again on demand on the stream's own context
+ * (diagnostics) */
+int hdfs3_input_readahead_stats(hdfs3_input_stream *s, uint64_t *prefetch_readers_opened,
+                                uint64_t *prefetch_local_faults);
 int hdfs3_input_close(hdfs3_input_stream *s);
 
 /* ------------------------------------------------------------------------------------

@@ -78,6 +78,31 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx);
  * mix release with destroy for the same context. */
 int hdfs3_crc_ctx_acquire(int device, hdfs3_crc_ctx **out);
 void hdfs3_crc_ctx_release(hdfs3_crc_ctx *ctx);
+/* The pool's retained pinned host memory is capped process-wide: a released context first gives
+ * back cached arenas and staging until the pooled total fits, and is destroyed when it still does
+ * not. The cap is HDFS3_POOL_PINNED_MAX (bytes, or with a K/M/G suffix; read once) and defaults to
+ * 512 MiB; 0 pools nothing. The reference holds one packet buffer per reader
+ * (RemoteBlockReader.cpp:244) and nothing once it is closed. */
+typedef struct hdfs3_crc_pool_stats {
+    uint64_t pooled_contexts;   /* idle contexts in the pool                                  */
+    uint64_t pinned_bytes;      /* pinned host memory they retain (staging, arenas, results)   */
+    uint64_t device_bytes;      /* device memory they retain (tables, staging, arenas)         */
+    uint64_t pinned_cap_bytes;  /* the cap above                                               */
+} hdfs3_crc_pool_stats;
+int hdfs3_crc_pool_stats_get(hdfs3_crc_pool_stats *out);
+/* Destroy every pooled (idle) context, returning its pinned and device memory; contexts in use
+ * are not affected. Returns the number destroyed. */
+int hdfs3_crc_pool_trim(void);
+
+/* NUMA-local placement. Every thread the library runs for a device (the multi-device
+ * workers, the block readers' receivers, the local readers' loaders) binds itself to the CPUs of
+ * that device's NUMA node, intersected with the process's allowed CPUs, and allocates its pinned
+ * staging there; HDFS3_NUMA=0 turns this off. hdfs3_device_numa_node: the node of `device` from
+ * its PCI function (-1 when the platform does not say). hdfs3_numa_cpus: the policy's input for a
+ * PCI function under a sysfs tree (sysfs_root "/sys" on a real host): the CPUs of its node, up to
+ * max_cpus of them in cpus[]; returns their count, 0 when the node is unknown, or -errno. */
+int hdfs3_device_numa_node(int device, int *node);
+int hdfs3_numa_cpus(const char *sysfs_root, const char *pci_bdf, int *cpus, int max_cpus);
 /* Attach an external hipStream_t (e.g. a framework's current stream); NULL
  * restores the ctx-owned stream. */
 int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream);

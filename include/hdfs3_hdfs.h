@@ -99,8 +99,8 @@ int hdfs3_fs_set_pipeline(hdfsFS fs, const char *path, const hdfs3_located_block
  * opened O_APPEND (Pipeline.cpp:274-276); unset: that block's stamp + 1. 0, or -1 with errno. */
 int hdfs3_fs_set_append_stamp(hdfsFS fs, const char *path, uint64_t new_generation_stamp);
 /* block read-ahead for files opened for reading from now on (hdfs3_input_set_readahead in
- * hdfs3_client.h; 0 blocks = off, the reference's one-block-at-a-time reading). 0, or -1 with
- * errno (EINVAL). */
+ * hdfs3_client.h; 0 blocks = off, the reference's one-block-at-a-time reading; at most
+ * HDFS3_READAHEAD_MAX_BLOCKS). 0, or -1 with errno (EINVAL). */
 int hdfs3_fs_set_readahead(hdfsFS fs, int blocks, int64_t max_bytes_per_block);
 
 #ifdef __cplusplus

@@ -51,6 +51,10 @@ PUBLIC_API = {
     "hdfs3_crc_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
     "hdfs3_crc_ctx_acquire": (c_int, [c_int, POINTER(c_void_p)]),
     "hdfs3_crc_ctx_release": (None, [c_void_p]),
+    "hdfs3_crc_pool_stats_get": (c_int, [c_void_p]),
+    "hdfs3_crc_pool_trim": (c_int, []),
+    "hdfs3_device_numa_node": (c_int, [c_int, POINTER(c_int)]),
+    "hdfs3_numa_cpus": (c_int, [ctypes.c_char_p, ctypes.c_char_p, POINTER(c_int), c_int]),
     "hdfs3_crc_ctx_destroy": (None, [c_void_p]),
     "hdfs3_crc_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
     "hdfs3_crc_ctx_get_stream": (c_void_p, [c_void_p]),
@@ -165,6 +169,13 @@ class WriterOpts(ctypes.Structure):
                 ("block_size", c_int64), ("batch_packets", c_int)]
 
 
+class PoolStats(ctypes.Structure):
+    """hdfs3_crc_pool_stats (include/hdfs3_crc.h)."""
+
+    _fields_ = [("pooled_contexts", c_uint64), ("pinned_bytes", c_uint64), ("device_bytes", c_uint64),
+                ("pinned_cap_bytes", c_uint64)]
+
+
 class AppendInfo(ctypes.Structure):
     """hdfs3_append_info (include/hdfs3_client.h)."""
 
@@ -205,7 +216,7 @@ CLIENT_API = {
     "hdfs3_input_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "hdfs3_input_close": (c_int, [c_void_p]),
     "hdfs3_input_set_readahead": (c_int, [c_void_p, c_int, c_int64]),
-    "hdfs3_input_readahead_stats": (c_int, [c_void_p, POINTER(c_uint64)]),
+    "hdfs3_input_readahead_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "hdfs3_local_reader_open": (c_int, [ctypes.c_char_p, ctypes.c_char_p, c_int64, c_int64, POINTER(LocalOpts),
                                         POINTER(c_void_p)]),
     "hdfs3_local_reader_read": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),
@@ -272,6 +283,7 @@ BENCH_API = {
     "hdfs3x_set_variant": (None, [c_int]),
     "hdfs3x_set_trace": (None, [c_void_p]),
     "hdfs3x_block_reader_timing": (c_int, [c_void_p, POINTER(c_uint64)]),
+    "hdfs3x_fail_prefetch_arenas": (None, [c_int]),
 }
 
 

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../ctx.h"
+#include "../numa.h"
 #include "block_reader.h"
 #include "hdfs3_crc.h"
 #include "net.h"
@@ -88,6 +89,12 @@ struct Timer {  // adds the scope's duration to a counter
 // another replica cannot cure (the input stream must not fail over on it).
 thread_local bool t_hip_fault = false;
 
+#if HDFS3_LAB
+// fault injection (libhdfs3_crc_lab.so only, tests/test_input_readahead.py): the next n arena
+// allocations of read-ahead (prefetch) readers fail as a pinned-memory shortage would
+std::atomic<int> g_fail_prefetch_arenas{0};
+#endif
+
 int hip_err(hipError_t e, const char *what) {
     t_hip_fault = true;
     return fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
@@ -105,7 +112,7 @@ int grow(PacketArena &a, size_t cap, size_t descs) {
         if (a.d) (void)hipFree(a.d);
         a.h = a.d = nullptr;
         a.cap = 0;
-        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h), cap, hipHostMallocDefault));
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h), cap, pinned_host_flags()));
         HIP_OK(hipMalloc(reinterpret_cast<void **>(&a.d), cap));
         a.cap = cap;
     }
@@ -114,13 +121,13 @@ int grow(PacketArena &a, size_t cap, size_t descs) {
         if (a.d_desc) (void)hipFree(a.d_desc);
         a.h_desc = a.d_desc = nullptr;
         a.desc_cap = 0;
-        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h_desc), descs * sizeof(DevSegment), hipHostMallocDefault));
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h_desc), descs * sizeof(DevSegment), pinned_host_flags()));
         HIP_OK(hipMalloc(reinterpret_cast<void **>(&a.d_desc), descs * sizeof(DevSegment)));
         a.desc_cap = descs;
     }
     if (!a.d_res) {
         HIP_OK(hipMalloc(reinterpret_cast<void **>(&a.d_res), sizeof(unsigned long long)));
-        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long), hipHostMallocDefault));
+        HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long), pinned_host_flags()));
         HIP_OK(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
     }
     return 0;
@@ -135,6 +142,7 @@ struct hdfs3_block_reader {
     bool verify = true;
     hdfs3_crc_ctx *ctx = nullptr;
     bool own_ctx = true;       // false when borrowed from an input stream
+    bool prefetch = false;     // opened ahead of the cursor with its own ring (slots > 0)
     wire::ExtendedBlock block;
     int64_t start = 0, end_offset = 0;
     uint32_t chunk_size = 0;
@@ -308,6 +316,12 @@ struct hdfs3_block_reader {
     // an arena for `b`: already owned, else one the ctx cached from an earlier reader, else new
     int acquire(Batch &b) {
         Timer tm(t_ns[1]);
+#if HDFS3_LAB
+        if (prefetch && g_fail_prefetch_arenas.load() > 0 && g_fail_prefetch_arenas.fetch_sub(1) > 0) {
+            t_hip_fault = true;
+            return rx_fail(fail(-ENOMEM, "injected pinned-memory shortage"), "arena allocation failed");
+        }
+#endif
         if (!b.a.h) {
             std::lock_guard<std::mutex> lk(ctx->arena_mu);
             if (!ctx->arena_cache.empty()) {
@@ -322,6 +336,8 @@ struct hdfs3_block_reader {
 
     void receiver() {
         (void)hipSetDevice(ctx->device);
+        // the socket's data lands in host memory here (RemoteBlockReader.cpp:245): on the GPU's node
+        bind_thread_to_device(ctx->device);
         for (;;) {
             int s;
             {
@@ -513,6 +529,7 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
     hdfs3_block_reader *r = new (std::nothrow) hdfs3_block_reader();
     if (!r) return fail(-ENOMEM, "reader allocation");
     r->slot.resize(size_t(std::min(std::max(slots > 0 ? slots : kSlots, kSlots), kMaxSlots)));
+    r->prefetch = slots > 0;
     const int device = opts ? opts->device : 0;
     r->verify = opts ? opts->verify != 0 : true;
     if (opts && opts->batch_packets > 0) r->batch_packets = opts->batch_packets;
@@ -581,6 +598,8 @@ int hdfs3_block_reader_stats(hdfs3_block_reader *r, uint32_t *bpc, uint64_t *pac
 }
 
 #if HDFS3_LAB
+void hdfs3x_fail_prefetch_arenas(int n) { g_fail_prefetch_arenas = n; }
+
 // measurement hook (libhdfs3_crc_lab.so only): nanoseconds spent per phase so far
 int hdfs3x_block_reader_timing(hdfs3_block_reader *r, uint64_t *out5) {
     if (!r || !out5) return fail(-EINVAL, "invalid argument");

@@ -179,7 +179,8 @@ int hdfs3_fs_set_sink(hdfsFS fs, const char *path, hdfs3_packet_sink sink, void 
 }
 
 int hdfs3_fs_set_readahead(hdfsFS fs, int blocks, int64_t max_bytes_per_block) {
-    PARAMETER_ASSERT(fs && blocks >= 0 && max_bytes_per_block >= 0, -1, EINVAL);
+    PARAMETER_ASSERT(fs && blocks >= 0 && blocks <= HDFS3_READAHEAD_MAX_BLOCKS && max_bytes_per_block >= 0, -1,
+                     EINVAL);
     std::lock_guard<std::mutex> lk(fs->mu);
     fs->readahead_blocks = blocks;
     fs->readahead_bytes = max_bytes_per_block;

@@ -76,6 +76,7 @@ struct hdfs3_input_stream {
     std::deque<Ahead> ahead;        // readers of blocks after `cur`, by block
     hdfs3_crc_ctx *reader_ctx = nullptr;  // the current reader's own ctx when it came from `ahead`
     uint64_t ahead_opened = 0;
+    uint64_t ahead_faults = 0;      // read-ahead readers dropped on a local fault and re-read on demand
 
     ~hdfs3_input_stream() {
         drop_ahead(-1);
@@ -212,10 +213,19 @@ struct hdfs3_input_stream {
                 cursor += n;
                 return n;
             }
-            // a local GPU/memory fault is not the replica's: report it, do not burn the replicas
+            // a local GPU/memory fault is not the replica's: report it, do not burn the replicas.
+            // A read-ahead reader faults on its own pooled ctx and deep ring, which an on-demand
+            // reader does not need: that block is read again on demand from the cursor on the
+            // stream's ctx, and only a fault there is reported (same bytes and errors as with
+            // read-ahead off)
             if (block_reader_local_fault(reader)) {
                 last_error = hdfs3_crc_last_error();
+                const bool prefetched = reader_ctx != nullptr;
                 drop_reader();
+                if (prefetched) {
+                    ++ahead_faults;
+                    continue;
+                }
                 return n < 0 ? n : -EIO;
             }
             // ChecksumException or I/O failure: this replica is bad, try another (:682-708)
@@ -398,15 +408,20 @@ int hdfs3_input_stats(hdfs3_input_stream *s, uint64_t *failovers, uint64_t *read
 
 int hdfs3_input_set_readahead(hdfs3_input_stream *s, int blocks, int64_t max_bytes_per_block) {
     if (!s || blocks < 0 || max_bytes_per_block < 0) return fail(-EINVAL, "invalid argument");
+    // every block opened ahead holds a pooled ctx, a connection and a pinned ring at once
+    if (blocks > HDFS3_READAHEAD_MAX_BLOCKS)
+        return fail(-EINVAL, "read-ahead of %d blocks: at most %d", blocks, HDFS3_READAHEAD_MAX_BLOCKS);
     s->ahead_blocks = blocks;
     s->ahead_bytes = max_bytes_per_block;
     if (blocks == 0) s->drop_ahead(-1);
     return 0;
 }
 
-int hdfs3_input_readahead_stats(hdfs3_input_stream *s, uint64_t *prefetch_readers_opened) {
+int hdfs3_input_readahead_stats(hdfs3_input_stream *s, uint64_t *prefetch_readers_opened,
+                                uint64_t *prefetch_local_faults) {
     if (!s) return fail(-EINVAL, "null stream");
     if (prefetch_readers_opened) *prefetch_readers_opened = s->ahead_opened;
+    if (prefetch_local_faults) *prefetch_local_faults = s->ahead_faults;
     return 0;
 }
 

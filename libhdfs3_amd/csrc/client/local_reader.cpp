@@ -42,6 +42,7 @@
 
 #include "../copy_pool.h"
 #include "../ctx.h"
+#include "../numa.h"
 #include "hdfs3_client.h"
 #include "hdfs3_crc.h"
 #include "wire.h"
@@ -252,6 +253,7 @@ struct hdfs3_local_reader {
 
     void run_loader() {
         (void)hipSetDevice(ctx->device);
+        bind_thread_to_device(ctx->device);  // preads land next to the GPU (numa.h)
         int64_t next = first;
         while (next < length) {
             int s;
@@ -460,16 +462,28 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
         for (int i = 0; i < kSlots; ++i) r->slot[i].a = pooled.a[i];
     } else {
         if (int rc = ctx_acquire(device, &r->ctx)) return bail(rc);
-        for (Window &w : r->slot) {
-            PacketArena &a = w.a;
-            if (hipHostMalloc(reinterpret_cast<void **>(&a.h), r->cap_data + crc_bytes, hipHostMallocDefault) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&a.d), r->cap_data + crc_bytes) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&a.d_res), sizeof(unsigned long long)) != hipSuccess ||
-                hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
-                hipEventCreateWithFlags(&a.done, hipEventDisableTiming) != hipSuccess)
-                return bail(fail(-ENOMEM, "LocalBlockReader: window allocation failed"));
-            a.cap = r->cap_data + crc_bytes;
-        }
+        // the windows are pinned from a thread bound to the GPU's NUMA node (numa.h), so the
+        // block file's pages are read into memory next to the GPU that DMAs them
+        bool ok = true;
+        std::thread([&] {
+            (void)hipSetDevice(device);
+            bind_thread_to_device(device);
+            for (Window &w : r->slot) {
+                PacketArena &a = w.a;
+                if (hipHostMalloc(reinterpret_cast<void **>(&a.h), r->cap_data + crc_bytes, pinned_host_flags()) !=
+                        hipSuccess ||
+                    hipMalloc(reinterpret_cast<void **>(&a.d), r->cap_data + crc_bytes) != hipSuccess ||
+                    hipMalloc(reinterpret_cast<void **>(&a.d_res), sizeof(unsigned long long)) != hipSuccess ||
+                    hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long),
+                                  pinned_host_flags()) != hipSuccess ||
+                    hipEventCreateWithFlags(&a.done, hipEventDisableTiming) != hipSuccess) {
+                    ok = false;
+                    return;
+                }
+                a.cap = r->cap_data + crc_bytes;
+            }
+        }).join();
+        if (!ok) return bail(fail(-ENOMEM, "LocalBlockReader: window allocation failed"));
     }
     if (int rc = hdfs3_crc_ctx_set_checksum_type(r->ctx, r->engine_type())) return bail(rc);
     for (int i = 0; i < kSlots; ++i) r->free_slots.push_back(i);

@@ -65,15 +65,22 @@ class CopyPool {
         std::atomic<int> *pending = nullptr;
         std::atomic<int> *err = nullptr;
     };
-    static void run(const Job &j) {
+    void run(const Job &j) {
         if (j.src) {
             std::memcpy(j.dst, j.src, j.n);
         } else if (int rc = pread_fully(j.fd, j.dst, j.n, j.off)) {
             j.err->store(rc, std::memory_order_relaxed);
         }
-        j.pending->fetch_sub(1, std::memory_order_release);
+        // the last piece of a split wakes its waiter (after this, the split's counters may be gone:
+        // only pool members are touched)
+        if (j.pending->fetch_sub(1, std::memory_order_acq_rel) == 1) {
+            std::lock_guard<std::mutex> lk(done_mu_);
+            done_cv_.notify_all();
+        }
     }
-    // help with pieces no helper has taken yet, then wait for the rest
+    // help with pieces no helper has taken yet, then wait for the rest: a short spin (the pieces
+    // are equal, so they usually finish together), then block on the pool's completion variable
+    // instead of burning a core per waiting caller
     void help_and_wait(std::atomic<int> &pending) {
         for (;;) {
             Job j;
@@ -85,7 +92,10 @@ class CopyPool {
             }
             run(j);
         }
-        while (pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+        for (int i = 0; i < 64 && pending.load(std::memory_order_acquire) != 0; ++i) std::this_thread::yield();
+        if (pending.load(std::memory_order_acquire) == 0) return;
+        std::unique_lock<std::mutex> lk(done_mu_);
+        done_cv_.wait(lk, [&] { return pending.load(std::memory_order_acquire) == 0; });
     }
     int split(uint8_t *dst, const uint8_t *src, int fd, int64_t foff, size_t n) {
         std::atomic<int> pending{0}, err{0};
@@ -131,6 +141,8 @@ class CopyPool {
     std::mutex mu_;
     std::condition_variable cv_;
     std::deque<Job> jobs_;
+    std::mutex done_mu_;
+    std::condition_variable done_cv_;
 };
 
 }  // namespace hdfs3crc

@@ -14,6 +14,7 @@
 #include <cstddef>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 #include <mutex>
@@ -23,6 +24,7 @@
 #include "crc32c_kernels.h"
 #include "crc32c_tables.h"
 #include "ctx.h"
+#include "numa.h"
 
 namespace hdfs3crc {
 uint32_t host_update(uint32_t state, const void *p, size_t n);
@@ -110,7 +112,7 @@ int grow_slot(Slot &s, size_t data_bytes, size_t crc_bytes) {
         if (s.d_data) (void)hipFree(s.d_data);
         s.h_data = s.d_data = nullptr;
         s.data_cap = 0;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_data), data_bytes, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_data), data_bytes, pinned_host_flags()));
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d_data), data_bytes));
         s.data_cap = data_bytes;
     }
@@ -119,7 +121,7 @@ int grow_slot(Slot &s, size_t data_bytes, size_t crc_bytes) {
         if (s.d_crc) (void)hipFree(s.d_crc);
         s.h_crc = s.d_crc = nullptr;
         s.crc_cap = 0;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_crc), crc_bytes, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_crc), crc_bytes, pinned_host_flags()));
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d_crc), crc_bytes));
         s.crc_cap = crc_bytes;
     }
@@ -530,6 +532,74 @@ std::vector<hdfs3_crc_ctx *> g_ctx_pool;
 constexpr size_t kCtxPoolMax = 32;
 constexpr size_t kArenaCacheKeep = 6;  // arenas any pooled ctx keeps (block_reader.cpp kArenaCacheMax)
 constexpr size_t kDeepCtxMax = 8;      // pooled contexts allowed to keep a read-ahead ring's worth
+constexpr uint64_t kPoolPinnedDefault = uint64_t(512) << 20;
+
+// HDFS3_POOL_PINNED_MAX: bytes, or with a K/M/G suffix
+uint64_t pool_pinned_cap() {
+    static const uint64_t cap = [] {
+        const char *e = std::getenv("HDFS3_POOL_PINNED_MAX");
+        if (!e || !*e) return kPoolPinnedDefault;
+        char *end = nullptr;
+        const unsigned long long v = std::strtoull(e, &end, 10);
+        if (end == e) return kPoolPinnedDefault;
+        const int shift = *end == 'K' || *end == 'k' ? 10 : *end == 'M' || *end == 'm' ? 20
+                          : *end == 'G' || *end == 'g' ? 30 : 0;
+        return uint64_t(v) << shift;
+    }();
+    return cap;
+}
+
+struct Footprint {
+    uint64_t pinned = 0, device = 0;
+};
+
+// what a ctx holds beyond its tables: pinned host and device bytes of its staging slots, cached
+// arenas, descriptor stagings, word scratch and result word
+Footprint footprint(hdfs3_crc_ctx *ctx) {
+    Footprint f;
+    for (const Slot &s : ctx->slot) {
+        f.pinned += s.data_cap + s.crc_cap;
+        f.device += s.data_cap + s.crc_cap;
+    }
+    {
+        std::lock_guard<std::mutex> lk(ctx->arena_mu);
+        for (const PacketArena &a : ctx->arena_cache) {
+            const uint64_t desc = a.desc_cap * sizeof(DevSegment) + (a.h_res ? sizeof(unsigned long long) : 0);
+            f.pinned += a.cap + desc;
+            f.device += a.cap + desc;
+        }
+    }
+    for (const auto &st : ctx->seg_ring) {
+        f.pinned += st.cap * sizeof(DevSegment);
+        f.device += st.cap * sizeof(DevSegment);
+    }
+    f.pinned += sizeof(unsigned long long);
+    f.device += ctx->words.cap + sizeof(unsigned long long);
+    for (int p = 0; p < 2; ++p) f.device += sizeof(host_images()[p].t) + sizeof(host_images()[p].fold);
+    return f;
+}
+
+// give back what a pooled ctx can rebuild on demand: cached arenas beyond `keep`, then the
+// staging slots of the host API
+void shed(hdfs3_crc_ctx *ctx, size_t keep_arenas, bool slots) {
+    DeviceGuard g(ctx->device);
+    {
+        std::lock_guard<std::mutex> alk(ctx->arena_mu);
+        while (ctx->arena_cache.size() > keep_arenas) {
+            ctx->arena_cache.back().release();
+            ctx->arena_cache.pop_back();
+        }
+    }
+    if (!slots) return;
+    for (Slot &s : ctx->slot) {
+        if (s.h_data) (void)hipHostFree(s.h_data);
+        if (s.h_crc) (void)hipHostFree(s.h_crc);
+        if (s.d_data) (void)hipFree(s.d_data);
+        if (s.d_crc) (void)hipFree(s.d_crc);
+        s.h_data = s.h_crc = s.d_data = s.d_crc = nullptr;
+        s.data_cap = s.crc_cap = 0;
+    }
+}
 }  // namespace
 
 int ctx_acquire(int device, hdfs3_crc_ctx **out, bool deep) {
@@ -574,19 +644,21 @@ void ctx_release(hdfs3_crc_ctx *ctx) {
         if (g_ctx_pool.size() < kCtxPoolMax) {
             // a read-ahead reader's deep ring leaves up to a block's worth of pinned arenas in
             // its ctx (block_reader.cpp); at most kDeepCtxMax pooled contexts keep that much,
-            // the others go back to the usual few arenas, so the pool's pinned memory is bounded
+            // the others go back to the usual few arenas
             size_t deep = 0;
             for (hdfs3_crc_ctx *c : g_ctx_pool) deep += c->arena_cache.size() > kArenaCacheKeep;
-            if (deep >= kDeepCtxMax && ctx->arena_cache.size() > kArenaCacheKeep) {
-                DeviceGuard g(ctx->device);
-                std::lock_guard<std::mutex> alk(ctx->arena_mu);
-                while (ctx->arena_cache.size() > kArenaCacheKeep) {
-                    ctx->arena_cache.back().release();
-                    ctx->arena_cache.pop_back();
-                }
+            if (deep >= kDeepCtxMax && ctx->arena_cache.size() > kArenaCacheKeep) shed(ctx, kArenaCacheKeep, false);
+            // and the pool as a whole retains at most pool_pinned_cap() pinned bytes: this ctx sheds
+            // arenas, then its staging, and is destroyed if it still does not fit
+            const uint64_t cap = pool_pinned_cap();
+            uint64_t others = 0;
+            for (hdfs3_crc_ctx *c : g_ctx_pool) others += footprint(c).pinned;
+            if (others + footprint(ctx).pinned > cap) shed(ctx, 0, false);
+            if (others + footprint(ctx).pinned > cap) shed(ctx, 0, true);
+            if (others + footprint(ctx).pinned <= cap) {
+                g_ctx_pool.push_back(ctx);
+                return;
             }
-            g_ctx_pool.push_back(ctx);
-            return;
         }
     }
     hdfs3_crc_ctx_destroy(ctx);
@@ -598,6 +670,31 @@ extern "C" {
 
 int hdfs3_crc_ctx_acquire(int device, hdfs3_crc_ctx **out) { return hdfs3crc::ctx_acquire(device, out); }
 void hdfs3_crc_ctx_release(hdfs3_crc_ctx *ctx) { hdfs3crc::ctx_release(ctx); }
+
+int hdfs3_crc_pool_stats_get(hdfs3_crc_pool_stats *out) {
+    if (!out) return fail(-EINVAL, "null out");
+    hdfs3_crc_pool_stats st{};
+    std::lock_guard<std::mutex> lk(hdfs3crc::g_ctx_pool_mu);
+    for (hdfs3_crc_ctx *c : hdfs3crc::g_ctx_pool) {
+        const hdfs3crc::Footprint f = hdfs3crc::footprint(c);
+        st.pinned_bytes += f.pinned;
+        st.device_bytes += f.device;
+    }
+    st.pooled_contexts = hdfs3crc::g_ctx_pool.size();
+    st.pinned_cap_bytes = hdfs3crc::pool_pinned_cap();
+    *out = st;
+    return 0;
+}
+
+int hdfs3_crc_pool_trim(void) {
+    std::vector<hdfs3_crc_ctx *> idle;
+    {
+        std::lock_guard<std::mutex> lk(hdfs3crc::g_ctx_pool_mu);
+        idle.swap(hdfs3crc::g_ctx_pool);
+    }
+    for (hdfs3_crc_ctx *c : idle) hdfs3_crc_ctx_destroy(c);
+    return int(idle.size());
+}
 
 int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream) {
     if (!ctx) return fail(-EINVAL, "null ctx");

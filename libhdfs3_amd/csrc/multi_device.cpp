@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "numa.h"
 
 using hdfs3crc::fail;
 
@@ -45,6 +46,7 @@ struct Worker {
 
     void run() {
         (void)hipSetDevice(device);
+        hdfs3crc::bind_thread_to_device(device);  // its staging and copies on the GPU's own node
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
             cv.wait(lk, [&] { return has_job || quit; });
@@ -82,7 +84,7 @@ struct Worker {
         d_res = h_res = nullptr;
         res_cap = 0;
         if (hipMalloc(reinterpret_cast<void **>(&d_res), n * 8) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void **>(&h_res), n * 8, hipHostMallocDefault) != hipSuccess)
+            hipHostMalloc(reinterpret_cast<void **>(&h_res), n * 8, hdfs3crc::pinned_host_flags()) != hipSuccess)
             return fail(-ENOMEM, "device %d: result array for %zu blocks", device, n);
         res_cap = n;
         return 0;

@@ -453,8 +453,10 @@ class InputStream:
     in file order."""
 
     def __init__(self, blocks, *, device: int = 0, verify: bool = True, batch_packets: int = 64,
-                 timeout_ms: int = 60000, pool_id: bytes = b"BP-loopback", generation_stamp: int = 1):
-        self._lib = _native.lib()
+                 timeout_ms: int = 60000, pool_id: bytes = b"BP-loopback", generation_stamp: int = 1, lib=None):
+        """lib: the library to run on (default the product library; tests pass _native.lab() to
+        reach its fault-injection hooks)."""
+        self._lib = lib or _native.lib()
         arr, self._keep = _located_blocks(blocks, pool_id, generation_stamp)
         opts = _native.ReaderOpts(device, int(verify), batch_packets, timeout_ms)
         p = c_void_p()
@@ -500,10 +502,11 @@ class InputStream:
 
     def stats(self):
         from ctypes import c_uint64
-        f, o, a = c_uint64(), c_uint64(), c_uint64()
+        f, o, a, lf = c_uint64(), c_uint64(), c_uint64(), c_uint64()
         check("hdfs3_input_stats", self._lib.hdfs3_input_stats(self.s, byref(f), byref(o)))
-        check("hdfs3_input_readahead_stats", self._lib.hdfs3_input_readahead_stats(self.s, byref(a)))
-        return {"failovers": f.value, "readers_opened": o.value, "prefetch_readers_opened": a.value}
+        check("hdfs3_input_readahead_stats", self._lib.hdfs3_input_readahead_stats(self.s, byref(a), byref(lf)))
+        return {"failovers": f.value, "readers_opened": o.value, "prefetch_readers_opened": a.value,
+                "prefetch_local_faults": lf.value}
 
     def set_readahead(self, blocks: int, max_bytes_per_block: int = 0) -> None:
         """hdfs3_input_set_readahead: blocks i+1 .. i+blocks read by background threads while

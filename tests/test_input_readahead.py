@@ -228,3 +228,58 @@ def test_random_walk_of_reads_seeks_and_preads(cluster, ahead):
                 got = s.pread_into(p, buf)
                 assert got == min(n, whole.nbytes - p) and np.array_equal(buf[:got], whole[p:p + got])
             assert s.tell() == pos
+
+
+def test_local_fault_in_a_prefetched_reader_is_read_on_demand(cluster):
+    """A read-ahead reader whose pinned arena cannot be allocated (a local fault, injected through
+    the measurement library's hook) is dropped and its block read again on demand on the stream's
+    own context: the same bytes as with read-ahead off, no replica failed over, and the fault only
+    counted (turning read-ahead on must not make a read fail)."""
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import InputStream
+
+    a, b, blocks, whole = cluster
+    lab = _native.lab()
+    try:
+        lab.hdfs3x_fail_prefetch_arenas(3)
+        with InputStream([(bid, n, [("127.0.0.1", a.port)]) for bid, n in blocks], lib=lab) as s:
+            s.set_readahead(2)
+            got, _ = _read_all(s, whole.nbytes)
+            st = s.stats()
+        assert np.array_equal(got, whole)
+        assert st["failovers"] == 0 and st["prefetch_local_faults"] >= 1
+    finally:
+        lab.hdfs3x_fail_prefetch_arenas(0)
+
+
+def test_readahead_depth_is_bounded(cluster):
+    from libhdfs3_amd._native import Hdfs3CrcError
+
+    a, b, blocks, whole = cluster
+    with _stream(blocks, [("127.0.0.1", a.port)]) as s:
+        s.set_readahead(8)
+        with pytest.raises(Hdfs3CrcError):
+            s.set_readahead(9)
+
+
+def test_pool_pinned_memory_stays_under_the_cap(cluster):
+    """Streams with deep read-ahead rings opened and closed over many blocks leave at most the
+    pool's pinned cap retained (hdfs3_crc_pool_stats_get), and hdfs3_crc_pool_trim empties it."""
+    import ctypes
+
+    from libhdfs3_amd import _native
+
+    a, b, blocks, whole = cluster
+    lib = _native.lib()
+    st = _native.PoolStats()
+    for rep in range(3):
+        for ahead in (2, 5):
+            with _stream(blocks, [("127.0.0.1", a.port)], ahead) as s:
+                got, _ = _read_all(s, whole.nbytes)
+                assert np.array_equal(got, whole)
+            assert lib.hdfs3_crc_pool_stats_get(ctypes.byref(st)) == 0
+            assert st.pinned_bytes <= st.pinned_cap_bytes, (st.pinned_bytes, st.pinned_cap_bytes)
+    assert st.pinned_cap_bytes == 512 << 20 and st.pooled_contexts > 0
+    assert lib.hdfs3_crc_pool_trim() == st.pooled_contexts
+    assert lib.hdfs3_crc_pool_stats_get(ctypes.byref(st)) == 0
+    assert st.pooled_contexts == 0 and st.pinned_bytes == 0

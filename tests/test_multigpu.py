@@ -54,6 +54,9 @@ def test_bench_gpus_2_real_run_on_one_gpu():
     j = _bench("--gpus", "2", "--steps", "20", "--warmup", "5", "--blocks", "2", "--block-mib", "16",
                "--no-cpu-baseline", "--no-pmc", timeout=240)
     assert j["n_gpus"] == 2 and len(j["per_rank"]) == 2
+    # the line proves its world: the process group's own size and backend, each rank's device
+    assert j["world_size"] == 2 and j["backend"] == "gloo"
+    assert [r["current_device"] for r in j["per_rank"]] == [0, 0]  # one GPU here: both on cuda:0
     a, b = j["per_rank"]
     assert a["seed"] != b["seed"] and a["value"] > 0 and b["value"] > 0
     slowest = max(a["ms_per_step"], b["ms_per_step"])
@@ -122,5 +125,46 @@ def test_multi_device_api_matches_oracle(gpu_ctx, workers):
         # a host pointer where device memory is required: -EINVAL, nothing launched
         arr[2] = DevBlock(datas[2].ctypes.data, keep[5].ptr, datas[2].nbytes)
         assert lib.hdfs3_crc32c_verify_blocks_multi(m, arr, len(sizes), 512, 1, bad) == -22
+    finally:
+        lib.hdfs3_multi_destroy(m)
+
+
+@pytest.mark.gpu
+def test_config4_sharding_at_size_on_one_gpu():
+    """BASELINE.json configs[3] rehearsed on one device: 8 independent 128 MiB blocks through
+    hdfs3_crc32c_{compute,verify}_blocks_multi with 8 workers (device 0 listed 8 times: 8 contexts,
+    streams and host threads, block b -> worker b % 8, no collective). Every CRC word of every block
+    against the oracle, then one flipped bit per worker's block reported at its chunk and nowhere
+    else. The unit sharded is the reference's serial per-block verify
+    (InputStreamImpl.cpp:616-708, RemoteBlockReader.cpp:306-326)."""
+    import ctypes
+
+    import torch
+
+    from libhdfs3_amd import _native
+    from libhdfs3_amd._native import DevBlock
+
+    nb, bs, bpc = 8, 128 << 20, 512
+    lib, m = _multi([0] * nb)
+    try:
+        g = torch.Generator(device="cuda:0")
+        g.manual_seed(4242)
+        data = torch.randint(0, 256, (nb, bs), dtype=torch.uint8, device="cuda:0", generator=g)
+        words = torch.zeros((nb, 4 * (bs // bpc)), dtype=torch.uint8, device="cuda:0")
+        arr = (DevBlock * nb)(*[DevBlock(data[b].data_ptr(), words[b].data_ptr(), bs) for b in range(nb)])
+        _native.check("compute_multi", lib.hdfs3_crc32c_compute_blocks_multi(m, arr, nb, bpc))
+        torch.cuda.synchronize()
+        for b in range(nb):
+            want = oracle_compute(data[b].cpu().numpy(), bpc)
+            assert np.array_equal(words[b].cpu().numpy(), want), b
+        bad = (ctypes.c_int64 * nb)()
+        _native.check("verify_multi", lib.hdfs3_crc32c_verify_blocks_multi(m, arr, nb, bpc, 0, bad))
+        assert list(bad) == [-1] * nb
+        flips = [(b, (b * 37_123 + 11) % (bs // bpc)) for b in range(nb)]  # one chunk per worker's block
+        for b, k in flips:
+            data[b, k * bpc + (b * 13) % bpc] ^= 1 << (b % 8)
+        torch.cuda.synchronize()
+        _native.check("verify_multi", lib.hdfs3_crc32c_verify_blocks_multi(m, arr, nb, bpc, 0, bad))
+        assert list(bad) == [k for _, k in flips]
     finally:
         lib.hdfs3_multi_destroy(m)
