@@ -186,13 +186,22 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
         return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
     }
     case 92:  // the round-3 kernel with its prefetch issued at the start of each step (early)
-        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, false>(a, tab, fold, grid_cap, s);
+        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, 0>(a, tab, fold, grid_cap, s);
         return hipErrorInvalidValue;
-    case 93:  // the round-3 kernel, solo last step when overlapped (as the round-2 production)
-        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, true, true>(a, tab, fold, grid_cap, s);
+    case 93:  // the round-3 kernel, late prefetch, no solo last step
+        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, 1, false>(a, tab, fold, grid_cap, s);
         return hipErrorInvalidValue;
     case 94:  // 92 + solo last step when overlapped
-        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, false, true>(a, tab, fold, grid_cap, s);
+        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, 0, V>(a, tab, fold, grid_cap, s);
+        return hipErrorInvalidValue;
+    case 97:  // late prefetch in the first step of each pair, early in the second (+ solo)
+        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, 3, V>(a, tab, fold, grid_cap, s);
+        return hipErrorInvalidValue;
+    case 98:  // early in the first step of each pair, late in the second (+ solo)
+        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, 4, V>(a, tab, fold, grid_cap, s);
+        return hipErrorInvalidValue;
+    case 96:  // production with the prefetch held until every load of the wave landed (LATE 2)
+        if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, 2, V>(a, tab, fold, grid_cap, s);
         return hipErrorInvalidValue;
     case 34: {  // 24 (no table math) with timestamps
         if (!g_trace) return hipErrorInvalidValue;

@@ -22,7 +22,9 @@ hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
 #if HDFS3_LAB
     if (g_variant != 0) return launch_experiment(g_variant, a, V, tab, fold, grid_cap, s);
 #endif
-    if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false>(a, tab, fold, grid_cap, s);
+    // late prefetch; overlapped verifies end with the solo last step (for compute it costs 40 %:
+    // profiles/r03/ab_cmp_ovl.jsonl)
+    if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, 1, V>(a, tab, fold, grid_cap, s);
     return launch_wave<BPC, V, 2, true>(a, tab, fold, grid_cap, s);
 }
 
@@ -270,6 +272,10 @@ hipError_t launch_seg_k(const SegLaunch &L, bool verify, const uint32_t *tab, co
 template <int BPC>
 hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *fold, int grid,
                         hipStream_t s) {
+    // production: the round kernel's core over a segment walk (crc32c_wave.h); lab variant 95 (and
+    // the diagnostic 49) keep the round-2 segmented kernel for A/B
+    if (g_variant != 95 && g_variant != 49 && g_variant != 50)
+        return verify ? launch_segments3<BPC, true>(L, tab, fold, grid, s) : launch_segments3<BPC, false>(L, tab, fold, grid, s);
     constexpr int set = BPC == 512 ? 0 : BPC == 1024 ? 1 : BPC == 2048 ? 2 : 3;
     const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
     if (g_variant == 49 && L.nseg == 1) return launch_seg_k<BPC, true, true>(L, verify, tab, nib, grid, s);

@@ -44,8 +44,11 @@ struct WView {
 };
 
 // Rounds of one contiguous block: the wave's rounds are units wave, wave + W, ... (W = waves).
+// kLaneView: view() also takes a lane-varying round index (the held compute stores find their
+// words' addresses at flush time); a walk without it holds each word's address instead.
 template <int CPU>
 struct BlockWalk {
+    static constexpr bool kLaneView = true;
     const uint8_t *data;
     uint8_t *words;
     uint64_t key0, first, stride;
@@ -64,6 +67,7 @@ struct BlockWalk {
 // pitch). Keys are (packet << 32) | chunk.
 template <int CPU>
 struct PitchWalk {
+    static constexpr bool kLaneView = true;
     const uint8_t *data;
     uint8_t *words;
     uint64_t dpitch, wpitch, first, stride;
@@ -78,12 +82,69 @@ struct PitchWalk {
     }
 };
 
+// The union of a list of independent segments' whole rounds (SegLaunch, crc32c_device.h): global
+// unit u belongs to the segment with the largest unit_begin <= u, found as u / uniform when the host
+// found equal segments (UNI), else by a wave-uniform binary search over the descriptors. The prefetch
+// stream's current segment is cached in scalar registers, so a round inside it costs arithmetic only
+// and crossing into another one a lookup and its scalar descriptor loads. Views are asked for in
+// increasing round order (the core resolves the next step's views at the end of each step).
+template <int CPU, bool UNI>
+struct SegWalk {
+    static constexpr bool kLaneView = false;
+    const SegLaunch *L;
+    uint64_t first, stride;
+    uint32_t K;
+    const uint8_t *dummy;
+    uint64_t c_begin = 1, c_end = 0, c_key = 0;
+    const uint8_t *c_data = nullptr;
+    uint8_t *c_crc = nullptr;
+
+    __device__ __forceinline__ const DevSegment *segp(uint32_t i) const { return L->seg ? L->seg + i : L->inl + i; }
+    __device__ __forceinline__ uint32_t seg_of(uint64_t u) const {
+        if constexpr (UNI) {  // unit counts stay < 2^32 (16 TiB per launch): 32-bit divide
+            const uint32_t si = uint32_t(u) / uint32_t(L->uniform);
+            return si < L->nseg ? si : L->nseg - 1;
+        } else {
+            uint32_t lo = 0, hi = L->nseg - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (rfl64(segp(mid)->unit_begin) <= u) lo = mid;
+                else hi = mid - 1;
+            }
+            return lo;
+        }
+    }
+    __device__ __forceinline__ WView view(uint32_t k) {
+        if (k >= K) return WView{dummy, const_cast<uint8_t *>(dummy), 0};
+        const uint64_t u = first + uint64_t(k) * stride;
+        if (u < c_begin || u >= c_end) {
+            const uint32_t si = seg_of(u);
+            if (L->stride) {  // packets at one pitch: kernel-argument arithmetic, no descriptor loads
+                c_begin = uint64_t(si) * L->uniform;
+                c_end = c_begin + (si + 1 < L->nseg ? L->uniform : L->inl[1].len / kRoundBytes);
+                c_data = L->inl[0].data + uint64_t(si) * L->stride;
+                c_crc = L->inl[0].crc + uint64_t(si) * L->stride;
+                c_key = uint64_t(si) << 32;
+            } else {
+                const DevSegment *sd = segp(si);
+                c_begin = rfl64(sd->unit_begin);
+                c_end = c_begin + rfl64(sd->len) / kRoundBytes;
+                c_data = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->data)));
+                c_crc = reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->crc)));
+                c_key = rfl64(sd->key_base);
+            }
+        }
+        const uint64_t r = u - c_begin;
+        return WView{c_data + r * kRoundBytes, c_crc + 4 * CPU * r, c_key + CPU * r};
+    }
+};
+
 // The core: prologue, steps, last step. VERIFY: compare with the stored words and fold the first bad
 // key into *result; else store the words. SOLO: the last step runs its two rounds as single chains one
 // after the other (overlapped launches: the first chain overlaps the second round's arrival and only
 // one round's lookups remain once the wave's last data landed). HOLD (compute, bpc 512): the words of
 // 8 rounds are transposed into one VGPR and up to 8 such VGPRs are stored in one burst.
-template <int BPC, bool VERIFY, bool SOLO, bool HOLD, bool LATE, class Walk>
+template <int BPC, bool VERIFY, bool SOLO, bool HOLD, int LATE, class Walk>
 __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uint32_t *__restrict__ g_tab,
                                             const uint32_t *__restrict__ g_nib, unsigned long long *result) {
     constexpr int G = BPC / 64;
@@ -146,19 +207,27 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         return 0;
     };
     constexpr bool kHold = HOLD && !VERIFY && G == 8;
+    constexpr bool kAddr = !Walk::kLaneView;
     // kHold: lane 8r + c collects chunk c of round r of the current octet (8 rounds) in `line`; up to
     // 8 closed octets wait in hold[] (hold[i] = octet hold_base + nheld - 1 - i) and go out in one
-    // burst. Their addresses come from the walk at flush time (lane-varying round index), so holding
-    // costs one VGPR per octet.
+    // burst. With a lane view their addresses come from the walk at flush time (one VGPR per held
+    // octet); otherwise each lane keeps its word's address beside it (a segment walk's rounds may
+    // belong to different segments).
     uint32_t line = 0;
     uint32_t hold[kHold ? 8 : 1];
+    gu32 *laddr = nullptr;
+    gu32 *hold_addr[kHold && kAddr ? 8 : 1];
     uint32_t nheld = 0, hold_base = 0;
     auto flush = [&]() {
 #pragma unroll
         for (int i = 0; i < (kHold ? 8 : 0); ++i) {
             if (uint32_t(i) < nheld) {
-                const uint32_t kk = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
-                if (kk < K) *(gu32 *)((gu8 *)walk.view(kk).w + 4 * (lane & 7)) = __builtin_bswap32(hold[i]);
+                if constexpr (kAddr) {
+                    if (hold_addr[i]) *hold_addr[i] = __builtin_bswap32(hold[i]);
+                } else {
+                    const uint32_t kk = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
+                    if (kk < K) *(gu32 *)((gu8 *)walk.view(kk).w + 4 * (lane & 7)) = __builtin_bswap32(hold[i]);
+                }
             }
         }
         hold_base += nheld;
@@ -171,11 +240,20 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             const uint32_t r = k & 7;
             // group c's lanes all hold chunk c's state (group_xor is a butterfly)
             const uint32_t got = uint32_t(__builtin_amdgcn_ds_bpermute(int(32 * (lane & 7)), int(y)));
-            line = (lane >> 3) == r ? got : line;
+            const bool mine = (lane >> 3) == r;
+            line = mine ? got : line;
+            if constexpr (kAddr) laddr = mine ? (gu32 *)((gu8 *)v.w + 4 * (lane & 7)) : laddr;
             if (r == 7 || k + 1 == K) {
 #pragma unroll
-                for (int i = (kHold ? 7 : 0); i > 0; --i) hold[i] = hold[i - 1];
+                for (int i = (kHold ? 7 : 0); i > 0; --i) {
+                    hold[i] = hold[i - 1];
+                    if constexpr (kAddr) hold_addr[i] = hold_addr[i - 1];
+                }
                 hold[0] = line;
+                if constexpr (kAddr) {
+                    hold_addr[0] = laddr;
+                    laddr = nullptr;
+                }
                 if (++nheld == 8) flush();
             }
             return;
@@ -224,9 +302,13 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // the wave's last round: the cache-resident table image), then the chains over c0, c1. The next
     // views are resolved at the end. `fin` (wave-uniform) marks the wave's last step: with SOLO its
     // rounds run as single chains one after the other.
-    auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k, bool fin) {
+    // LATE (lab A/B): 0 early, 1 late, 2 late after every load, 3 late in the first step of each
+    // pair and early in the second, 4 the reverse. `pair_b` = the second step of a pair.
+    auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k, bool fin, auto pair_b) {
+        constexpr bool kLate = LATE == 1 || LATE == 2 || (LATE == 3 && !decltype(pair_b)::value) ||
+                               (LATE == 4 && decltype(pair_b)::value);
         const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
-        if (!LATE) {
+        if (!kLate) {
             load_round_buf<true>(p0, pv0.p, lane_off);
             load_round_buf<true>(p1, pv1.p, lane_off);
         }
@@ -239,12 +321,13 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         } else {
             regroup(c0);
             regroup(c1);
-            if constexpr (LATE) {
+            if constexpr (kLate) {
                 // the prefetch goes out once this step's rounds have landed: at most 8 KiB in
                 // flight per wave (128 KiB per CU), not 16 (more requests in flight lower the
                 // DRAM efficiency; the round-2 kernel got this by accident from
-                // register-reuse waits at its loop head)
+                // register-reuse waits at its loop head). LATE 2 (lab): also after the words.
                 __builtin_amdgcn_sched_barrier(0);
+                if constexpr (LATE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 load_round_buf<true>(p0, pv0.p, lane_off);
                 load_round_buf<true>(p1, pv1.p, lane_off);
                 __builtin_amdgcn_sched_barrier(0);
@@ -265,9 +348,9 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // the loop made the register allocator copy the rounds: 32 v_mov per step in round 2).
     const uint32_t nr = (K + 1) & ~1u;  // rounds rounded up to whole steps
     for (uint32_t k = 0; k < nr; k += 4) {
-        step(a0, a1, b0, b1, k, k + 2 >= nr);
+        step(a0, a1, b0, b1, k, k + 2 >= nr, std::false_type{});
         if (k + 2 >= nr) break;
-        step(b0, b1, a0, a1, k + 2, k + 4 >= nr);
+        step(b0, b1, a0, a1, k + 2, k + 4 >= nr, std::true_type{});
     }
     if constexpr (kHold) flush();
 }
@@ -298,7 +381,7 @@ __device__ __forceinline__ void slow_region(const uint32_t *lds, const uint8_t *
 }
 
 // One block (PITCH = false) or a constant-pitch stream (PITCH = true, ChunkLaunch::pitch/npk/...).
-template <int BPC, bool VERIFY, bool PITCH, bool SOLO, bool LATE = true>
+template <int BPC, bool VERIFY, bool PITCH, bool SOLO, int LATE = 1>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 512 == 0, "one-round units");
@@ -328,12 +411,58 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     }
 }
 
+// A list of segments (blocks of a batch, packets of a descriptor list): the core over a SegWalk,
+// then every segment's leftover chunks and short tail, one chunk per thread spread over the
+// workgroups (item i -> segment i / chunks-per-round, block i % grid).
+template <int BPC, bool VERIFY, bool UNI>
+__global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunch L, const uint32_t *__restrict__ g_tab,
+                                                                        const uint32_t *__restrict__ g_nib) {
+    static_assert(BPC <= kRoundBytes && BPC % 512 == 0, "one-round units");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytesWave / 4];
+    constexpr int kCpu = kRoundBytes / BPC;
+    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
+    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    SegWalk<kCpu, UNI> w{&L, wave, nwaves,
+                         uint32_t(rfl64(wave < L.units ? (L.units - wave + nwaves - 1) / nwaves : 0)),
+                         reinterpret_cast<const uint8_t *>(g_tab)};
+    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, true>(w, lds, g_tab, g_nib, L.result);
+
+    const Lut t(lds);
+    const uint64_t items = uint64_t(L.nseg) * kCpu;
+    for (uint64_t it = uint64_t(threadIdx.x) * gridDim.x + blockIdx.x; it < items;
+         it += uint64_t(gridDim.x) * kBlockThreads) {
+        const uint32_t si = uint32_t(it / kCpu);
+        DevSegment sd;
+        if (L.stride) {
+            sd = L.inl[0];
+            sd.data += uint64_t(si) * L.stride;
+            sd.crc += uint64_t(si) * L.stride;
+            sd.len = si + 1 < L.nseg ? L.inl[0].len : L.inl[1].len;
+            sd.key_base = uint64_t(si) << 32;
+        } else {
+            sd = *w.segp(si);
+        }
+        const uint64_t nfull = sd.len / BPC;
+        const uint64_t c = (sd.len / kRoundBytes) * kCpu + it % kCpu;
+        if (c < nfull + (sd.len % BPC ? 1 : 0)) {
+            const uint32_t sz = c < nfull ? uint32_t(BPC) : uint32_t(sd.len % BPC);
+            const uint32_t v = ~crc_run_lines(t, 0xFFFFFFFFu, sd.data + c * BPC, sz);
+            if constexpr (VERIFY) {
+                if ((sz == uint32_t(BPC) || L.check_short_tail) && load_be32(sd.crc + 4 * c, true) != v)
+                    atomicMax(L.result, ~(unsigned long long)(sd.key_base + c));
+            } else {
+                store_be32(sd.crc + 4 * c, v, true);
+            }
+        }
+    }
+}
+
 // Overlapped verifies up to 256 MiB per launch end with the solo last step (21.94 -> 21.34 us per
 // 128 MiB launch at bpc 512 in round 2; 1 % slower at 1 GiB per launch, +0.9 us barriered:
 // profiles/r02_kernel_study/r02_ab_solo_*.jsonl).
 constexpr uint64_t kSoloTailMaxBytes = uint64_t(256) << 20;
 
-template <int BPC, bool V, bool PITCH, bool LATE = true, bool SOLO = false>
+template <int BPC, bool V, bool PITCH, int LATE = 1, bool SOLO = false>
 hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
     constexpr int G = BPC / 64;
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
@@ -343,7 +472,7 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
     if (grid < 1) grid = 1;
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
-        if constexpr (SOLO && V && !PITCH) {
+        if constexpr (SOLO && !PITCH) {
             if (units * kRoundBytes <= kSoloTailMaxBytes) {
                 hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LATE>), dim3(grid), dim3(kBlockThreads),
                                       0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
@@ -356,6 +485,18 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
         hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LATE>), dim3(grid), dim3(kBlockThreads), 0, s, a,
                            tab, nib);
     }
+    return hipGetLastError();
+}
+
+template <int BPC, bool V>
+hipError_t launch_segments3(const SegLaunch &L, const uint32_t *tab, const uint32_t *fold, int grid, hipStream_t s) {
+    constexpr int G = BPC / 64;
+    constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
+    const uint32_t *nib = fold + kFoldAffineOff + set * kFoldNibbleWords;
+    if (L.uniform)
+        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, true>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
+    else
+        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, false>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
     return hipGetLastError();
 }
 

@@ -130,7 +130,7 @@ def test_multi_device_api_matches_oracle(gpu_ctx, workers):
 
 
 @pytest.mark.gpu
-def test_config4_sharding_at_size_on_one_gpu():
+def test_config4_sharding_at_size_on_one_gpu(gpu_ctx):
     """BASELINE.json configs[3] rehearsed on one device: 8 independent 128 MiB blocks through
     hdfs3_crc32c_{compute,verify}_blocks_multi with 8 workers (device 0 listed 8 times: 8 contexts,
     streams and host threads, block b -> worker b % 8, no collective). Every CRC word of every block
@@ -139,31 +139,33 @@ def test_config4_sharding_at_size_on_one_gpu():
     (InputStreamImpl.cpp:616-708, RemoteBlockReader.cpp:306-326)."""
     import ctypes
 
-    import torch
-
     from libhdfs3_amd import _native
     from libhdfs3_amd._native import DevBlock
+    from libhdfs3_amd.engine import DeviceBuffer
 
     nb, bs, bpc = 8, 128 << 20, 512
+    base = splitmix_bytes(bs, 4242)
     lib, m = _multi([0] * nb)
+    keep = []
     try:
-        g = torch.Generator(device="cuda:0")
-        g.manual_seed(4242)
-        data = torch.randint(0, 256, (nb, bs), dtype=torch.uint8, device="cuda:0", generator=g)
-        words = torch.zeros((nb, 4 * (bs // bpc)), dtype=torch.uint8, device="cuda:0")
-        arr = (DevBlock * nb)(*[DevBlock(data[b].data_ptr(), words[b].data_ptr(), bs) for b in range(nb)])
-        _native.check("compute_multi", lib.hdfs3_crc32c_compute_blocks_multi(m, arr, nb, bpc))
-        torch.cuda.synchronize()
+        arr = (DevBlock * nb)()
+        hosts = []
         for b in range(nb):
-            want = oracle_compute(data[b].cpu().numpy(), bpc)
-            assert np.array_equal(words[b].cpu().numpy(), want), b
+            h = base ^ np.uint8((b * 37 + 1) & 0xFF)  # 8 distinct blocks
+            hosts.append(h)
+            dd, dw = gpu_ctx.upload(h), DeviceBuffer(4 * (bs // bpc))
+            keep += [dd, dw]
+            arr[b] = DevBlock(dd.ptr, dw.ptr, bs)
+        _native.check("compute_multi", lib.hdfs3_crc32c_compute_blocks_multi(m, arr, nb, bpc))
+        for b in range(nb):
+            assert np.array_equal(gpu_ctx.download(keep[2 * b + 1], 4 * (bs // bpc)), oracle_compute(hosts[b], bpc)), b
         bad = (ctypes.c_int64 * nb)()
         _native.check("verify_multi", lib.hdfs3_crc32c_verify_blocks_multi(m, arr, nb, bpc, 0, bad))
         assert list(bad) == [-1] * nb
         flips = [(b, (b * 37_123 + 11) % (bs // bpc)) for b in range(nb)]  # one chunk per worker's block
         for b, k in flips:
-            data[b, k * bpc + (b * 13) % bpc] ^= 1 << (b % 8)
-        torch.cuda.synchronize()
+            pos = k * bpc + (b * 13) % bpc
+            gpu_ctx.upload(np.array([hosts[b][pos] ^ (1 << (b % 8))], np.uint8), keep[2 * b], offset=pos)
         _native.check("verify_multi", lib.hdfs3_crc32c_verify_blocks_multi(m, arr, nb, bpc, 0, bad))
         assert list(bad) == [k for _, k in flips]
     finally:

@@ -68,7 +68,8 @@ def main():
                 c.verify_dev_async(data[i % blocks].data_ptr(), bb, bpc, crc[i % blocks].data_ptr(),
                                    res.data_ptr() + 8 * (i % 4096), overlap_previous=args.overlap and i > 0)
             else:
-                c.compute_dev(data[i % blocks].data_ptr(), bb, bpc, crc[i % blocks].data_ptr())
+                c.compute_dev(data[i % blocks].data_ptr(), bb, bpc, crc[i % blocks].data_ptr(),
+                              overlap_previous=args.overlap and i > 0)
 
         cases = [("v%d_s%d" % (v, ns), (lambda v, ns: (lambda i: run(v, i, ns)))(v, ns))
                  for v in variants for ns in nstreams]
