@@ -21,14 +21,8 @@ struct ChunkLaunch {
     unsigned long long *result;  // verify: atomicMax(~first_bad) target (device)
     uint64_t chunk_base;      // added to chunk indices reported in *result
     int check_short_tail;     // 1: tail chunk checked (LocalBlockReader semantics)
-    uint64_t *trace = nullptr;  // diagnostic variant 13 only: 4 s_memrealtime stamps per wave
     bool overlap_previous = false;  // HDFS3_LAUNCH_OVERLAP_PREVIOUS: AQL packet without barrier bit
-    // the ctx's polynomial and its lane-fold matrices (host copy of crc32c_tables.h
-    // build_fold_matrices: G = 8 at word 0, G = 16 at word 8 * 32): the block kernel
-    // (crc32c_block.h) builds all its tables from these, with no table loads
-    uint32_t poly = 0;
-    const uint32_t *fold_host = nullptr;
-    // Packet stream at a constant pitch (kOptPitch, launch_packet_stream): packet i's data at
+    // Packet stream at a constant pitch (PitchWalk, launch_packet_stream): packet i's data at
     // data + i*pitch, its BE32 words at crc_be/out_be + i*pitch; every packet but the last holds
     // exactly 1 << upp_log2 whole 4 KiB rounds, the last one last_len <= that many bytes. len is
     // unused; result keys are (packet << 32) | chunk.
@@ -36,9 +30,6 @@ struct ChunkLaunch {
     uint64_t npk = 0;
     uint32_t upp_log2 = 0;
     uint32_t last_len = 0;
-    // kOptFastTail: the M_32 (advance over 32 bytes) nibble image of the ctx's polynomial,
-    // 128 words: word k*16 + e = M_32(e << 4k); set by launch_wave
-    const uint32_t *m32 = nullptr;
     // pitch mode over independent blocks at constant strides (a [blocks, bytes] tensor and its
     // [blocks, words] tensor): the words' own pitch; 0 = `pitch` (the wire layout of packets)
     uint64_t crc_pitch = 0;
@@ -135,11 +126,9 @@ hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_
 #if HDFS3_LAB
 void set_variant(int v);
 extern int g_variant;
-extern uint64_t *g_trace;
 // The A/B variants (crc32c_experiments.hip): variant != 0, bpc with a whole-round kernel.
 hipError_t launch_experiment(int variant, const ChunkLaunch &a, bool verify, const uint32_t *tab,
                              const uint32_t *fold, int grid_cap, hipStream_t s);
-void set_trace(uint64_t *d_trace);  // buffer for variant 13 (4 x u64 per wave)
 
 // Measurement-only kernels (bench/profiling): HBM read ceiling and the CRC
 // kernel's access pattern without the table arithmetic.

@@ -6,8 +6,7 @@
 namespace hdfs3crc {
 
 #if HDFS3_LAB
-int g_variant = 0;          // measurement knob (hdfs3x_set_variant); 0 = production choice
-uint64_t *g_trace = nullptr;  // timestamp buffer of the traced variants
+int g_variant = 0;  // measurement knob (hdfs3x_set_variant); 0 = production choice
 #endif
 
 namespace {
@@ -15,17 +14,15 @@ namespace {
 template <int BPC, bool V>
 hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                     hipStream_t s) {
-    // Production path: the round kernel of crc32c_wave.h for bpc <= 4096 (the multi-round kernel
-    // above that). An opted-in overlapped launch (HDFS3_LAUNCH_OVERLAP_PREVIOUS) goes out as an AQL
-    // packet without the barrier bit. Non-zero variants select the designs kept for in-process A/B
-    // (crc32c_experiments.hip, tools/ab.py; variant 90 = the round-2 production kernel).
+    // Production path: the round kernel of crc32c_wave.h for bpc <= 4096, late prefetch, the solo
+    // last step for overlapped verifies (HDFS3_LAUNCH_OVERLAP_PREVIOUS: an AQL packet without the
+    // barrier bit); the multi-round kernel above 4096. Non-zero variants select the designs kept
+    // for in-process A/B (crc32c_experiments.hip, tools/ab.py).
 #if HDFS3_LAB
     if (g_variant != 0) return launch_experiment(g_variant, a, V, tab, fold, grid_cap, s);
 #endif
-    // late prefetch; overlapped verifies end with the solo last step (for compute it costs 40 %:
-    // profiles/r03/ab_cmp_ovl.jsonl)
-    if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, 1, V>(a, tab, fold, grid_cap, s);
-    return launch_wave<BPC, V, 2, true>(a, tab, fold, grid_cap, s);
+    if constexpr (BPC <= kRoundBytes) return launch_wave3<BPC, V, false, true>(a, tab, fold, grid_cap, s);
+    return launch_r3<BPC, V, 1, true>(a, tab, fold, grid_cap, s);
 }
 
 template <int BPC>
@@ -38,15 +35,7 @@ hipError_t launch_rv(const ChunkLaunch &a, bool verify, const uint32_t *tab, con
 // packet streams at a constant pitch: the production round kernel's pitch walk
 template <int BPC, bool V>
 hipError_t launch_p(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
-#if HDFS3_LAB
-    if (g_variant == 91) {  // A/B: the round-2 kernel's pitch mode
-        constexpr int kOpt = kOptLeanFill | kOptPitch | (!V && BPC == 512 ? kOptHoldStore : 0);
-        if (a.overlap_previous)
-            return launch_wave<BPC, V, 2, true, true, false, false, true, kOpt>(a, tab, fold, grid_cap, s);
-        return launch_wave<BPC, V, 2, true, true, false, false, false, kOpt>(a, tab, fold, grid_cap, s);
-    }
-#endif
-    return launch_wave3<BPC, V, true>(a, tab, fold, grid_cap, s);
+    return launch_wave3<BPC, V, true, false>(a, tab, fold, grid_cap, s);
 }
 
 template <int BPC>
@@ -254,33 +243,10 @@ bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc) {
     return true;
 }
 
-template <int BPC, bool UNI, bool ONE = false>
-hipError_t launch_seg_k(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *nib, int grid,
-                        hipStream_t s) {
-    if (verify)
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, true, UNI, ONE>), dim3(grid), dim3(kBlockThreads), 0,
-                           s, L, tab, nib);
-    else if (BPC != 512 || g_variant == 50)  // A/B variant 50: per-round CRC-word stores (before held stores)
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false, UNI, ONE>), dim3(grid), dim3(kBlockThreads), 0,
-                           s, L, tab, nib);
-    else  // compute at bpc 512: held stores (-2.4 % per GiB of blocks, -4.3 % for packet streams)
-        hipLaunchKernelGGL((crc32c_seg_kernel<BPC, false, UNI, ONE, true>), dim3(grid), dim3(kBlockThreads), 0,
-                           s, L, tab, nib);
-    return hipGetLastError();
-}
-
 template <int BPC>
 hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *fold, int grid,
                         hipStream_t s) {
-    // production: the round kernel's core over a segment walk (crc32c_wave.h); lab variant 95 (and
-    // the diagnostic 49) keep the round-2 segmented kernel for A/B
-    if (g_variant != 95 && g_variant != 49 && g_variant != 50)
-        return verify ? launch_segments3<BPC, true>(L, tab, fold, grid, s) : launch_segments3<BPC, false>(L, tab, fold, grid, s);
-    constexpr int set = BPC == 512 ? 0 : BPC == 1024 ? 1 : BPC == 2048 ? 2 : 3;
-    const uint32_t *nib = fold + kFoldWords + set * kFoldNibbleWords;
-    if (g_variant == 49 && L.nseg == 1) return launch_seg_k<BPC, true, true>(L, verify, tab, nib, grid, s);
-    if (L.uniform) return launch_seg_k<BPC, true>(L, verify, tab, nib, grid, s);
-    return launch_seg_k<BPC, false>(L, verify, tab, nib, grid, s);
+    return verify ? launch_segments3<BPC, true>(L, tab, fold, grid, s) : launch_segments3<BPC, false>(L, tab, fold, grid, s);
 }
 
 hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,

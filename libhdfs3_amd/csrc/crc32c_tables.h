@@ -90,29 +90,19 @@ inline void build_fold_nibbles(const uint32_t fold[kFoldWords], int set, uint32_
     }
 }
 
-// M_32 (advance over 32 bytes) as a nibble image for the wave kernel's fast tail: word
-// k * 16 + e = M_32(e << 4k). Appended after the four lane-fold nibble sets.
-constexpr int kM32Words = 8 * 16;
-constexpr int kFoldM32Off = kFoldWords + 4 * kFoldNibbleWords;
-inline void build_m32_nibbles(const uint32_t t0[kTableEntries], uint32_t out[kM32Words]) {
-    uint32_t cols[32];
-    shift_cols(t0, 32, cols);
-    for (int k = 0; k < 8; ++k)
-        for (uint32_t e = 0; e < 16; ++e) out[k * 16 + e] = apply_cols(cols, e << (4 * k));
-}
-
 // Affine lane-fold nibble sets (the production round kernel, crc32c_wave.h): the sets above with
 // the chunk's init and final xor folded in. By linearity the CRC of a chunk of C = 64 G bytes is
 //   ~state(init ~0) = crc0 ^ A^C(~0) ^ ~0,   crc0 = XOR_j M_j(x_j) over chains started from 0,
 // so adding the constant K_C = A^C(~0) ^ ~0 to every k = 0 entry of lane G-1 (whose M is the
 // identity) makes the lane fold + group xor return the finished CRC: no init xor per round and
 // no final complement per chunk.
-constexpr int kFoldAffineOff = kFoldM32Off + kM32Words;
-inline void build_fold_affine(const uint32_t t0[kTableEntries], const uint32_t nib[kFoldNibbleWords], int set,
-                              uint32_t out[kFoldNibbleWords]) {
+// The device fold image is the kFoldWords matrix columns followed by the 4 affine sets.
+constexpr int kFoldAffineOff = kFoldWords;
+constexpr int kFoldImageWords = kFoldAffineOff + 4 * kFoldNibbleWords;
+// `out` holds set `set` built by build_fold_nibbles; adds K_C in place
+inline void build_fold_affine(const uint32_t t0[kTableEntries], int set, uint32_t out[kFoldNibbleWords]) {
     const int g = kFoldGs[set];
     const uint32_t kc = advance_bytes(t0, 0xFFFFFFFFu, uint64_t(64) * g) ^ 0xFFFFFFFFu;
-    for (int i = 0; i < kFoldNibbleWords; ++i) out[i] = nib[i];
     for (int lane = 0; lane < 64; ++lane)
         if (lane % g == g - 1)
             for (uint32_t e = 0; e < 16; ++e) out[e * 64 + lane] ^= kc;  // k = 0

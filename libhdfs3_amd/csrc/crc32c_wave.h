@@ -16,12 +16,12 @@
 // Every view a walk returns (data pointer, the round's CRC-word pointer, the key of its first chunk)
 // is wave-uniform, so its arithmetic is SALU and the word loads/stores take the saddr form.
 //
-// Loop shape (round 3). The buffers rotate A -> B -> A by unrolling, and the loop has ONE exit, at
-// its bottom: full steps (the ones with something to prefetch) run in pairs, then one more full step
-// if their count is odd, then the LAST step, which prefetches nothing. The round-2 kernel left its
-// loop from the middle of the body into two inlined tails; the register allocator then kept the
-// second step's rounds in two places and copied them (32 v_mov per step, +11 % VALU per round in the
-// PMC of the bench launch) and drained every load at the loop head (vmcnt(0)).
+// Loop shape (round 3). The buffers rotate A -> B -> A by unrolling; every step in a loop is the same
+// code, and whatever follows a loop reads only ONE buffer set. The round-2 kernel left its loop from
+// the middle of the body into two inlined tails, one per buffer set; the register allocator then kept
+// the second step's rounds in two places and copied them (32 v_mov per step) and drained every load
+// at the loop head (vmcnt(0)). Overlapped verifies end with a solo last step after the loop, on the
+// buffer set fixed by the parity of the wave's step count (two copies of the loop, wave_rounds).
 #pragma once
 
 #include "crc32c_device.h"
@@ -140,11 +140,11 @@ struct SegWalk {
 };
 
 // The core: prologue, steps, last step. VERIFY: compare with the stored words and fold the first bad
-// key into *result; else store the words. SOLO: the last step runs its two rounds as single chains one
-// after the other (overlapped launches: the first chain overlaps the second round's arrival and only
-// one round's lookups remain once the wave's last data landed). HOLD (compute, bpc 512): the words of
-// 8 rounds are transposed into one VGPR and up to 8 such VGPRs are stored in one burst.
-template <int BPC, bool VERIFY, bool SOLO, bool HOLD, int LATE, class Walk>
+// key into *result; else store the words. SOLO (overlapped verifies): the last step runs its two
+// rounds as single chains one after the other. HOLD (compute, bpc 512): the words of 8 rounds are
+// transposed into one VGPR and up to 8 such VGPRs are stored in one burst. LATE: see `step`. NOMATH
+// (lab diagnostic, wrong results on purpose): the table lookups replaced by an XOR of the words.
+template <int BPC, bool VERIFY, bool SOLO, bool HOLD, bool LATE, bool NOMATH, class Walk>
 __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uint32_t *__restrict__ g_tab,
                                             const uint32_t *__restrict__ g_nib, unsigned long long *result) {
     constexpr int G = BPC / 64;
@@ -179,7 +179,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
 #pragma unroll
         for (int r = 0; r < 8; ++r) l4[slot0 + ((r + tt) & 7)] = u32x4{tw, tw, tw, tw};
         if constexpr (kHalfFold) {
-            reinterpret_cast<u32x4 *>(lds + kPoolFoldOff / 4)[tt] = n0;
+            reinterpret_cast<u32x4 *>(lds + kHalfFoldOff / 4)[tt] = n0;
         } else {
             u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * tt;
             dst[0] = n0;
@@ -269,30 +269,35 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         }
     };
     auto word = [](const Round &r, int i) -> uint32_t { return r.w[i >> 2][i & 3]; };
+    // the table step of one word (NOMATH, diagnostic: a plain XOR instead, wrong on purpose)
+    auto look = [&](uint32_t x) -> Look {
+        if constexpr (NOMATH) return Look{{x, 0u, 0u, 0u}};
+        return lookups(t, x);
+    };
     // two interleaved chains over c0, c1 (chain 1's 4 reads fly while chain 0 folds)
     auto chains = [&](Round &c0, Round &c1, uint32_t &x0, uint32_t &x1) {
         x0 = word(c0, 0);
         x1 = word(c1, 0);
-        Look l0 = lookups(t, x0), l1;
+        Look l0 = look(x0), l1;
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            l1 = lookups(t, x1);
+            l1 = look(x1);
             __builtin_amdgcn_sched_barrier(0);
             x0 = combine(l0, i < 15 ? word(c0, i < 15 ? i + 1 : 15) : 0u);
             __builtin_amdgcn_sched_barrier(0);
-            if (i < 15) l0 = lookups(t, x0);
+            if (i < 15) l0 = look(x0);
             __builtin_amdgcn_sched_barrier(0);
             x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    // one round as a single chain. The two solo rounds of a last step end in different asm markers:
+    // one round as a single chain. The two solo rounds of the last step end in different asm markers:
     // identical code otherwise gets tail-merged into one copy that both run (register copies in).
     auto solo = [&](Round &c, const WView &v, uint32_t k, uint32_t w, auto id) {
         uint32_t x = word(c, 0);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) x = combine(lookups(t, x), i < 15 ? word(c, i < 15 ? i + 1 : 15) : 0u);
+        for (int i = 0; i < 16; ++i) x = combine(look(x), i < 15 ? word(c, i < 15 ? i + 1 : 15) : 0u);
         finish(k, v, group_xor<G>(fold(x)), w);
         if constexpr (decltype(id)::value == 0) asm volatile("; solo round 0" ::: "memory");
         else asm volatile("; solo round 1" ::: "memory");
@@ -300,43 +305,29 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // A step: the words of rounds k, k+1 are requested first (older than the prefetch, so waiting for
     // them never drains it: vmcnt is in-order), then the prefetch of rounds k+2, k+3 into p0, p1 (past
     // the wave's last round: the cache-resident table image), then the chains over c0, c1. The next
-    // views are resolved at the end. `fin` (wave-uniform) marks the wave's last step: with SOLO its
-    // rounds run as single chains one after the other.
-    // LATE (lab A/B): 0 early, 1 late, 2 late after every load, 3 late in the first step of each
-    // pair and early in the second, 4 the reverse. `pair_b` = the second step of a pair.
-    auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k, bool fin, auto pair_b) {
-        constexpr bool kLate = LATE == 1 || LATE == 2 || (LATE == 3 && !decltype(pair_b)::value) ||
-                               (LATE == 4 && decltype(pair_b)::value);
+    // views are resolved at the end.
+    // LATE (production): the prefetch goes out once this step's rounds have landed, so at most 8 KiB
+    // are in flight per wave (128 KiB per CU), not 16: more requests in flight lower the DRAM
+    // efficiency. LATE = false (lab A/B): issued at the start of the step.
+    auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k) {
         const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
-        if (!kLate) {
+        if constexpr (!LATE) {
             load_round_buf<true>(p0, pv0.p, lane_off);
             load_round_buf<true>(p1, pv1.p, lane_off);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (SOLO && fin) {
-            regroup(c0);
-            solo(c0, cv0, k, w0, std::integral_constant<int, 0>{});
-            regroup(c1);
-            solo(c1, cv1, k + 1, w1, std::integral_constant<int, 1>{});
-        } else {
-            regroup(c0);
-            regroup(c1);
-            if constexpr (kLate) {
-                // the prefetch goes out once this step's rounds have landed: at most 8 KiB in
-                // flight per wave (128 KiB per CU), not 16 (more requests in flight lower the
-                // DRAM efficiency; the round-2 kernel got this by accident from
-                // register-reuse waits at its loop head). LATE 2 (lab): also after the words.
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (LATE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                load_round_buf<true>(p0, pv0.p, lane_off);
-                load_round_buf<true>(p1, pv1.p, lane_off);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            uint32_t x0, x1;
-            chains(c0, c1, x0, x1);
-            finish(k, cv0, group_xor<G>(fold(x0)), w0);
-            finish(k + 1, cv1, group_xor<G>(fold(x1)), w1);
+        regroup(c0);
+        regroup(c1);
+        if constexpr (LATE) {
+            __builtin_amdgcn_sched_barrier(0);
+            load_round_buf<true>(p0, pv0.p, lane_off);
+            load_round_buf<true>(p1, pv1.p, lane_off);
+            __builtin_amdgcn_sched_barrier(0);
         }
+        uint32_t x0, x1;
+        chains(c0, c1, x0, x1);
+        finish(k, cv0, group_xor<G>(fold(x0)), w0);
+        finish(k + 1, cv1, group_xor<G>(fold(x1)), w1);
         __builtin_amdgcn_sched_barrier(0);
         cv0 = pv0;
         cv1 = pv1;
@@ -344,13 +335,47 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         pv1 = walk.view(k + 5);
     };
 
-    // The A -> B -> A rotation by unrolling, every step the same code (a special last step outside
-    // the loop made the register allocator copy the rounds: 32 v_mov per step in round 2).
+    // The A -> B -> A rotation by unrolling. Every loop has one exit, at its bottom, and every step
+    // in it is the same code: an exit from the middle of the body, or a special last step that values
+    // reach from both buffer sets, makes the register allocator copy the rounds (32 v_mov per step).
     const uint32_t nr = (K + 1) & ~1u;  // rounds rounded up to whole steps
-    for (uint32_t k = 0; k < nr; k += 4) {
-        step(a0, a1, b0, b1, k, k + 2 >= nr, std::false_type{});
-        if (k + 2 >= nr) break;
-        step(b0, b1, a0, a1, k + 2, k + 4 >= nr, std::true_type{});
+    if constexpr (SOLO) {
+        // The last step outside the loop, its two rounds as single chains one after the other: the
+        // first chain overlaps the second round's arrival, and only one round's lookups remain once
+        // the wave's last data has landed. Its buffers are STATIC: with F = nr / 2 - 1 full steps,
+        // F even runs pairs A -> B -> A and ends in A; F odd runs one step A -> B, then pairs
+        // B -> A -> B, and ends in B. Two copies of the loop; no value crosses between them.
+        auto last = [&](Round &c0, Round &c1, uint32_t k) {
+            const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
+            __builtin_amdgcn_sched_barrier(0);
+            regroup(c0);
+            solo(c0, cv0, k, w0, std::integral_constant<int, 0>{});
+            regroup(c1);
+            solo(c1, cv1, k + 1, w1, std::integral_constant<int, 1>{});
+        };
+        if (nr != 0) {
+            const uint32_t kl = nr - 2;  // the last step's first round
+            if ((kl >> 1) & 1) {
+                step(a0, a1, b0, b1, 0);
+                for (uint32_t k = 2; k < kl; k += 4) {
+                    step(b0, b1, a0, a1, k);
+                    step(a0, a1, b0, b1, k + 2);
+                }
+                last(b0, b1, kl);
+            } else {
+                for (uint32_t k = 0; k < kl; k += 4) {
+                    step(a0, a1, b0, b1, k);
+                    step(b0, b1, a0, a1, k + 2);
+                }
+                last(a0, a1, kl);
+            }
+        }
+    } else {
+        for (uint32_t k = 0; k < nr; k += 4) {
+            step(a0, a1, b0, b1, k);
+            if (k + 2 >= nr) break;
+            step(b0, b1, a0, a1, k + 2);
+        }
     }
     if constexpr (kHold) flush();
 }
@@ -381,7 +406,7 @@ __device__ __forceinline__ void slow_region(const uint32_t *lds, const uint8_t *
 }
 
 // One block (PITCH = false) or a constant-pitch stream (PITCH = true, ChunkLaunch::pitch/npk/...).
-template <int BPC, bool VERIFY, bool PITCH, bool SOLO, int LATE = 1>
+template <int BPC, bool VERIFY, bool PITCH, bool SOLO, bool LATE = true, bool NOMATH = false>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 512 == 0, "one-round units");
@@ -398,7 +423,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves,
                           uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), a.upp_log2,
                           dummy};
-        wave_rounds<BPC, VERIFY, SOLO, kHold, LATE>(w, lds, g_tab, g_nib, a.result);
+        wave_rounds<BPC, VERIFY, SOLO, kHold, LATE, NOMATH>(w, lds, g_tab, g_nib, a.result);
         const uint64_t lp = a.npk - 1;
         slow_region<BPC, VERIFY>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
                                  a.check_short_tail, a.result);
@@ -406,7 +431,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         const uint64_t nunits = a.len / kRoundBytes;
         BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves,
                           uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), dummy};
-        wave_rounds<BPC, VERIFY, SOLO, kHold, LATE>(w, lds, g_tab, g_nib, a.result);
+        wave_rounds<BPC, VERIFY, SOLO, kHold, LATE, NOMATH>(w, lds, g_tab, g_nib, a.result);
         slow_region<BPC, VERIFY>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     }
 }
@@ -425,7 +450,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunc
     SegWalk<kCpu, UNI> w{&L, wave, nwaves,
                          uint32_t(rfl64(wave < L.units ? (L.units - wave + nwaves - 1) / nwaves : 0)),
                          reinterpret_cast<const uint8_t *>(g_tab)};
-    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, true>(w, lds, g_tab, g_nib, L.result);
+    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, true, false>(w, lds, g_tab, g_nib, L.result);
 
     const Lut t(lds);
     const uint64_t items = uint64_t(L.nseg) * kCpu;
@@ -457,12 +482,15 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunc
     }
 }
 
-// Overlapped verifies up to 256 MiB per launch end with the solo last step (21.94 -> 21.34 us per
-// 128 MiB launch at bpc 512 in round 2; 1 % slower at 1 GiB per launch, +0.9 us barriered:
-// profiles/r02_kernel_study/r02_ab_solo_*.jsonl).
+// Overlapped verifies up to 256 MiB per launch end with the solo last step: 21.45 -> 21.02 us per
+// 128 MiB launch at bpc 512 and 21.61 -> 21.48 at 4096 against the round-2 kernel in the same
+// process (profiles/r03/r3g_ab_ovl.jsonl, variants 102 / 90). Barriered launches and launches past
+// 256 MiB keep the interleaved last step (round 2: +0.9 us barriered, +1 % at 1 GiB with it);
+// compute keeps it too (its held stores flush at the wave's end).
 constexpr uint64_t kSoloTailMaxBytes = uint64_t(256) << 20;
 
-template <int BPC, bool V, bool PITCH, int LATE = 1, bool SOLO = false>
+// SOLO: the solo last step when the launch qualifies (above); LATE / NOMATH: lab A/B.
+template <int BPC, bool V, bool PITCH, bool SOLO, bool LATE = true, bool NOMATH = false>
 hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
     constexpr int G = BPC / 64;
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
@@ -472,18 +500,18 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
     if (grid < 1) grid = 1;
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
-        if constexpr (SOLO && !PITCH) {
+        if constexpr (SOLO && V && !PITCH) {
             if (units * kRoundBytes <= kSoloTailMaxBytes) {
-                hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LATE>), dim3(grid), dim3(kBlockThreads),
-                                      0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+                hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LATE, NOMATH>), dim3(grid),
+                                      dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
                 return hipGetLastError();
             }
         }
-        hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LATE>), dim3(grid), dim3(kBlockThreads), 0, s,
-                              nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+        hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LATE, NOMATH>), dim3(grid),
+                              dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
     } else {
-        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LATE>), dim3(grid), dim3(kBlockThreads), 0, s, a,
-                           tab, nib);
+        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LATE, NOMATH>), dim3(grid), dim3(kBlockThreads),
+                           0, s, a, tab, nib);
     }
     return hipGetLastError();
 }

@@ -95,7 +95,6 @@ struct hdfs3_crc_ctx {
     uint32_t *d_fold_by[2] = {nullptr, nullptr};
     int checksum_type = 2;
     uint32_t poly = 0x82F63B78u;        // reflected polynomial of checksum_type
-    const uint32_t *fold_host = nullptr;  // host fold matrices of checksum_type (ChunkLaunch::fold_host)
     unsigned long long *d_result = nullptr;
     unsigned long long *h_result = nullptr;  // pinned
     // blocks API: a ring of descriptor stagings, each reusable once its event fired

@@ -49,11 +49,11 @@ int fail(int code, const char *fmt, ...) {
 namespace hdfs3crc {
 
 // Per polynomial ([0] CRC32C, [1] CRC32): slice tables, then the fold image (kFoldWords
-// matrix columns, 4 nibble-table sets for G = 8, 16, 32, 64, the M_32 image and the 4 affine
-// sets of the production round kernel), built once per process.
+// matrix columns, then the 4 affine nibble-table sets for G = 8, 16, 32, 64 of the round
+// kernel), built once per process.
 struct HostImage {
     uint32_t t[kSlices][kTableEntries];
-    uint32_t fold[kFoldWords + 4 * kFoldNibbleWords + kM32Words + 4 * kFoldNibbleWords];
+    uint32_t fold[kFoldImageWords];
 };
 
 const HostImage *host_images() {
@@ -64,12 +64,11 @@ const HostImage *host_images() {
         for (int p = 0; p < 2; ++p) {
             build_slice_tables(img[p].t, polys[p]);
             build_fold_matrices(img[p].t[0], img[p].fold);
-            for (int set = 0; set < 4; ++set)
-                build_fold_nibbles(img[p].fold, set, img[p].fold + kFoldWords + set * kFoldNibbleWords);
-            build_m32_nibbles(img[p].t[0], img[p].fold + kFoldM32Off);
-            for (int set = 0; set < 4; ++set)
-                build_fold_affine(img[p].t[0], img[p].fold + kFoldWords + set * kFoldNibbleWords, set,
-                                  img[p].fold + kFoldAffineOff + set * kFoldNibbleWords);
+            for (int set = 0; set < 4; ++set) {
+                uint32_t *nib = img[p].fold + kFoldAffineOff + set * kFoldNibbleWords;
+                build_fold_nibbles(img[p].fold, set, nib);
+                build_fold_affine(img[p].t[0], set, nib);
+            }
         }
     });
     return img;
@@ -140,8 +139,6 @@ int finish_pending(Slot &s) {
 
 int launch(hdfs3_crc_ctx *ctx, const ChunkLaunch &in, bool verify) {
     ChunkLaunch a = in;
-    a.poly = ctx->poly;
-    a.fold_host = ctx->fold_host;
     HIP_TRY(launch_chunks(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
     ++ctx->launches;
     return 0;
@@ -489,7 +486,6 @@ int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out) {
     ctx->d_tables = ctx->d_tables_by[0];
     ctx->d_fold = ctx->d_fold_by[0];
     ctx->poly = kPolyReflected;
-    ctx->fold_host = img[0].fold;
     *out = ctx;
     return 0;
 }
@@ -623,7 +619,6 @@ int ctx_acquire(int device, hdfs3_crc_ctx **out, bool deep) {
             ctx->d_tables = ctx->d_tables_by[0];
             ctx->d_fold = ctx->d_fold_by[0];
             ctx->poly = kPolyReflected;
-            ctx->fold_host = host_images()[0].fold;
             *out = ctx;
             return 0;
         }
@@ -714,7 +709,6 @@ int hdfs3_crc_ctx_set_checksum_type(hdfs3_crc_ctx *ctx, int type) {
     ctx->d_tables = ctx->d_tables_by[i];
     ctx->d_fold = ctx->d_fold_by[i];
     ctx->poly = i == 0 ? kPolyReflected : kPolyCrc32;
-    ctx->fold_host = host_images()[i].fold;
     ctx->checksum_type = type;
     return 0;
 }
@@ -1063,7 +1057,6 @@ int hdfs3x_grid_cap(hdfs3_crc_ctx *ctx) { return ctx ? ctx->grid_cap : 0; }
 
 // Process-wide kernel-variant knob for in-process A/B measurements (tools/ab.py).
 void hdfs3x_set_variant(int v) { set_variant(v); }
-void hdfs3x_set_trace(void *d_trace) { set_trace(static_cast<uint64_t *>(d_trace)); }
 
 }  // extern "C"
 #endif  // HDFS3_LAB

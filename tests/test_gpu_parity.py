@@ -255,11 +255,10 @@ def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
             assert gpu_ctx.verify(bad, 512, crc, True) == 3
 
 
-# every bit-exact variant (diagnostic variants 9-13, 15, 19, 21-25, 29, 34, 35, 37, 38, 41 time
-# or trace and give wrong results on purpose)
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 14, 16, 18, 20, 26, 27, 28, 30, 31, 32, 33, 36, 40, 42, 43, 44, 46, 47, 48,
-                                     60, 61, 70, 72, 73, 74, 75, 78, 79, 82])
-@pytest.mark.parametrize("bpc", [512, 1024, 2048, 4096, 8192])
+# every bit-exact variant (the diagnostic variant 77 gives wrong results on purpose); the lab
+# variants exist for the round kernel's chunk sizes only
+@pytest.mark.parametrize("variant,bpc", [(0, b) for b in (512, 1024, 2048, 4096, 8192)] +
+                         [(v, b) for v in (92, 93) for b in (512, 1024, 2048, 4096)])
 def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
     """All kernel designs kept for A/B (hdfs3x_set_variant) are parity-checked too:
     whole rounds, the slow region (len not a multiple of the 4 KiB round) and the tail."""
@@ -283,6 +282,47 @@ def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
                 lab_ctx.upload(np.array([data[pos] ^ 4], np.uint8), d, offset=pos)
                 assert lab_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, False) == k, (variant, bpc, n, k)
                 lab_ctx.upload(data[pos:pos + 1], d, offset=pos)
+    finally:
+        lib.hdfs3x_set_variant(0)
+
+
+@pytest.mark.parametrize("variant", [0, 92, 93])
+@pytest.mark.parametrize("bpc", [512, 2048, 4096])
+def test_round_kernel_variants_overlapped_match_oracle(lab_ctx, variant, bpc):
+    """The round kernel's prefetch/last-step variants as they run in the bench: overlapped
+    launches (the solo last step only runs there), sizes giving 1 to 9 rounds per wave so both
+    loop copies of the solo form (an even and an odd number of full steps) run, a bad chunk
+    located."""
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    lib = _native.lab()
+    sizes = [(8 << 20) + 4099, (48 << 20) + 3 * 4096, 64 << 20, (100 << 20) + 777, (132 << 20) + bpc]
+    try:
+        lib.hdfs3x_set_variant(variant)
+        res = DeviceBuffer(8 * 2 * len(sizes))
+        lab_ctx.memset(res, 0, 8 * 2 * len(sizes))
+        blocks, bads = [], []
+        for i, n in enumerate(sizes):
+            data = splitmix_bytes(n, 7000 + variant * 10 + i + bpc)
+            blocks.append((lab_ctx.upload(data), lab_ctx.upload(oracle_compute(data, bpc)), n, data))
+            nc = n // bpc
+            bads.append((nc - 1) if i % 2 else (nc // 3 + i))
+        lab_ctx.synchronize()
+        for i, (d, c, n, _) in enumerate(blocks):  # one overlapped chain over clean blocks
+            lab_ctx.verify_dev_async(d.ptr, n, bpc, c.ptr, res.ptr + 16 * i, overlap_previous=i > 0)
+        lab_ctx.synchronize()
+        for (d, _, _, data), bad in zip(blocks, bads):
+            pos = bad * bpc + 7
+            lab_ctx.upload(np.array([data[pos] ^ 0x10], np.uint8), d, offset=pos)
+        lab_ctx.synchronize()
+        for i, (d, c, n, _) in enumerate(blocks):  # and over the corrupted ones
+            lab_ctx.verify_dev_async(d.ptr, n, bpc, c.ptr, res.ptr + 16 * i + 8, overlap_previous=i > 0)
+        lab_ctx.synchronize()
+        words = lab_ctx.download(res, 16 * len(sizes)).view(np.uint64)
+        for i in range(len(sizes)):
+            assert lab_ctx.decode_result(int(words[2 * i])) == -1, (variant, bpc, i)
+            assert lab_ctx.decode_result(int(words[2 * i + 1])) == bads[i], (variant, bpc, i)
     finally:
         lib.hdfs3x_set_variant(0)
 

@@ -150,16 +150,15 @@ def test_packet_fast_path_agrees_with_packet_kernel(lab_ctx, bpc):
 
 
 @pytest.mark.parametrize("bpc", [512, 2048, 4096])
-@pytest.mark.parametrize("variant", [0, 49])
-def test_single_segment_batch(lab_ctx, bpc, variant):
-    """One block through the batch API (segmented kernel with one segment); variant 49 fixes
-    the segment view at kernel start (A/B, tools/seg_ab.py). Words and first bad chunk."""
+def test_single_segment_batch(lab_ctx, bpc):
+    """One block through the batch API (segmented kernel with one segment). Words and first
+    bad chunk."""
     from libhdfs3_amd import _native
 
     lib = _native.lab()
     n = 4096 * 1000 + 3 * bpc + 77
     try:
-        lib.hdfs3x_set_variant(variant)
+        lib.hdfs3x_set_variant(0)
         blocks, keep, datas = make_blocks(lab_ctx, [n], bpc, 4900 + bpc)
         lab_ctx.compute_blocks_dev(blocks, bpc)
         d, c, _ = blocks[0]

@@ -3,8 +3,7 @@
   contiguous   hdfs3_crc32c_verify_dev_async over the 8 contiguous 128 MiB blocks
   blocks       hdfs3_crc32c_verify_blocks_dev_async, the same bytes as 8 independent blocks
   one_segment  the same API with the whole 1 GiB as ONE block (segmented kernel, 1 segment)
-  one_segment_r2_v95 the same through the round-2 segmented kernel (A/B variant 95)
-  ragged       the same bytes as 8 blocks of unequal lengths (binary-search segment walk), and _r2_v95
+  ragged       the same bytes as 8 blocks of unequal lengths (binary-search segment walk)
 HIP-event timed, interleaved rounds, median us per launch."""
 import json
 import os
@@ -47,13 +46,6 @@ def main():
     def one_segment(i):
         ctx.verify_blocks_dev_async(one, bpc, res.data_ptr() + 8 * (i % 1024))
 
-    def one_segment_v(v):
-        def f(i):
-            lib.hdfs3x_set_variant(v)
-            ctx.verify_blocks_dev_async(one, bpc, res.data_ptr() + 8 * (i % 1024))
-            lib.hdfs3x_set_variant(0)
-        return f
-
     # ragged: the same bytes as 8 blocks of unequal whole-round lengths (binary-search segment walk)
     cut = [0] + [b * bb + (b * 37 % 11 - 5) * 4096 * 16 for b in range(1, nb)] + [nb * bb]
     ragged = [(data.data_ptr() + cut[b], crc.data_ptr() + 4 * (cut[b] // bpc), cut[b + 1] - cut[b]) for b in range(nb)]
@@ -65,9 +57,7 @@ def main():
             lib.hdfs3x_set_variant(0)
         return f
 
-    # v95: the round-2 segmented kernel (before the segment walk of crc32c_wave.h)
-    cases = {"contiguous": contiguous, "blocks": blk(0), "one_segment": one_segment,
-             "one_segment_r2_v95": one_segment_v(95), "ragged": ragged_v(0), "ragged_r2_v95": ragged_v(95)}
+    cases = {"contiguous": contiguous, "blocks": blk(0), "one_segment": one_segment, "ragged": ragged_v(0)}
     samples = {k: [] for k in cases}
     for f in cases.values():  # ramp the clocks (~25 ms of load)
         for i in range(100):
