@@ -15,11 +15,15 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
     if constexpr (BPC <= kRoundBytes) {
         switch (variant) {
         case 92:  // production with the prefetch issued at the start of each step (early)
-            return launch_wave3<BPC, V, false, true, false>(a, tab, fold, grid_cap, s);
+            return launch_wave3<BPC, V, false, true, kLabEarly>(a, tab, fold, grid_cap, s);
         case 93:  // production without the solo last step (overlapped verifies end interleaved)
             return launch_wave3<BPC, V, false, false>(a, tab, fold, grid_cap, s);
+        case 94:  // the solo last step for overlapped verifies only (round-3 production before r3i)
+            return launch_wave3<BPC, V, false, V>(a, tab, fold, grid_cap, s);
+        case 95:  // compute at bpc 512 without held stores (each round's words stored at once)
+            return launch_wave3<BPC, V, false, true, kLabNoHold>(a, tab, fold, grid_cap, s);
         case 77:  // diagnostic: production with the table lookups replaced by an XOR (wrong results)
-            return launch_wave3<BPC, V, false, true, true, true>(a, tab, fold, grid_cap, s);
+            return launch_wave3<BPC, V, false, true, kLabNoMath>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;
         }
     }

@@ -15,8 +15,8 @@ template <int BPC, bool V>
 hipError_t launch_r(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                     hipStream_t s) {
     // Production path: the round kernel of crc32c_wave.h for bpc <= 4096, late prefetch, the solo
-    // last step for overlapped verifies (HDFS3_LAUNCH_OVERLAP_PREVIOUS: an AQL packet without the
-    // barrier bit); the multi-round kernel above 4096. Non-zero variants select the designs kept
+    // last step for overlapped launches up to 256 MiB (HDFS3_LAUNCH_OVERLAP_PREVIOUS: an AQL packet
+    // without the barrier bit); the multi-round kernel above 4096. Non-zero variants select the designs kept
     // for in-process A/B (crc32c_experiments.hip, tools/ab.py).
 #if HDFS3_LAB
     if (g_variant != 0) return launch_experiment(g_variant, a, V, tab, fold, grid_cap, s);

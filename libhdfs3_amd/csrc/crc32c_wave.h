@@ -29,11 +29,18 @@
 namespace hdfs3crc {
 namespace {
 
+// Lab-only bits of the round kernel (crc32c_experiments.hip; production passes 0):
+constexpr int kLabEarly = 1;   // prefetch issued at the start of each step, not after its rounds landed
+constexpr int kLabNoMath = 2;  // diagnostic: table lookups replaced by an XOR of the words (wrong results)
+constexpr int kLabNoHold = 4;  // compute at bpc 512: store each round's words at once (no held stores)
+
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
 typedef __attribute__((address_space(1))) const uint8_t gcu8;
 typedef __attribute__((address_space(1))) uint8_t gu8;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(4))) const SegLaunch CSegLaunch;
+typedef __attribute__((address_space(4))) const DevSegment CDevSegment;
 
 // A round's view: data, CRC words of its first chunk (stored words when verifying, the output when
 // computing), result key of its first chunk.
@@ -91,7 +98,11 @@ struct PitchWalk {
 template <int CPU, bool UNI>
 struct SegWalk {
     static constexpr bool kLaneView = false;
-    const SegLaunch *L;
+    // The launch record and the descriptors through the CONSTANT address space: their fields are
+    // wave-uniform, so they load with s_load (lgkmcnt). Through a generic pointer they compiled to
+    // FLAT loads, which count on vmcnt as well, and every segment crossing then waited for the whole
+    // prefetch stream (vmcnt(0)) before it could resolve the next view.
+    CSegLaunch *L;
     uint64_t first, stride;
     uint32_t K;
     const uint8_t *dummy;
@@ -99,7 +110,9 @@ struct SegWalk {
     const uint8_t *c_data = nullptr;
     uint8_t *c_crc = nullptr;
 
-    __device__ __forceinline__ const DevSegment *segp(uint32_t i) const { return L->seg ? L->seg + i : L->inl + i; }
+    __device__ __forceinline__ CDevSegment *segp(uint32_t i) const {
+        return L->seg ? (CDevSegment *)(L->seg) + i : L->inl + i;
+    }
     __device__ __forceinline__ uint32_t seg_of(uint64_t u) const {
         if constexpr (UNI) {  // unit counts stay < 2^32 (16 TiB per launch): 32-bit divide
             const uint32_t si = uint32_t(u) / uint32_t(L->uniform);
@@ -126,7 +139,7 @@ struct SegWalk {
                 c_crc = L->inl[0].crc + uint64_t(si) * L->stride;
                 c_key = uint64_t(si) << 32;
             } else {
-                const DevSegment *sd = segp(si);
+                CDevSegment *sd = segp(si);
                 c_begin = rfl64(sd->unit_begin);
                 c_end = c_begin + rfl64(sd->len) / kRoundBytes;
                 c_data = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->data)));
@@ -142,13 +155,13 @@ struct SegWalk {
 // The core: prologue, steps, last step. VERIFY: compare with the stored words and fold the first bad
 // key into *result; else store the words. SOLO (overlapped verifies): the last step runs its two
 // rounds as single chains one after the other. HOLD (compute, bpc 512): the words of 8 rounds are
-// transposed into one VGPR and up to 8 such VGPRs are stored in one burst. LATE: see `step`. NOMATH
-// (lab diagnostic, wrong results on purpose): the table lookups replaced by an XOR of the words.
-template <int BPC, bool VERIFY, bool SOLO, bool HOLD, bool LATE, bool NOMATH, class Walk>
+// transposed into one VGPR and up to 8 such VGPRs are stored in one burst. LAB: lab-only bits (kLab*).
+template <int BPC, bool VERIFY, bool SOLO, bool HOLD, int LAB, class Walk>
 __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uint32_t *__restrict__ g_tab,
                                             const uint32_t *__restrict__ g_nib, unsigned long long *result) {
     constexpr int G = BPC / 64;
     constexpr bool kHalfFold = G <= 32;
+    constexpr bool LATE = (LAB & kLabEarly) == 0, NOMATH = (LAB & kLabNoMath) != 0;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = lane % G;
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
@@ -261,7 +274,9 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         if (k >= K || j != 0) return;
         const uint32_t c = y;
         if constexpr (VERIFY) {
-            if (__builtin_bswap32(want) != c)
+            // kLabNoMath computes wrong CRCs: compare inverted so it does not flag every chunk (an
+            // atomic per chunk would dominate the diagnostic's time)
+            if ((__builtin_bswap32(want) != c) != NOMATH)
                 __hip_atomic_fetch_max((gu64 *)result, ~(unsigned long long)(v.key + lane / G), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         } else {
@@ -269,7 +284,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         }
     };
     auto word = [](const Round &r, int i) -> uint32_t { return r.w[i >> 2][i & 3]; };
-    // the table step of one word (NOMATH, diagnostic: a plain XOR instead, wrong on purpose)
+    // the table step of one word (kLabNoMath, diagnostic: a plain XOR instead, wrong on purpose)
     auto look = [&](uint32_t x) -> Look {
         if constexpr (NOMATH) return Look{{x, 0u, 0u, 0u}};
         return lookups(t, x);
@@ -308,7 +323,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // views are resolved at the end.
     // LATE (production): the prefetch goes out once this step's rounds have landed, so at most 8 KiB
     // are in flight per wave (128 KiB per CU), not 16: more requests in flight lower the DRAM
-    // efficiency. LATE = false (lab A/B): issued at the start of the step.
+    // efficiency. kLabEarly (lab A/B): issued at the start of the step.
     auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k) {
         const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
         if constexpr (!LATE) {
@@ -406,7 +421,7 @@ __device__ __forceinline__ void slow_region(const uint32_t *lds, const uint8_t *
 }
 
 // One block (PITCH = false) or a constant-pitch stream (PITCH = true, ChunkLaunch::pitch/npk/...).
-template <int BPC, bool VERIFY, bool PITCH, bool SOLO, bool LATE = true, bool NOMATH = false>
+template <int BPC, bool VERIFY, bool PITCH, bool SOLO, int LAB = 0>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 512 == 0, "one-round units");
@@ -416,14 +431,14 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
     const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t *words = VERIFY ? const_cast<uint8_t *>(a.crc_be) : a.out_be;
     const uint8_t *dummy = reinterpret_cast<const uint8_t *>(g_tab);
-    constexpr bool kHold = !VERIFY && BPC == 512;
+    constexpr bool kHold = !VERIFY && BPC == 512 && (LAB & kLabNoHold) == 0;
     if constexpr (PITCH) {
         const uint64_t nunits = ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes;
         // the division runs in VALU; readfirstlane puts K back in SGPRs so every k < K below is SALU
         PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves,
                           uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), a.upp_log2,
                           dummy};
-        wave_rounds<BPC, VERIFY, SOLO, kHold, LATE, NOMATH>(w, lds, g_tab, g_nib, a.result);
+        wave_rounds<BPC, VERIFY, SOLO, kHold, LAB>(w, lds, g_tab, g_nib, a.result);
         const uint64_t lp = a.npk - 1;
         slow_region<BPC, VERIFY>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
                                  a.check_short_tail, a.result);
@@ -431,7 +446,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         const uint64_t nunits = a.len / kRoundBytes;
         BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves,
                           uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), dummy};
-        wave_rounds<BPC, VERIFY, SOLO, kHold, LATE, NOMATH>(w, lds, g_tab, g_nib, a.result);
+        wave_rounds<BPC, VERIFY, SOLO, kHold, LAB>(w, lds, g_tab, g_nib, a.result);
         slow_region<BPC, VERIFY>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     }
 }
@@ -447,10 +462,10 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunc
     constexpr int kCpu = kRoundBytes / BPC;
     const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
     const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    SegWalk<kCpu, UNI> w{&L, wave, nwaves,
+    SegWalk<kCpu, UNI> w{(CSegLaunch *)(&L), wave, nwaves,
                          uint32_t(rfl64(wave < L.units ? (L.units - wave + nwaves - 1) / nwaves : 0)),
                          reinterpret_cast<const uint8_t *>(g_tab)};
-    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, true, false>(w, lds, g_tab, g_nib, L.result);
+    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, 0>(w, lds, g_tab, g_nib, L.result);
 
     const Lut t(lds);
     const uint64_t items = uint64_t(L.nseg) * kCpu;
@@ -465,7 +480,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunc
             sd.len = si + 1 < L.nseg ? L.inl[0].len : L.inl[1].len;
             sd.key_base = uint64_t(si) << 32;
         } else {
-            sd = *w.segp(si);
+            sd = L.seg ? L.seg[si] : L.inl[si];  // per-thread index: vector loads
         }
         const uint64_t nfull = sd.len / BPC;
         const uint64_t c = (sd.len / kRoundBytes) * kCpu + it % kCpu;
@@ -482,15 +497,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunc
     }
 }
 
-// Overlapped verifies up to 256 MiB per launch end with the solo last step: 21.45 -> 21.02 us per
-// 128 MiB launch at bpc 512 and 21.61 -> 21.48 at 4096 against the round-2 kernel in the same
-// process (profiles/r03/r3g_ab_ovl.jsonl, variants 102 / 90). Barriered launches and launches past
-// 256 MiB keep the interleaved last step (round 2: +0.9 us barriered, +1 % at 1 GiB with it);
-// compute keeps it too (its held stores flush at the wave's end).
+// Overlapped launches up to 256 MiB end with the solo last step. Verify, 128 MiB at bpc 512:
+// 21.52 -> 20.71 us per launch against the interleaved last step (variant 93), 21.45 -> 21.02
+// against the round-2 kernel (profiles/r03/r3h_ab_ovl.jsonl, r3g_ab_ovl.jsonl); compute at bpc
+// 512: 22.63 -> 22.24 us (variant 94 before it became production, r3i_ab_cmp_ovl.jsonl).
+// Barriered launches and launches past 256 MiB keep the interleaved last step (round 2: +0.9 us
+// barriered and +1 % at 1 GiB with it).
 constexpr uint64_t kSoloTailMaxBytes = uint64_t(256) << 20;
 
-// SOLO: the solo last step when the launch qualifies (above); LATE / NOMATH: lab A/B.
-template <int BPC, bool V, bool PITCH, bool SOLO, bool LATE = true, bool NOMATH = false>
+// SOLO: the solo last step when the launch qualifies (above); LAB: lab A/B bits.
+template <int BPC, bool V, bool PITCH, bool SOLO, int LAB = 0>
 hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
     constexpr int G = BPC / 64;
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
@@ -500,17 +516,17 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
     if (grid < 1) grid = 1;
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
-        if constexpr (SOLO && V && !PITCH) {
+        if constexpr (SOLO && !PITCH) {
             if (units * kRoundBytes <= kSoloTailMaxBytes) {
-                hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LATE, NOMATH>), dim3(grid),
+                hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LAB>), dim3(grid),
                                       dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
                 return hipGetLastError();
             }
         }
-        hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LATE, NOMATH>), dim3(grid),
+        hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB>), dim3(grid),
                               dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
     } else {
-        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LATE, NOMATH>), dim3(grid), dim3(kBlockThreads),
+        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB>), dim3(grid), dim3(kBlockThreads),
                            0, s, a, tab, nib);
     }
     return hipGetLastError();

@@ -62,7 +62,7 @@ def test_ragged_lengths_host_and_device(ctx32, bpc):
     assert ctx32.compute(first, bpc)[:4].view(">u4")[0] == zlib.crc32(first[:bpc].tobytes())
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95])
 @pytest.mark.parametrize("bpc", [512, 4096])
 def test_every_kernel_variant_crc32(lab_ctx, variant, bpc):
     from libhdfs3_amd import _native

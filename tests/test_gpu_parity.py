@@ -258,7 +258,7 @@ def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
 # every bit-exact variant (the diagnostic variant 77 gives wrong results on purpose); the lab
 # variants exist for the round kernel's chunk sizes only
 @pytest.mark.parametrize("variant,bpc", [(0, b) for b in (512, 1024, 2048, 4096, 8192)] +
-                         [(v, b) for v in (92, 93) for b in (512, 1024, 2048, 4096)])
+                         [(v, b) for v in (92, 93, 94, 95) for b in (512, 1024, 2048, 4096)])
 def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
     """All kernel designs kept for A/B (hdfs3x_set_variant) are parity-checked too:
     whole rounds, the slow region (len not a multiple of the 4 KiB round) and the tail."""
@@ -286,7 +286,7 @@ def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
         lib.hdfs3x_set_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94])
 @pytest.mark.parametrize("bpc", [512, 2048, 4096])
 def test_round_kernel_variants_overlapped_match_oracle(lab_ctx, variant, bpc):
     """The round kernel's prefetch/last-step variants as they run in the bench: overlapped
@@ -492,3 +492,33 @@ def test_host_api_random_sizes_and_offsets(gpu_ctx):
         bad = data.copy()
         bad[pos] ^= 0x02
         assert gpu_ctx.verify(bad, bpc, want, True) == pos // bpc, (n, off, bpc, pos)
+
+
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95])
+@pytest.mark.parametrize("bpc", [512, 4096])
+def test_round_kernel_variants_overlapped_compute_match_oracle(lab_ctx, variant, bpc):
+    """Compute-mode variants of the round kernel (held stores or not, solo last step or not) as
+    overlapped chains: sizes giving 1 to 9 rounds per wave (both loop copies of the solo form, a
+    partial octet of held words), arrays poisoned with 0xA5 first, every word against the oracle."""
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    lib = _native.lab()
+    sizes = [(8 << 20) + 4099, (48 << 20) + 3 * 4096, 64 << 20, (100 << 20) + 777, (132 << 20) + bpc]
+    try:
+        lib.hdfs3x_set_variant(variant)
+        blocks = []
+        for i, n in enumerate(sizes):
+            data = splitmix_bytes(n, 8100 + variant * 10 + i + bpc)
+            want = oracle_compute(data, bpc)
+            out = DeviceBuffer(want.nbytes)
+            lab_ctx.memset(out, 0xA5, want.nbytes)
+            blocks.append((lab_ctx.upload(data), out, n, want))
+        lab_ctx.synchronize()
+        for i, (d, out, n, _) in enumerate(blocks):
+            lab_ctx.compute_dev(d.ptr, n, bpc, out.ptr, overlap_previous=i > 0)
+        lab_ctx.synchronize()
+        for i, (_, out, _, want) in enumerate(blocks):
+            assert np.array_equal(lab_ctx.download(out, want.nbytes), want), (variant, bpc, i)
+    finally:
+        lib.hdfs3x_set_variant(0)
