@@ -245,7 +245,7 @@ def run_steps(work, ctx, mode, n, result, events=None, base=0, overlap=False):
             events[2 * i + 1].record()
 
 
-def batched_rate(torch, work, ctx, mode, reps=50, warm=30):
+def batched_rate(torch, work, ctx, mode, reps=100, warm=300):
     """Secondary measurement (never `value`): the same `blocks` blocks per call through the
     multi-block batch API (hdfs3_crc32c_{verify,compute}_blocks_dev*, one launch of the
     segmented wave kernel; each block keeps its own data, CRC array and (block, chunk)
@@ -260,7 +260,7 @@ def batched_rate(torch, work, ctx, mode, reps=50, warm=30):
         else:
             ctx.compute_blocks_dev(blocks, work.bpc)
 
-    # its own sustained state: `warm` calls (~5 ms) before the timed ones, so the mode measured
+    # its own sustained state: `warm` calls (~50 ms) before the timed ones, so the mode measured
     # just before (the compute block writes every word of 8 blocks) does not carry over
     for i in range(warm):
         one(0)

@@ -24,6 +24,8 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabNoHold>(a, tab, fold, grid_cap, s);
         case 77:  // diagnostic: production with the table lookups replaced by an XOR (wrong results)
             return launch_wave3<BPC, V, false, true, kLabNoMath>(a, tab, fold, grid_cap, s);
+        case 78:  // diagnostic: 77 without the slice-table LDS fill
+            return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;
         }
     }

@@ -33,6 +33,7 @@ namespace {
 constexpr int kLabEarly = 1;   // prefetch issued at the start of each step, not after its rounds landed
 constexpr int kLabNoMath = 2;  // diagnostic: table lookups replaced by an XOR of the words (wrong results)
 constexpr int kLabNoHold = 4;  // compute at bpc 512: store each round's words at once (no held stores)
+constexpr int kLabNoFill = 8;  // diagnostic: the slice tables are not written to LDS (wrong results)
 
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
 typedef __attribute__((address_space(1))) const uint8_t gcu8;
@@ -162,6 +163,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     constexpr int G = BPC / 64;
     constexpr bool kHalfFold = G <= 32;
     constexpr bool LATE = (LAB & kLabEarly) == 0, NOMATH = (LAB & kLabNoMath) != 0;
+    constexpr bool kWrong = (LAB & (kLabNoMath | kLabNoFill)) != 0;  // diagnostics: wrong CRCs
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = lane % G;
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
@@ -190,7 +192,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         const uint32_t slot0 = ((slice >> 1) << 16 | entry << 8 | (slice & 1) << 7) / 16;
         // 32 copies as 8 x b128, rotated by thread so 8 neighbouring threads hit 8 bank groups
 #pragma unroll
-        for (int r = 0; r < 8; ++r) l4[slot0 + ((r + tt) & 7)] = u32x4{tw, tw, tw, tw};
+        for (int r = 0; r < ((LAB & kLabNoFill) ? 0 : 8); ++r) l4[slot0 + ((r + tt) & 7)] = u32x4{tw, tw, tw, tw};
         if constexpr (kHalfFold) {
             reinterpret_cast<u32x4 *>(lds + kHalfFoldOff / 4)[tt] = n0;
         } else {
@@ -274,9 +276,9 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         if (k >= K || j != 0) return;
         const uint32_t c = y;
         if constexpr (VERIFY) {
-            // kLabNoMath computes wrong CRCs: compare inverted so it does not flag every chunk (an
-            // atomic per chunk would dominate the diagnostic's time)
-            if ((__builtin_bswap32(want) != c) != NOMATH)
+            // the diagnostics compute wrong CRCs: compare inverted so they do not flag every chunk
+            // (an atomic per chunk would dominate their time)
+            if ((__builtin_bswap32(want) != c) != kWrong)
                 __hip_atomic_fetch_max((gu64 *)result, ~(unsigned long long)(v.key + lane / G), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         } else {

@@ -102,6 +102,7 @@ struct hdfs3_crc_ctx {
         hdfs3crc::DevSegment *h = nullptr, *d = nullptr;
         size_t cap = 0;
         hipEvent_t done = nullptr;
+        bool armed = false;  // done recorded after a copy out of h that may still be pending
     } seg_ring[4];
     unsigned seg_next = 0;
     hdfs3crc::WordScratch words;  // dense CRC words of compute over in-packet word regions

@@ -6,6 +6,7 @@
 //
 //   hipcc -O3 --offload-arch=gfx950 -o tools/read_probe tools/read_probe.hip
 //   tools/read_probe > gpurun_out/read_probe.jsonl
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -276,6 +277,16 @@ struct Res {
 static uint8_t *g_buf;
 static uint32_t *g_sink;
 static hipStream_t g_st;
+// mode 6: launches after the first of each back-to-back batch go out without the AQL barrier bit
+// (hipExtAnyOrderLaunch, as the CRC kernels' HDFS3_LAUNCH_OVERLAP_PREVIOUS)
+static bool g_overlap = false, g_ovl_now = false;
+template <typename K, typename... A>
+static void launch_k(K k, dim3 g, dim3 b, size_t lds, A... a) {
+    if (g_ovl_now)
+        hipExtLaunchKernelGGL(k, g, b, lds, g_st, nullptr, nullptr, hipExtAnyOrderLaunch, a...);
+    else
+        hipLaunchKernelGGL(k, g, b, lds, g_st, a...);
+}
 static const uint64_t kBlk = 128ull << 20, kAll = 1ull << 30;
 
 template <typename F>
@@ -283,11 +294,18 @@ static Res measure(F launch) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int i = 0; i < 10; ++i) launch(g_buf + (i % 8) * kBlk, kBlk);
+    for (int i = 0; i < 10; ++i) {
+        g_ovl_now = g_overlap && i > 0;
+        launch(g_buf + (i % 8) * kBlk, kBlk);
+    }
     CK(hipStreamSynchronize(g_st));
     const int K = 100;
     CK(hipEventRecord(e0, g_st));
-    for (int i = 0; i < K; ++i) launch(g_buf + (i % 8) * kBlk, kBlk);
+    for (int i = 0; i < K; ++i) {
+        g_ovl_now = g_overlap && i > 0;
+        launch(g_buf + (i % 8) * kBlk, kBlk);
+    }
+    g_ovl_now = false;
     CK(hipEventRecord(e1, g_st));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -321,9 +339,9 @@ static void report(const char *kind, int grid, int block, int depth, int nt, int
 template <int U, bool NT>
 static void run_stride(int grid, int block) {
     Res r = measure([&](const uint8_t *p, uint64_t n) {
-        hipLaunchKernelGGL((k_stride<U, NT>), dim3(grid), dim3(block), 0, g_st, p, n / 16, g_sink);
+        launch_k(k_stride<U, NT>, dim3(grid), dim3(block), 0, p, n / 16, g_sink);
     });
-    report("stride", grid, block, U, NT, 0, r);
+    report(g_overlap ? "stride_ovl" : "stride", grid, block, U, NT, 0, r);
 }
 
 template <int D, bool NT, int MODE>
@@ -331,10 +349,11 @@ static void run_rounds(int grid, int block, int lds_kib) {
     CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rounds<D, NT, MODE>),
                            hipFuncAttributeMaxDynamicSharedMemorySize, lds_kib * 1024));
     Res r = measure([&](const uint8_t *p, uint64_t n) {
-        hipLaunchKernelGGL((k_rounds<D, NT, MODE>), dim3(grid), dim3(block), lds_kib * 1024, g_st, p, n, g_sink);
+        launch_k(k_rounds<D, NT, MODE>, dim3(grid), dim3(block), lds_kib * 1024, p, n, g_sink);
     });
     static const char *names[] = {"rounds_rr", "rounds_contig", "rounds_xcd", "rounds_xcdblk"};
-    report(names[MODE], grid, block, D, NT, lds_kib, r);
+    static const char *onames[] = {"rounds_rr_ovl", "rounds_contig_ovl", "rounds_xcd_ovl", "rounds_xcdblk_ovl"};
+    report(g_overlap ? onames[MODE] : names[MODE], grid, block, D, NT, lds_kib, r);
 }
 
 template <int D, int NV, int NL>
@@ -472,6 +491,21 @@ int main(int argc, char **argv) {
             run_gather<16>();
             run_gather<32>();
             run_work<2, 0, 32>(160);
+        }
+    }
+    if (only == 6) {  // co-residency: the CRC geometry (1 workgroup/CU) against 2 per CU, both launch modes
+        for (int rep = 0; rep < 3; ++rep) {
+            for (bool ov : {false, true}) {
+                g_overlap = ov;
+                run_rounds<2, true, 0>(256, 1024, 160);
+                run_rounds<2, true, 0>(256, 1024, 80);
+                run_rounds<2, true, 0>(512, 1024, 80);
+                run_rounds<2, true, 0>(512, 512, 80);
+                run_rounds<2, true, 0>(256, 1024, 0);
+                run_stride<4, true>(512, 256);
+                run_stride<4, false>(512, 256);
+            }
+            g_overlap = false;
         }
     }
     CK(hipFree(g_buf));
