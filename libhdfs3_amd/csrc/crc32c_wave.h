@@ -157,7 +157,7 @@ struct SegWalk {
 // key into *result; else store the words. SOLO (overlapped verifies): the last step runs its two
 // rounds as single chains one after the other. HOLD (compute, bpc 512): the words of 8 rounds are
 // transposed into one VGPR and up to 8 such VGPRs are stored in one burst. LAB: lab-only bits (kLab*).
-template <int BPC, bool VERIFY, bool SOLO, bool HOLD, int LAB, class Walk>
+template <int BPC, bool VERIFY, bool SOLO, bool HOLD, int LAB, int TPB, class Walk>
 __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uint32_t *__restrict__ g_tab,
                                             const uint32_t *__restrict__ g_nib, unsigned long long *result) {
     constexpr int G = BPC / 64;
@@ -169,16 +169,23 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
     const uint32_t K = walk.K;
 
-    // lean fill: one slice-table word per thread replicated 32x; for G <= 32 the half fold image
-    const uint32_t tw = g_tab[threadIdx.x];
-    u32x4 n0, n1;
-    if constexpr (kHalfFold) {
-        const uint32_t t = threadIdx.x;
-        const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
-        n0 = *reinterpret_cast<const u32x4 *>(g_nib + (fk * 16 + fe) * 64 + fc);
-    } else {
-        n0 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x);
-        n1 = *reinterpret_cast<const u32x4 *>(g_nib + 8 * threadIdx.x + 4);
+    // lean fill: each of the image's 1024 slice-table words replicated 32x (TPB threads take 1024 / TPB
+    // words each); for G <= 32 the half fold image
+    constexpr int kFillIters = 1024 / TPB;
+    static_assert(kFillIters * TPB == 1024, "TPB divides 1024");
+    uint32_t tw[kFillIters];
+    u32x4 n0[kFillIters], n1[kFillIters];
+#pragma unroll
+    for (int f = 0; f < kFillIters; ++f) {
+        const uint32_t t = threadIdx.x + f * TPB;
+        tw[f] = g_tab[t];
+        if constexpr (kHalfFold) {
+            const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
+            n0[f] = *reinterpret_cast<const u32x4 *>(g_nib + (fk * 16 + fe) * 64 + fc);
+        } else {
+            n0[f] = *reinterpret_cast<const u32x4 *>(g_nib + 8 * t);
+            n1[f] = *reinterpret_cast<const u32x4 *>(g_nib + 8 * t + 4);
+        }
     }
     WView cv0 = walk.view(0), cv1 = walk.view(1);
     __builtin_amdgcn_sched_barrier(0);
@@ -186,19 +193,21 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     load_round_buf<true>(a0, cv0.p, lane_off);
     load_round_buf<true>(a1, cv1.p, lane_off);
     __builtin_amdgcn_sched_barrier(0);
-    {
-        const uint32_t tt = threadIdx.x, slice = tt >> 8, entry = tt & 255;
+#pragma unroll
+    for (int f = 0; f < kFillIters; ++f) {
+        const uint32_t tt = threadIdx.x + f * TPB, slice = tt >> 8, entry = tt & 255;
         u32x4 *l4 = reinterpret_cast<u32x4 *>(lds);
         const uint32_t slot0 = ((slice >> 1) << 16 | entry << 8 | (slice & 1) << 7) / 16;
+        const uint32_t w = tw[f];
         // 32 copies as 8 x b128, rotated by thread so 8 neighbouring threads hit 8 bank groups
 #pragma unroll
-        for (int r = 0; r < ((LAB & kLabNoFill) ? 0 : 8); ++r) l4[slot0 + ((r + tt) & 7)] = u32x4{tw, tw, tw, tw};
+        for (int r = 0; r < ((LAB & kLabNoFill) ? 0 : 8); ++r) l4[slot0 + ((r + tt) & 7)] = u32x4{w, w, w, w};
         if constexpr (kHalfFold) {
-            reinterpret_cast<u32x4 *>(lds + kHalfFoldOff / 4)[tt] = n0;
+            reinterpret_cast<u32x4 *>(lds + kHalfFoldOff / 4)[tt] = n0[f];
         } else {
             u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * tt;
-            dst[0] = n0;
-            dst[1] = n1;
+            dst[0] = n0[f];
+            dst[1] = n1[f];
         }
     }
     lds_barrier();
@@ -399,7 +408,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
 
 // Slow region of one contiguous run: the chunks after its last whole round plus its short tail, one
 // chunk per thread of the grid (at most 8 + 1), 128-byte lines (crc_run_lines).
-template <int BPC, bool VERIFY>
+template <int BPC, bool VERIFY, int TPB = kBlockThreads>
 __device__ __forceinline__ void slow_region(const uint32_t *lds, const uint8_t *sdata, uint8_t *sw, uint64_t len,
                                             uint64_t skey, int check_short_tail, unsigned long long *result) {
     constexpr int kChunksPerUnit = kRoundBytes / BPC;
@@ -407,7 +416,7 @@ __device__ __forceinline__ void slow_region(const uint32_t *lds, const uint8_t *
     const uint64_t nfull = len / BPC;
     const uint64_t first_slow = (len / kRoundBytes) * kChunksPerUnit;
     const uint64_t nslow = nfull - first_slow + (len % BPC ? 1 : 0);
-    const uint64_t gtid = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x;
+    const uint64_t gtid = uint64_t(blockIdx.x) * TPB + threadIdx.x;
     const bool crc_al4 = (reinterpret_cast<uintptr_t>(sw) & 3u) == 0;
     if (gtid < nslow) {
         const uint64_t chunk = first_slow + gtid;
@@ -423,14 +432,15 @@ __device__ __forceinline__ void slow_region(const uint32_t *lds, const uint8_t *
 }
 
 // One block (PITCH = false) or a constant-pitch stream (PITCH = true, ChunkLaunch::pitch/npk/...).
-template <int BPC, bool VERIFY, bool PITCH, bool SOLO, int LAB = 0>
-__global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
+template <int BPC, bool VERIFY, bool PITCH, bool SOLO, int LAB = 0, int TPB = kBlockThreads>
+__global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 512 == 0, "one-round units");
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytesWave / 4];
     constexpr int kCpu = kRoundBytes / BPC;
-    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
-    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int kWpb = TPB / 64;
+    const uint64_t nwaves = uint64_t(gridDim.x) * kWpb;
+    const uint64_t wave = uint64_t(blockIdx.x) * kWpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t *words = VERIFY ? const_cast<uint8_t *>(a.crc_be) : a.out_be;
     const uint8_t *dummy = reinterpret_cast<const uint8_t *>(g_tab);
     constexpr bool kHold = !VERIFY && BPC == 512 && (LAB & kLabNoHold) == 0;
@@ -440,16 +450,16 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_wave_kernel(ChunkLaunch 
         PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves,
                           uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), a.upp_log2,
                           dummy};
-        wave_rounds<BPC, VERIFY, SOLO, kHold, LAB>(w, lds, g_tab, g_nib, a.result);
+        wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
         const uint64_t lp = a.npk - 1;
-        slow_region<BPC, VERIFY>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
+        slow_region<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
                                  a.check_short_tail, a.result);
     } else {
         const uint64_t nunits = a.len / kRoundBytes;
         BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves,
                           uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), dummy};
-        wave_rounds<BPC, VERIFY, SOLO, kHold, LAB>(w, lds, g_tab, g_nib, a.result);
-        slow_region<BPC, VERIFY>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
+        wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
+        slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     }
 }
 
@@ -467,7 +477,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunc
     SegWalk<kCpu, UNI> w{(CSegLaunch *)(&L), wave, nwaves,
                          uint32_t(rfl64(wave < L.units ? (L.units - wave + nwaves - 1) / nwaves : 0)),
                          reinterpret_cast<const uint8_t *>(g_tab)};
-    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, 0>(w, lds, g_tab, g_nib, L.result);
+    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, 0, kBlockThreads>(w, lds, g_tab, g_nib, L.result);
 
     const Lut t(lds);
     const uint64_t items = uint64_t(L.nseg) * kCpu;
@@ -508,27 +518,27 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunc
 constexpr uint64_t kSoloTailMaxBytes = uint64_t(256) << 20;
 
 // SOLO: the solo last step when the launch qualifies (above); LAB: lab A/B bits.
-template <int BPC, bool V, bool PITCH, bool SOLO, int LAB = 0>
+template <int BPC, bool V, bool PITCH, bool SOLO, int LAB = 0, int TPB = kBlockThreads>
 hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
     constexpr int G = BPC / 64;
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
     const uint32_t *nib = fold + kFoldAffineOff + set * kFoldNibbleWords;
     const uint64_t units = PITCH ? ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes : a.len / kRoundBytes;
-    const uint64_t need = (units + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock);
+    const uint64_t need = (units + 2 * (TPB / 64) - 1) / (2 * (TPB / 64));
     int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
     if (grid < 1) grid = 1;
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
         if constexpr (SOLO && !PITCH) {
             if (units * kRoundBytes <= kSoloTailMaxBytes) {
-                hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LAB>), dim3(grid),
-                                      dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+                hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LAB, TPB>), dim3(grid),
+                                      dim3(TPB), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
                 return hipGetLastError();
             }
         }
-        hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB>), dim3(grid),
-                              dim3(kBlockThreads), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+        hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB, TPB>), dim3(grid),
+                              dim3(TPB), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
     } else {
-        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB>), dim3(grid), dim3(kBlockThreads),
+        hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB, TPB>), dim3(grid), dim3(TPB),
                            0, s, a, tab, nib);
     }
     return hipGetLastError();

@@ -508,6 +508,23 @@ int main(int argc, char **argv) {
             g_overlap = false;
         }
     }
+    if (only == 7) {  // in flight per CU: waves per CU x rounds in flight, 1 workgroup per CU (160 KiB)
+        for (int rep = 0; rep < 3; ++rep) {
+            for (bool ov : {false, true}) {
+                g_overlap = ov;
+                run_rounds<1, true, 0>(256, 1024, 160);
+                run_rounds<2, true, 0>(256, 1024, 160);
+                run_rounds<2, true, 0>(256, 768, 160);
+                run_rounds<2, true, 0>(256, 512, 160);
+                run_rounds<3, true, 0>(256, 512, 160);
+                run_rounds<4, true, 0>(256, 512, 160);
+                run_rounds<2, true, 0>(256, 256, 160);
+                run_rounds<4, true, 0>(256, 256, 160);
+                run_stride<4, true>(512, 256);
+            }
+            g_overlap = false;
+        }
+    }
     CK(hipFree(g_buf));
     CK(hipFree(g_sink));
     return 0;
