@@ -24,6 +24,21 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabNoHold>(a, tab, fold, grid_cap, s);
         case 77:  // diagnostic: production with the table lookups replaced by an XOR (wrong results)
             return launch_wave3<BPC, V, false, true, kLabNoMath>(a, tab, fold, grid_cap, s);
+        case 99:    // the pitch walk over this contiguous block as ONE packet (power-of-two rounds only)
+        case 100: {  // the pitch walk over it as 8 equal packets (blocks of one 2-D tensor)
+            const uint64_t units = a.len / kRoundBytes;
+            const uint64_t npk = variant == 99 ? 1 : 8;
+            const uint64_t upp = units / npk;
+            if (a.len % kRoundBytes || units % npk || (upp & (upp - 1)) || a.chunk_base) return hipErrorInvalidValue;
+            ChunkLaunch p = a;
+            p.npk = npk;
+            p.upp_log2 = 0;
+            while ((uint64_t(1) << p.upp_log2) < upp) ++p.upp_log2;
+            p.pitch = upp * kRoundBytes;
+            p.crc_pitch = upp * (kRoundBytes / BPC) * 4;
+            p.last_len = uint32_t(upp * kRoundBytes);
+            return launch_wave3<BPC, V, true, false>(p, tab, fold, grid_cap, s);
+        }
         case 78:  // diagnostic: 77 without the slice-table LDS fill
             return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;

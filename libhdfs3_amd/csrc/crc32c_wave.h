@@ -110,6 +110,7 @@ struct SegWalk {
     uint64_t c_begin = 1, c_end = 0, c_key = 0;
     const uint8_t *c_data = nullptr;
     uint8_t *c_crc = nullptr;
+    uint32_t c_si = ~0u;  // index of the cached segment (~0: none yet)
 
     __device__ __forceinline__ CDevSegment *segp(uint32_t i) const {
         return L->seg ? (CDevSegment *)(L->seg) + i : L->inl + i;
@@ -132,7 +133,19 @@ struct SegWalk {
         if (k >= K) return WView{dummy, const_cast<uint8_t *>(dummy), 0};
         const uint64_t u = first + uint64_t(k) * stride;
         if (u < c_begin || u >= c_end) {
-            const uint32_t si = seg_of(u);
+            uint32_t si;
+            if constexpr (UNI) {
+                si = seg_of(u);
+            } else {
+                // the walk only moves forward, and with segments longer than the walk's stride it
+                // lands in the next one: try that first (one descriptor load, which the view needs
+                // anyway) before the binary search (a chain of dependent loads)
+                const uint32_t nx = c_si + 1;
+                si = nx < L->nseg && u >= rfl64(segp(nx)->unit_begin) &&
+                             u < rfl64(segp(nx)->unit_begin) + rfl64(segp(nx)->len) / kRoundBytes
+                         ? nx
+                         : seg_of(u);
+            }
             if (L->stride) {  // packets at one pitch: kernel-argument arithmetic, no descriptor loads
                 c_begin = uint64_t(si) * L->uniform;
                 c_end = c_begin + (si + 1 < L->nseg ? L->uniform : L->inl[1].len / kRoundBytes);
@@ -147,6 +160,7 @@ struct SegWalk {
                 c_crc = reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->crc)));
                 c_key = rfl64(sd->key_base);
             }
+            c_si = si;
         }
         const uint64_t r = u - c_begin;
         return WView{c_data + r * kRoundBytes, c_crc + 4 * CPU * r, c_key + CPU * r};
