@@ -4,7 +4,7 @@
 // Bit-exact variants are parity-tested (tests/test_gpu_parity.py); the diagnostic one gives
 // wrong results on purpose. The designs that lost their A/B were removed in round 3; their
 // numbers stay in DESIGN.md §5 and profiles/.
-#include "crc32c_wave.h"
+#include "crc32c_wave_n.h"
 
 namespace hdfs3crc {
 namespace {
@@ -39,6 +39,12 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             p.last_len = uint32_t(upp * kRoundBytes);
             return launch_wave3<BPC, V, true, false>(p, tab, fold, grid_cap, s);
         }
+        // round 3 (re-entry): NCH chains per step, TPB threads per workgroup (crc32c_wave_n.h)
+        case 110: return launch_wave_n<BPC, V, 4, 256>(a, tab, fold, grid_cap, s);
+        case 111: return launch_wave_n<BPC, V, 4, 512>(a, tab, fold, grid_cap, s);
+        case 112: return launch_wave_n<BPC, V, 8, 256>(a, tab, fold, grid_cap, s);
+        case 113: return launch_wave_n<BPC, V, 2, 1024>(a, tab, fold, grid_cap, s);  // control: the production geometry
+        case 114: return launch_wave_n<BPC, V, 6, 256>(a, tab, fold, grid_cap, s);
         case 78:  // diagnostic: 77 without the slice-table LDS fill
             return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;
