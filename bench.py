@@ -185,15 +185,31 @@ class Workload:
         g.manual_seed(seed)
         self.data = torch.randint(0, 256, (blocks, block_bytes), dtype=torch.uint8, device=device, generator=g)
         self.crc = torch.empty((blocks, 4 * self.nchunks), dtype=torch.uint8, device=device)
+        # device pointers resolved once: the timed loops index plain lists, not tensors (a tensor
+        # index costs the box's host several us per launch, DESIGN.md §5 "short timed regions")
+        self._dp = [self.data[b].data_ptr() for b in range(blocks)]
+        self._cp = [self.crc[b].data_ptr() for b in range(blocks)]
         for b in range(blocks):  # stored CRCs written by the GPU compute path, checked below
             ctx.compute_dev(self.data_ptr(b), block_bytes, bpc, self.crc_ptr(b))
         ctx.synchronize()
 
     def data_ptr(self, b):
-        return self.data[b].data_ptr()
+        return self._dp[b]
 
     def crc_ptr(self, b):
-        return self.crc[b].data_ptr()
+        return self._cp[b]
+
+
+def settle(torch, stream):
+    """Wait for everything queued so far with the host thread polling (it stays on its core), then
+    torch.cuda.synchronize(), which returns at once. A thread that sleeps in the synchronize wakes
+    up late on some boxes: the first launch of a 20-launch timed region then went out up to 180 us
+    after the start event (tools/launch_host_probe.py, profiles/r03/reentry/)."""
+    done = torch.cuda.Event()
+    done.record(stream)
+    while not done.query():
+        pass
+    torch.cuda.synchronize()
 
 
 def check_against_oracle(work, ctx):
@@ -229,18 +245,18 @@ def run_steps(work, ctx, mode, n, result, events=None, base=0, overlap=False):
     is a verify of this run and all blocks, CRC arrays and zeroed result words were ready
     before the run started; the first launch of a run stays barriered behind whatever the
     stream held before (the result memset, events)."""
+    rp, rn = result.data_ptr(), result.numel()
+    dp, cp, nb, bb, bpc = work._dp, work._cp, work.blocks, work.block_bytes, work.bpc
     for i in range(n):
         s = base + i
-        b = s % work.blocks
+        b = s % nb
         if events is not None:
             events[2 * i].record()
         if mode == "verify":
-            ctx.verify_dev_async(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b),
-                                 result.data_ptr() + 8 * (s % result.numel()),
+            ctx.verify_dev_async(dp[b], bb, bpc, cp[b], rp + 8 * (s % rn),
                                  overlap_previous=overlap and i > 0 and events is None)
         else:
-            ctx.compute_dev(work.data_ptr(b), work.block_bytes, work.bpc, work.crc_ptr(b),
-                            overlap_previous=overlap and i > 0 and events is None)
+            ctx.compute_dev(dp[b], bb, bpc, cp[b], overlap_previous=overlap and i > 0 and events is None)
         if events is not None:
             events[2 * i + 1].record()
 
@@ -324,18 +340,20 @@ def compute_block(torch, work, ctx, K, warm, stream, read_ceilings):
     out = torch.full_like(work.crc, 0xA5)
     alg = work.nchunks * (work.bpc + 4)  # reads C, writes 4 per chunk
 
+    op = [out[b].data_ptr() for b in range(work.blocks)]
+    dp, nb, bb, bpc = work._dp, work.blocks, work.block_bytes, work.bpc
+
     def launches(n, overlap):
         for i in range(n):
-            b = i % work.blocks
-            ctx.compute_dev(work.data_ptr(b), work.block_bytes, work.bpc, out[b].data_ptr(),
-                            overlap_previous=overlap and i > 0)
+            b = i % nb
+            ctx.compute_dev(dp[b], bb, bpc, op[b], overlap_previous=overlap and i > 0)
 
     res = {"api": "hdfs3_crc32c_compute_dev", "alg_bytes_per_launch": alg,
            "timing": "HIP events on the launch stream around K launches (the clock of value)"}
     for name, overlap in (("overlapped", True), ("barriered", False)):
         launches(warm, overlap)
         out.fill_(0xA5)
-        torch.cuda.synchronize()
+        settle(torch, stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         launches(K, overlap)
@@ -397,7 +415,36 @@ def stream_read_ceiling(torch, work, lab, reps=10, overlap=False):
         if r > best:
             best, best_grid = r, grid
     per_block = rate(best_grid, work.block_bytes, 400, lambda i: work.data_ptr(i % work.blocks), overlap)
-    return best, per_block
+    return best, per_block, best_grid
+
+
+def same_form_read(torch, work, lab, stream, grid, K, W, overlap, reps=5):
+    """The plain read in exactly the timed region's form: W warmup launches, settle (the
+    synchronize), then K launches of one block each between two HIP events, the first barriered
+    and the rest overlapped when `overlap`. Median per-launch GB/s over `reps` such regions. A short
+    region pays the start of a run from an idle GPU (a barriered first launch, the ramp of the
+    first few; profiles/r02/bench_k20_trace.jsonl) and the steady-state ceiling above does not."""
+    from libhdfs3_amd import _native
+    lib = _native.lab()
+    sink = torch.zeros(4, dtype=torch.int32, device=work.data.device)
+    dp, nb, bb = work._dp, work.blocks, work.block_bytes
+    sp = sink.data_ptr()
+
+    def launches(n):
+        for i in range(n):
+            lib.hdfs3x_stream_read_ex(lab.ctx, dp[i % nb], bb, grid, sp, int(overlap and i > 0))
+
+    rates = []
+    for _ in range(reps):
+        launches(W)
+        settle(torch, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        launches(K)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        rates.append(bb * K / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    return sorted(rates)[len(rates) // 2]
 
 
 def lane_read_rate(torch, work, lab, reps=10):
@@ -615,14 +662,14 @@ def main():
     run_steps(work, ctx, args.mode, W, result, overlap=overlap)
     graphs = StepGraphs(torch, work, ctx, args.mode, K, result, stream) if args.graph else None
     result.zero_()
-    torch.cuda.synchronize()
     # (1) timed region: W warmup steps done, now exactly K steps (graph replays, or K eager
     # launches), nothing else on the stream, bracketed by barrier + synchronize on both sides.
     # The clock of `value`: HIP events on the launch stream around the K steps (max over ranks).
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
+        settle(torch, stream)
         dist.barrier()
-    torch.cuda.synchronize()
+    settle(torch, stream)  # ends in torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
     if graphs is not None:
@@ -666,15 +713,23 @@ def main():
     if world == 1:
         try:
             lab = lab_context(work, stream)
-            whole, per_block = stream_read_ceiling(torch, work, lab, overlap=overlap)
+            whole, per_block, best_grid = stream_read_ceiling(torch, work, lab, overlap=overlap)
             roofline["achievable_read_GBps"] = round(whole, 1)
             # the same shape as the timed steps: a plain read of one block per launch, with
             # the same launch mode (overlapped or barriered)
             roofline["achievable_read_per_block_launch_GBps"] = round(per_block, 1)
             roofline["frac_of_achievable_per_block"] = round(achieved / (per_block * alg_bytes / block_bytes), 4)
+            # the same plain read in the timed region's own form (W warmup, synchronize, K launches):
+            # a short region (the driver's K = 20) starts from an idle GPU, the 400-launch ceiling
+            # above does not; both are reported, the ceiling above stays the conservative one
+            same = same_form_read(torch, work, lab, stream, best_grid, K, W, overlap)
+            roofline["achievable_read_same_form_GBps"] = round(same, 1)
+            roofline["frac_of_achievable_same_form"] = round(achieved / (same * alg_bytes / block_bytes), 4)
+            roofline["same_form"] = (f"plain read of one block per launch in the timed region's form: {W} warmup "
+                                     f"launches, synchronize, {K} timed launches (median of 5 regions)")
             ceilings = [per_block, None]
             if barriered is not None:
-                _, per_block_b = stream_read_ceiling(torch, work, lab, overlap=False)
+                _, per_block_b, _ = stream_read_ceiling(torch, work, lab, overlap=False)
                 ceilings[1] = per_block_b
                 barriered["achievable_read_per_block_launch_GBps"] = round(per_block_b, 1)
                 barriered["frac_of_achievable_per_block"] = round(

@@ -4,7 +4,7 @@
 // Bit-exact variants are parity-tested (tests/test_gpu_parity.py); the diagnostic one gives
 // wrong results on purpose. The designs that lost their A/B were removed in round 3; their
 // numbers stay in DESIGN.md §5 and profiles/.
-#include "crc32c_wave_n.h"
+#include "crc32c_wave.h"
 
 namespace hdfs3crc {
 namespace {
@@ -39,12 +39,14 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             p.last_len = uint32_t(upp * kRoundBytes);
             return launch_wave3<BPC, V, true, false>(p, tab, fold, grid_cap, s);
         }
-        // round 3 (re-entry): NCH chains per step, TPB threads per workgroup (crc32c_wave_n.h)
-        case 110: return launch_wave_n<BPC, V, 4, 256>(a, tab, fold, grid_cap, s);
-        case 111: return launch_wave_n<BPC, V, 4, 512>(a, tab, fold, grid_cap, s);
-        case 112: return launch_wave_n<BPC, V, 8, 256>(a, tab, fold, grid_cap, s);
-        case 113: return launch_wave_n<BPC, V, 2, 1024>(a, tab, fold, grid_cap, s);  // control: the production geometry
-        case 114: return launch_wave_n<BPC, V, 6, 256>(a, tab, fold, grid_cap, s);
+        case 115:  // s_setprio by rounds left at every launch size (production: waves of >= 16 rounds)
+            return launch_wave3<BPC, V, false, true, kLabPrio>(a, tab, fold, grid_cap, s);
+        case 117:  // no s_setprio at any size (production before r3y)
+            return launch_wave3<BPC, V, false, true, kLabNoPrio>(a, tab, fold, grid_cap, s);
+        case 118:  // diagnostic, compute: held words not stored (wrong results)
+            return launch_wave3<BPC, V, false, true, kLabNoStore>(a, tab, fold, grid_cap, s);
+        case 119:  // diagnostic, compute: held words stored over the wave's first round's words (wrong results)
+            return launch_wave3<BPC, V, false, true, kLabNearStore>(a, tab, fold, grid_cap, s);
         case 78:  // diagnostic: 77 without the slice-table LDS fill
             return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;

@@ -35,6 +35,10 @@ hipError_t launch_rv(const ChunkLaunch &a, bool verify, const uint32_t *tab, con
 // packet streams at a constant pitch: the production round kernel's pitch walk
 template <int BPC, bool V>
 hipError_t launch_p(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
+#if HDFS3_LAB
+    if (g_variant == 115) return launch_wave3<BPC, V, true, false, kLabPrio>(a, tab, fold, grid_cap, s);
+    if (g_variant == 117) return launch_wave3<BPC, V, true, false, kLabNoPrio>(a, tab, fold, grid_cap, s);
+#endif
     return launch_wave3<BPC, V, true, false>(a, tab, fold, grid_cap, s);
 }
 
@@ -246,6 +250,14 @@ bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc) {
 template <int BPC>
 hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *fold, int grid,
                         hipStream_t s) {
+#if HDFS3_LAB
+    if (g_variant == 115)
+        return verify ? launch_segments3<BPC, true, kLabPrio>(L, tab, fold, grid, s)
+                      : launch_segments3<BPC, false, kLabPrio>(L, tab, fold, grid, s);
+    if (g_variant == 117)
+        return verify ? launch_segments3<BPC, true, kLabNoPrio>(L, tab, fold, grid, s)
+                      : launch_segments3<BPC, false, kLabNoPrio>(L, tab, fold, grid, s);
+#endif
     return verify ? launch_segments3<BPC, true>(L, tab, fold, grid, s) : launch_segments3<BPC, false>(L, tab, fold, grid, s);
 }
 

@@ -34,6 +34,19 @@ constexpr int kLabEarly = 1;   // prefetch issued at the start of each step, not
 constexpr int kLabNoMath = 2;  // diagnostic: table lookups replaced by an XOR of the words (wrong results)
 constexpr int kLabNoHold = 4;  // compute at bpc 512: store each round's words at once (no held stores)
 constexpr int kLabNoFill = 8;  // diagnostic: the slice tables are not written to LDS (wrong results)
+constexpr int kLabPrio = 16;    // s_setprio by rounds left at every launch size (production: >= kPrioMinRounds)
+constexpr int kLabNoPrio = 32;  // no s_setprio at any launch size (the round-3 production before r3y)
+constexpr int kLabNoStore = 64;     // diagnostic, compute: the held words are not stored (wrong results)
+constexpr int kLabNearStore = 128;  // diagnostic, compute: every flush stores to the wave's first round's words
+
+// Waves with at least this many rounds set their priority by the rounds they have left (round 3):
+// the SIMD arbiter favours older waves, so with equal work a workgroup's waves end staggered and its
+// last ones run nearly alone, too few to keep the CU's share of HBM busy. With priority 3..0 by the
+// quartile of rounds left the lagging waves catch up and the workgroup drains together: 1 GiB per
+// launch 168.8 -> 162.5 us barriered, 161.9 -> 157.4 overlapped, the batch API (8 x 128 MiB) 167.1 ->
+// 161.0, compute 171.0 -> 163.8; 256 MiB -1.9 % / -1.0 %. At 128 MiB (8 rounds per wave) it costs
+// 0.2-0.7 us, so short waves keep the arbiter's order (profiles/r03/reentry/r3x_ab_*, r3y_*).
+constexpr uint32_t kPrioMinRounds = 16;
 
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
 typedef __attribute__((address_space(1))) const uint8_t gcu8;
@@ -177,7 +190,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     constexpr int G = BPC / 64;
     constexpr bool kHalfFold = G <= 32;
     constexpr bool LATE = (LAB & kLabEarly) == 0, NOMATH = (LAB & kLabNoMath) != 0;
-    constexpr bool kWrong = (LAB & (kLabNoMath | kLabNoFill)) != 0;  // diagnostics: wrong CRCs
+    constexpr bool kWrong = (LAB & (kLabNoMath | kLabNoFill)) != 0;  // diagnostics: wrong CRCs (verify)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = lane % G;
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
@@ -259,8 +272,11 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     auto flush = [&]() {
 #pragma unroll
         for (int i = 0; i < (kHold ? 8 : 0); ++i) {
-            if (uint32_t(i) < nheld) {
-                if constexpr (kAddr) {
+            // kLabNoStore keeps the words live through a compare that practically never stores
+            if (uint32_t(i) < nheld && ((LAB & kLabNoStore) == 0 || hold[i] == 0x9E3779B9u)) {
+                if constexpr ((LAB & kLabNearStore) != 0 && !kAddr) {
+                    *(gu32 *)((gu8 *)walk.view(0).w + 4 * lane) = __builtin_bswap32(hold[i]);
+                } else if constexpr (kAddr) {
                     if (hold_addr[i]) *hold_addr[i] = __builtin_bswap32(hold[i]);
                 } else {
                     const uint32_t kk = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
@@ -349,7 +365,19 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // LATE (production): the prefetch goes out once this step's rounds have landed, so at most 8 KiB
     // are in flight per wave (128 KiB per CU), not 16: more requests in flight lower the DRAM
     // efficiency. kLabEarly (lab A/B): issued at the start of the step.
+    // priority by rounds left (kPrioMinRounds); wave-uniform, so the branches are SALU
+    const bool use_prio = (LAB & kLabPrio) != 0 || ((LAB & kLabNoPrio) == 0 && K >= kPrioMinRounds);
+    auto prio = [&](uint32_t k) {
+        if (use_prio) {
+            const uint32_t left = K > k ? K - k : 0;
+            if (left * 4 > 3 * K) __builtin_amdgcn_s_setprio(3);
+            else if (left * 4 > 2 * K) __builtin_amdgcn_s_setprio(2);
+            else if (left * 4 > K) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+    };
     auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k) {
+        prio(k);
         const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
         if constexpr (!LATE) {
             load_round_buf<true>(p0, pv0.p, lane_off);
@@ -386,6 +414,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         // F even runs pairs A -> B -> A and ends in A; F odd runs one step A -> B, then pairs
         // B -> A -> B, and ends in B. Two copies of the loop; no value crosses between them.
         auto last = [&](Round &c0, Round &c1, uint32_t k) {
+            prio(k);
             const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
             __builtin_amdgcn_sched_barrier(0);
             regroup(c0);
@@ -480,7 +509,7 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
 // A list of segments (blocks of a batch, packets of a descriptor list): the core over a SegWalk,
 // then every segment's leftover chunks and short tail, one chunk per thread spread over the
 // workgroups (item i -> segment i / chunks-per-round, block i % grid).
-template <int BPC, bool VERIFY, bool UNI>
+template <int BPC, bool VERIFY, bool UNI, int LAB = 0>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunch L, const uint32_t *__restrict__ g_tab,
                                                                         const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 512 == 0, "one-round units");
@@ -491,7 +520,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunc
     SegWalk<kCpu, UNI> w{(CSegLaunch *)(&L), wave, nwaves,
                          uint32_t(rfl64(wave < L.units ? (L.units - wave + nwaves - 1) / nwaves : 0)),
                          reinterpret_cast<const uint8_t *>(g_tab)};
-    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, 0, kBlockThreads>(w, lds, g_tab, g_nib, L.result);
+    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, LAB, kBlockThreads>(w, lds, g_tab, g_nib, L.result);
 
     const Lut t(lds);
     const uint64_t items = uint64_t(L.nseg) * kCpu;
@@ -558,15 +587,17 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     return hipGetLastError();
 }
 
-template <int BPC, bool V>
+template <int BPC, bool V, int LAB = 0>
 hipError_t launch_segments3(const SegLaunch &L, const uint32_t *tab, const uint32_t *fold, int grid, hipStream_t s) {
     constexpr int G = BPC / 64;
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
     const uint32_t *nib = fold + kFoldAffineOff + set * kFoldNibbleWords;
     if (L.uniform)
-        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, true>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
+        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, true, LAB>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab,
+                           nib);
     else
-        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, false>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab, nib);
+        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, false, LAB>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab,
+                           nib);
     return hipGetLastError();
 }
 

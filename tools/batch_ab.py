@@ -15,6 +15,7 @@ def main():
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import CrcContext
 
+    extra = [int(v) for v in sys.argv[sys.argv.index("--variants") + 1].split(",")] if "--variants" in sys.argv else []
     lib = _native.lab()
     ctx = CrcContext(0, lib=lib)
     stream = torch.cuda.Stream()
@@ -58,6 +59,10 @@ def main():
         lib.hdfs3x_set_variant(54)
         samples["blocks_sliced_v54"].append(timed(cases["blocks_sliced_v0"]))
         samples["blocks_separate_v54"].append(timed(cases["blocks_separate_v0"]))
+        for v in extra:  # other lab variants over every case (pitch walk, segments, contiguous)
+            lib.hdfs3x_set_variant(v)
+            for name, fn in cases.items():
+                samples.setdefault(name.replace("_v0", "") + f"_v{v}", []).append(timed(fn))
         lib.hdfs3x_set_variant(0)
     assert int(res.item()) == 0, "clean blocks reported a bad chunk"
     for name, v in samples.items():
