@@ -423,7 +423,7 @@ __device__ __forceinline__ uint32_t group_xor(uint32_t v) {
     return v;
 }
 
-template <int BPC, bool VERIFY, int DEPTH, bool FOLD4>
+template <int BPC, bool VERIFY, int DEPTH, bool FOLD4, bool PRIO = false>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_rounds_kernel(ChunkLaunch a,
                                                                       const uint32_t *__restrict__ g_tab,
                                                                       const uint32_t *__restrict__ g_fold) {
@@ -513,6 +513,19 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_rounds_kernel(ChunkLaunc
             }
         }
     };
+    // PRIO (lab 115): s_setprio by the quartile of rounds left for waves of >= 16 rounds, as the round
+    // kernel does (crc32c_wave.h, kPrioMinRounds). Measured 1-2 us per GiB SLOWER here at bpc 8192 and
+    // 65536 (profiles/r03/reentry/r3za_r8k_*.jsonl), so production leaves the arbiter's order.
+    const bool use_prio = PRIO && K >= 16;
+    auto prio = [&](uint64_t k) {
+        if (use_prio && (k & 3) == 0) {
+            const uint64_t left = K - k;
+            if (left * 4 > 3 * K) __builtin_amdgcn_s_setprio(3);
+            else if (left * 4 > 2 * K) __builtin_amdgcn_s_setprio(2);
+            else if (left * 4 > K) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+    };
     // (DEPTH+1)-buffer ring unrolled so the buffers rotate by renaming (a loop-carried
     // register copy would make the compiler wait for the youngest prefetch)
     if constexpr (DEPTH == 2) {
@@ -525,6 +538,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_rounds_kernel(ChunkLaunc
         }
     } else {
         for (uint64_t k = 0; k < K; k += 2) {
+            prio(k);
             step(b0, b1, k);
             if (k + 1 >= K) break;
             step(b1, b0, k + 1);
@@ -636,6 +650,7 @@ struct SegLaunch {
     // key i << 32}, the last one with inl[1].len (uniform view only). Packets laid out at a
     // constant pitch in one arena need no descriptor array at all.
     uint64_t stride;
+    uint32_t kq, kr;  // a wave's round count: kq + (wave < kr), split on the host (launch_segments)
     DevSegment inl[kInlineSegments];
 };
 
@@ -766,14 +781,14 @@ hipError_t launch_t(const ChunkLaunch &a, const uint32_t *tab, int grid, hipStre
     return hipGetLastError();
 }
 
-template <int BPC, bool V, int DEPTH, bool FOLD4>
+template <int BPC, bool V, int DEPTH, bool FOLD4, bool PRIO = false>
 hipError_t launch_r3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                      hipStream_t s) {
     constexpr uint64_t kUnit = BPC <= kRoundBytes ? kRoundBytes : BPC;
     const uint64_t units = a.len / kUnit;
     const uint64_t need = (units + kWavesPerBlock - 1) / kWavesPerBlock;
     const int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
-    hipLaunchKernelGGL((crc32c_rounds_kernel<BPC, V, DEPTH, FOLD4>), dim3(grid), dim3(kBlockThreads), 0, s,
+    hipLaunchKernelGGL((crc32c_rounds_kernel<BPC, V, DEPTH, FOLD4, PRIO>), dim3(grid), dim3(kBlockThreads), 0, s,
                        a, tab, fold);
     return hipGetLastError();
 }

@@ -12,6 +12,9 @@ namespace {
 template <int BPC, bool V>
 hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                       hipStream_t s) {
+    if constexpr (BPC > kRoundBytes) {
+        if (variant == 115) return launch_r3<BPC, V, 1, true, true>(a, tab, fold, grid_cap, s);  // s_setprio
+    }
     if constexpr (BPC <= kRoundBytes) {
         switch (variant) {
         case 92:  // production with the prefetch issued at the start of each step (early)
@@ -47,6 +50,8 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabNoStore>(a, tab, fold, grid_cap, s);
         case 119:  // diagnostic, compute: held words stored over the wave's first round's words (wrong results)
             return launch_wave3<BPC, V, false, true, kLabNearStore>(a, tab, fold, grid_cap, s);
+        case 120:  // compute: the workgroup's waves meet at a barrier before their last flush
+            return launch_wave3<BPC, V, false, true, kLabBarFlush>(a, tab, fold, grid_cap, s);
         case 78:  // diagnostic: 77 without the slice-table LDS fill
             return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;

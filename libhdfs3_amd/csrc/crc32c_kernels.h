@@ -33,6 +33,9 @@ struct ChunkLaunch {
     // pitch mode over independent blocks at constant strides (a [blocks, bytes] tensor and its
     // [blocks, words] tensor): the words' own pitch; 0 = `pitch` (the wire layout of packets)
     uint64_t crc_pitch = 0;
+    // Round kernel (launch_wave3 fills these): a wave's round count is kq + (wave < kr), the units of
+    // the launch split over its waves on the host, so no wave divides 64-bit values in its prologue.
+    uint32_t kq = 0, kr = 0;
 };
 
 // Packet-descriptor as seen by the device (mirrors hdfs3_pkt_desc).

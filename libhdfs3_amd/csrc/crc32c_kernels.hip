@@ -289,6 +289,10 @@ hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t unit
     uint64_t g = need > slow_need ? need : slow_need;
     g = g < uint64_t(grid_cap) ? g : uint64_t(grid_cap);
     const int grid = int(g > 0 ? g : 1);
+    const uint64_t nwaves = uint64_t(grid) * kWavesPerBlock;
+    if (units / nwaves >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
+    L.kq = uint32_t(units / nwaves);
+    L.kr = uint32_t(units % nwaves);
     switch (bpc) {
     case 512: return launch_seg_t<512>(L, verify, d_tables, d_fold, grid, stream);
     case 1024: return launch_seg_t<1024>(L, verify, d_tables, d_fold, grid, stream);

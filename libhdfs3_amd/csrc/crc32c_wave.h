@@ -38,6 +38,7 @@ constexpr int kLabPrio = 16;    // s_setprio by rounds left at every launch size
 constexpr int kLabNoPrio = 32;  // no s_setprio at any launch size (the round-3 production before r3y)
 constexpr int kLabNoStore = 64;     // diagnostic, compute: the held words are not stored (wrong results)
 constexpr int kLabNearStore = 128;  // diagnostic, compute: every flush stores to the wave's first round's words
+constexpr int kLabBarFlush = 256;   // compute: the workgroup's waves meet at an s_barrier before their last flush
 
 // Waves with at least this many rounds set their priority by the rounds they have left (round 3):
 // the SIMD arbiter favours older waves, so with equal work a workgroup's waves end staggered and its
@@ -223,12 +224,14 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
 #pragma unroll
     for (int f = 0; f < kFillIters; ++f) {
         const uint32_t tt = threadIdx.x + f * TPB, slice = tt >> 8, entry = tt & 255;
-        u32x4 *l4 = reinterpret_cast<u32x4 *>(lds);
         const uint32_t slot0 = ((slice >> 1) << 16 | entry << 8 | (slice & 1) << 7) / 16;
         const uint32_t w = tw[f];
-        // 32 copies as 8 x b128, rotated by thread so 8 neighbouring threads hit 8 bank groups
+        // 32 copies as 8 x b128, permuted by thread (slot r ^ (tt & 7)) so 8 neighbouring threads hit
+        // 8 bank groups; the xor form costs one VALU per store
+        const uint32_t byte_t = (slot0 | (tt & 7)) << 4;
 #pragma unroll
-        for (int r = 0; r < ((LAB & kLabNoFill) ? 0 : 8); ++r) l4[slot0 + ((r + tt) & 7)] = u32x4{w, w, w, w};
+        for (int r = 0; r < ((LAB & kLabNoFill) ? 0 : 8); ++r)
+            *reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + (byte_t ^ uint32_t(16 * r))) = u32x4{w, w, w, w};
         if constexpr (kHalfFold) {
             reinterpret_cast<u32x4 *>(lds + kHalfFoldOff / 4)[tt] = n0[f];
         } else {
@@ -446,7 +449,12 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             step(b0, b1, a0, a1, k + 2);
         }
     }
-    if constexpr (kHold) flush();
+    if constexpr (kHold) {
+        // kLabBarFlush: every wave of the workgroup reaches this point (each runs wave_rounds to its
+        // end), so the 4 partial 32-B writes of each 128-B word line leave at the same moment
+        if constexpr ((LAB & kLabBarFlush) != 0) __builtin_amdgcn_s_barrier();
+        flush();
+    }
 }
 
 // Slow region of one contiguous run: the chunks after its last whole round plus its short tail, one
@@ -487,22 +495,21 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
     uint8_t *words = VERIFY ? const_cast<uint8_t *>(a.crc_be) : a.out_be;
     const uint8_t *dummy = reinterpret_cast<const uint8_t *>(g_tab);
     constexpr bool kHold = !VERIFY && BPC == 512 && (LAB & kLabNoHold) == 0;
+    // the wave's round count from the host's split (ChunkLaunch::kq/kr): SALU only
+    const uint32_t K = a.kq + (wave < a.kr ? 1u : 0u);
     if constexpr (PITCH) {
-        const uint64_t nunits = ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes;
-        // the division runs in VALU; readfirstlane puts K back in SGPRs so every k < K below is SALU
-        PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves,
-                          uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), a.upp_log2,
+        PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves, K, a.upp_log2,
                           dummy};
         wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
         const uint64_t lp = a.npk - 1;
-        slow_region<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
-                                 a.check_short_tail, a.result);
+        if (a.last_len % kRoundBytes)  // wave-uniform: a stream of whole rounds has no slow region
+            slow_region<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
+                                     a.check_short_tail, a.result);
     } else {
-        const uint64_t nunits = a.len / kRoundBytes;
-        BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves,
-                          uint32_t(rfl64(wave < nunits ? (nunits - wave + nwaves - 1) / nwaves : 0)), dummy};
+        BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, K, dummy};
         wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
-        slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
+        if (a.len % kRoundBytes)  // wave-uniform: a block of whole rounds has no slow region
+            slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     }
 }
 
@@ -517,8 +524,7 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunc
     constexpr int kCpu = kRoundBytes / BPC;
     const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
     const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    SegWalk<kCpu, UNI> w{(CSegLaunch *)(&L), wave, nwaves,
-                         uint32_t(rfl64(wave < L.units ? (L.units - wave + nwaves - 1) / nwaves : 0)),
+    SegWalk<kCpu, UNI> w{(CSegLaunch *)(&L), wave, nwaves, L.kq + (wave < L.kr ? 1u : 0u),
                          reinterpret_cast<const uint8_t *>(g_tab)};
     wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, LAB, kBlockThreads>(w, lds, g_tab, g_nib, L.result);
 
@@ -570,19 +576,26 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     const uint64_t need = (units + 2 * (TPB / 64) - 1) / (2 * (TPB / 64));
     int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
     if (grid < 1) grid = 1;
+    // units over the grid's waves: wave w takes kq rounds, plus one when w < kr (32-bit round counts:
+    // 16 TiB per launch; ChunkLaunch::kq/kr)
+    const uint64_t nwaves = uint64_t(grid) * (TPB / 64);
+    if (units / nwaves >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
+    ChunkLaunch b = a;
+    b.kq = uint32_t(units / nwaves);
+    b.kr = uint32_t(units % nwaves);
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
         if constexpr (SOLO && !PITCH) {
             if (units * kRoundBytes <= kSoloTailMaxBytes) {
                 hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LAB, TPB>), dim3(grid),
-                                      dim3(TPB), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+                                      dim3(TPB), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, b, tab, nib);
                 return hipGetLastError();
             }
         }
         hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB, TPB>), dim3(grid),
-                              dim3(TPB), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, a, tab, nib);
+                              dim3(TPB), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, b, tab, nib);
     } else {
         hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB, TPB>), dim3(grid), dim3(TPB),
-                           0, s, a, tab, nib);
+                           0, s, b, tab, nib);
     }
     return hipGetLastError();
 }

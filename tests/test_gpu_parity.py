@@ -258,7 +258,8 @@ def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
 # every bit-exact variant (the diagnostic variant 77 gives wrong results on purpose); the lab
 # variants exist for the round kernel's chunk sizes only
 @pytest.mark.parametrize("variant,bpc", [(0, b) for b in (512, 1024, 2048, 4096, 8192)] +
-                         [(v, b) for v in (92, 93, 94, 95, 115, 117) for b in (512, 1024, 2048, 4096)])
+                         [(v, b) for v in (92, 93, 94, 95, 115, 117) for b in (512, 1024, 2048, 4096)] +
+                         [(115, 8192), (120, 512), (120, 2048)])
 def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
     """All kernel designs kept for A/B (hdfs3x_set_variant) are parity-checked too:
     whole rounds, the slow region (len not a multiple of the 4 KiB round) and the tail."""
@@ -494,7 +495,7 @@ def test_host_api_random_sizes_and_offsets(gpu_ctx):
         assert gpu_ctx.verify(bad, bpc, want, True) == pos // bpc, (n, off, bpc, pos)
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95, 120])
 @pytest.mark.parametrize("bpc", [512, 4096])
 def test_round_kernel_variants_overlapped_compute_match_oracle(lab_ctx, variant, bpc):
     """Compute-mode variants of the round kernel (held stores or not, solo last step or not) as
