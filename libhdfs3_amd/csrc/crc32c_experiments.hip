@@ -50,8 +50,8 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabNoStore>(a, tab, fold, grid_cap, s);
         case 119:  // diagnostic, compute: held words stored over the wave's first round's words (wrong results)
             return launch_wave3<BPC, V, false, true, kLabNearStore>(a, tab, fold, grid_cap, s);
-        case 120:  // compute: the workgroup's waves meet at a barrier before their last flush
-            return launch_wave3<BPC, V, false, true, kLabBarFlush>(a, tab, fold, grid_cap, s);
+        case 122:  // compute: held stores where production stages the words in LDS (before r3zb)
+            return launch_wave3<BPC, V, false, true, kLabNoStage>(a, tab, fold, grid_cap, s);
         case 78:  // diagnostic: 77 without the slice-table LDS fill
             return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;

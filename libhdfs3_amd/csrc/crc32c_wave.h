@@ -38,7 +38,11 @@ constexpr int kLabPrio = 16;    // s_setprio by rounds left at every launch size
 constexpr int kLabNoPrio = 32;  // no s_setprio at any launch size (the round-3 production before r3y)
 constexpr int kLabNoStore = 64;     // diagnostic, compute: the held words are not stored (wrong results)
 constexpr int kLabNearStore = 128;  // diagnostic, compute: every flush stores to the wave's first round's words
-constexpr int kLabBarFlush = 256;   // compute: the workgroup's waves meet at an s_barrier before their last flush
+constexpr int kLabNoStage = 1024;   // compute: held stores even where production stages the words (kStageWords)
+// Not a lab bit: launch_wave3 sets it for compute at bpc 512 over a contiguous block whose waves have
+// at most kStageMaxRounds rounds (the words are staged in LDS and written as whole lines, §4.1)
+constexpr int kStageWords = 512;
+constexpr uint32_t kStageMaxRounds = 32;  // 16 waves x 32 rounds x 32 B = the 16 KiB the half fold image leaves
 
 // Waves with at least this many rounds set their priority by the rounds they have left (round 3):
 // the SIMD arbiter favours older waves, so with equal work a workgroup's waves end staggered and its
@@ -71,11 +75,13 @@ struct WView {
 template <int CPU>
 struct BlockWalk {
     static constexpr bool kLaneView = true;
+    static constexpr bool kContiguous = true;  // unit u's words at words + 4 * CPU * u
     const uint8_t *data;
     uint8_t *words;
     uint64_t key0, first, stride;
     uint32_t K;            // rounds of this wave (< 2^32: 16 TiB per launch); 32-bit so k < K is SALU
     const uint8_t *dummy;  // the cache-resident 4 KiB table image: reads past the wave's last round
+    uint32_t kq = 0, kr = 0;  // the launch's round split (ChunkLaunch::kq/kr): any wave's K
     __device__ __forceinline__ WView view(uint32_t k) const {
         const uint64_t u = first + uint64_t(k) * stride;
         const bool in = k < K;
@@ -90,6 +96,7 @@ struct BlockWalk {
 template <int CPU>
 struct PitchWalk {
     static constexpr bool kLaneView = true;
+    static constexpr bool kContiguous = false;
     const uint8_t *data;
     uint8_t *words;
     uint64_t dpitch, wpitch, first, stride;
@@ -113,6 +120,7 @@ struct PitchWalk {
 template <int CPU, bool UNI>
 struct SegWalk {
     static constexpr bool kLaneView = false;
+    static constexpr bool kContiguous = false;
     // The launch record and the descriptors through the CONSTANT address space: their fields are
     // wave-uniform, so they load with s_load (lgkmcnt). Through a generic pointer they compiled to
     // FLAT loads, which count on vmcnt as well, and every segment crossing then waited for the whole
@@ -291,7 +299,21 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         nheld = 0;
     };
     // y: the chunk's finished CRC (the affine fold image carries init and final xor)
+    // kStageWords (compute at bpc 512 over a contiguous block, at most kStageMaxRounds rounds per wave):
+    // every word waits in the LDS the half fold image leaves free (16 KiB: slot s's round k at word
+    // (k * 16 + s) * 8 + c) and the workgroup writes them at its end as whole 512-B runs, since the 16
+    // waves' k-th rounds are 16 consecutive units. The held stores send each wave's words as 32-B
+    // pieces of lines that three other waves complete later, into a saturated read stream: 0.4 us of
+    // the 1.1 us those writes cost an overlapped 128 MiB launch (profiles/r03/reentry/r3zb_c128_*).
+    constexpr bool kStage = kHold && (LAB & kStageWords) != 0 && Walk::kContiguous && kHalfFold && TPB == 1024;
+    static_assert(!kStage || G == 8, "staging holds 8 words per round");
+    uint32_t *stage = lds + kLdsBytesWave / 4 - 4096;
+    const uint32_t slot = threadIdx.x >> 6;
     auto finish = [&](uint32_t k, const WView &v, uint32_t y, uint32_t want) {
+        if constexpr (kStage) {
+            if (k < K && j == 0) stage[(k * 16 + slot) * 8 + lane / G] = y;
+            return;
+        }
         if constexpr (kHold) {
             if (k >= K) return;
             const uint32_t r = k & 7;
@@ -449,10 +471,18 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             step(b0, b1, a0, a1, k + 2);
         }
     }
-    if constexpr (kHold) {
-        // kLabBarFlush: every wave of the workgroup reaches this point (each runs wave_rounds to its
-        // end), so the 4 partial 32-B writes of each 128-B word line leave at the same moment
-        if constexpr ((LAB & kLabBarFlush) != 0) __builtin_amdgcn_s_barrier();
+    if constexpr (kStage) {
+        lds_barrier();  // every wave of the workgroup runs wave_rounds to its end
+        const uint64_t wg_first = walk.first - slot;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const uint32_t t = threadIdx.x + 1024 * p, k = t >> 7, s = (t >> 3) & 15, c = t & 7;
+            const uint32_t ks = walk.kq + (wg_first + s < walk.kr ? 1u : 0u);
+            if (k < ks)
+                *(gu32 *)((gu8 *)walk.words + 4 * (kRoundBytes / BPC) * (wg_first + s + uint64_t(k) * walk.stride) + 4 * c) =
+                    __builtin_bswap32(stage[t]);
+        }
+    } else if constexpr (kHold) {
         flush();
     }
 }
@@ -506,7 +536,7 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
             slow_region<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
                                      a.check_short_tail, a.result);
     } else {
-        BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, K, dummy};
+        BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, K, dummy, a.kq, a.kr};
         wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
         if (a.len % kRoundBytes)  // wave-uniform: a block of whole rounds has no slow region
             slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
@@ -583,6 +613,11 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     ChunkLaunch b = a;
     b.kq = uint32_t(units / nwaves);
     b.kr = uint32_t(units % nwaves);
+    // compute at bpc 512 over one contiguous block with few enough rounds per wave: staged words
+    if constexpr (!V && BPC == 512 && !PITCH && TPB == 1024 && (LAB & (kStageWords | kLabNoStage)) == 0) {
+        if (b.kq + (b.kr ? 1u : 0u) <= kStageMaxRounds)
+            return launch_wave3<BPC, V, PITCH, SOLO, LAB | kStageWords, TPB>(a, tab, fold, grid_cap, s);
+    }
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
         if constexpr (SOLO && !PITCH) {
             if (units * kRoundBytes <= kSoloTailMaxBytes) {

@@ -219,6 +219,31 @@ def test_compute_held_stores_past_64_rounds_per_wave(gpu_ctx, n):
     assert np.array_equal(gpu_ctx.download(dc, 4 * nc), oracle_compute(data, bpc))
 
 
+@pytest.mark.parametrize("n", [128 << 20, (512 << 20), (512 << 20) + 4096, (128 << 20) + 4096 * 3 + 517,
+                               4096 * 4096 * 7 + 4096 * 5, 4096 * 33 + 100])
+@pytest.mark.parametrize("overlap", [False, True])
+def test_compute_staged_words_boundaries(gpu_ctx, n, overlap):
+    """Compute at bpc 512 over a contiguous block whose waves have at most 32 rounds stages every
+    word in LDS and writes them as whole lines when the workgroup ends (kStageWords, crc32c_wave.h).
+    Sizes at exactly 32 rounds per wave (512 MiB), one round past it (held stores), waves with
+    unequal round counts, a slow region and short tail, and a small grid: every word against the
+    oracle, words poisoned first, barriered and overlapped (the solo last step)."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    bpc = 512
+    data = splitmix_bytes(n, 0x57A6E + n)
+    d = gpu_ctx.upload(data)
+    nc = (n + bpc - 1) // bpc
+    dc = gpu_ctx.upload(np.full(4 * nc + 64, 0xA5, dtype=np.uint8))
+    if overlap:  # the previous op on the stream is a compute whose inputs were ready (the ABI contract)
+        other = DeviceBuffer(4 * nc)
+        gpu_ctx.compute_dev(d.ptr, n, bpc, other.ptr)
+    gpu_ctx.compute_dev(d.ptr, n, bpc, dc.ptr, overlap_previous=overlap)
+    got = gpu_ctx.download(dc, 4 * nc + 64)
+    assert np.array_equal(got[:4 * nc], oracle_compute(data, bpc))
+    assert np.all(got[4 * nc:] == 0xA5)
+
+
 def test_block_128mib_async_result_and_launch_count(gpu_ctx):
     """Config 2: one 128 MiB block, 512 B chunks, device-resident async verify."""
     from libhdfs3_amd.engine import DeviceBuffer
@@ -259,7 +284,7 @@ def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
 # variants exist for the round kernel's chunk sizes only
 @pytest.mark.parametrize("variant,bpc", [(0, b) for b in (512, 1024, 2048, 4096, 8192)] +
                          [(v, b) for v in (92, 93, 94, 95, 115, 117) for b in (512, 1024, 2048, 4096)] +
-                         [(115, 8192), (120, 512), (120, 2048)])
+                         [(115, 8192), (122, 512), (122, 2048)])
 def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
     """All kernel designs kept for A/B (hdfs3x_set_variant) are parity-checked too:
     whole rounds, the slow region (len not a multiple of the 4 KiB round) and the tail."""
@@ -495,7 +520,7 @@ def test_host_api_random_sizes_and_offsets(gpu_ctx):
         assert gpu_ctx.verify(bad, bpc, want, True) == pos // bpc, (n, off, bpc, pos)
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95, 120])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95, 122])
 @pytest.mark.parametrize("bpc", [512, 4096])
 def test_round_kernel_variants_overlapped_compute_match_oracle(lab_ctx, variant, bpc):
     """Compute-mode variants of the round kernel (held stores or not, solo last step or not) as
