@@ -370,6 +370,7 @@ def compute_block(torch, work, ctx, K, warm, stream, read_ceilings):
         ceil = read_ceilings[0 if overlap else 1] if read_ceilings else None
         if ceil:
             r["frac_of_achievable_per_block"] = round(alg / t / 1e9 / (ceil * alg / work.block_bytes), 4)
+        r["paired"] = paired_regions(torch, work, ctx, stream, max(K, 200), overlap, sp)
         res[name] = r
     # every word the timed launches wrote (the last K launches covered all blocks when K >= blocks)
     host = out.cpu().numpy()
@@ -380,6 +381,42 @@ def compute_block(torch, work, ctx, K, warm, stream, read_ceilings):
             raise SystemExit(f"PARITY FAILURE: compute block {b} chunk {bad} differs from the oracle")
     res["checked"] = f"every CRC word of {min(K, work.blocks)} blocks against the oracle after the timed region"
     return res
+
+
+def paired_regions(torch, work, ctx, stream, n, overlap, dst, reps=3):
+    """Compute against verify in identical timed regions: per rep, a verify region then a compute
+    region, each 50 warmup launches, settle, n timed launches (first barriered, the rest overlapped
+    when `overlap`); medians of the per-launch times. Two 20-launch regions timed minutes apart on
+    a box differ by up to 12 % (the driver's form); a ratio of paired regions does not
+    carry that."""
+    res = torch.zeros(256, dtype=torch.int64, device=work.data.device)
+    rp, dp, cp, nb, bb, bpc = res.data_ptr(), work._dp, work._cp, work.blocks, work.block_bytes, work.bpc
+
+    def region(fn):
+        for i in range(50):
+            fn(i, i % 256)
+        settle(torch, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(n):
+            fn(i, i % 256)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / n
+
+    ver = lambda i, s: ctx.verify_dev_async(dp[i % nb], bb, bpc, cp[i % nb], rp + 8 * s,
+                                            overlap_previous=overlap and i > 0)
+    cmp_ = lambda i, s: ctx.compute_dev(dp[i % nb], bb, bpc, dst[i % nb], overlap_previous=overlap and i > 0)
+    v, c = [], []
+    for _ in range(reps):
+        v.append(region(ver))
+        c.append(region(cmp_))
+    if bool((res != 0).any().item()):
+        raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the paired verify regions")
+    vm, cm = sorted(v)[reps // 2], sorted(c)[reps // 2]
+    return {"launches": n, "verify_us": round(vm, 2), "compute_us": round(cm, 2),
+            "compute_vs_verify": round(vm / cm, 4),
+            "how": f"{reps} x (verify region, compute region), 50 warmup + settle + {n} timed launches each; medians"}
 
 
 def lab_context(work, stream):
