@@ -23,8 +23,9 @@
  * bpc is any positive byte count, as readers accept any bytesPerChecksum > 0 from a
  * datanode (RemoteBlockReader.cpp:150-156) or a .meta header (LocalBlockReader.cpp:110-115);
  * the reference requires a multiple of 512 only for writes (SessionConfig.cpp:112).
- * bpc in {512, 1024, 2048, 4096} on 16-byte aligned data takes the coalesced round kernels;
- * every other size is verified byte-exactly by the chunk-per-lane kernel.
+ * bpc in {512, 1024, 2048, 4096} on 16-byte aligned data takes the coalesced round kernels, and
+ * so do larger multiples of 4096 on the contiguous-block calls (the 4096-byte pieces' CRCs, then a
+ * combine kernel); every other size is verified byte-exactly by the chunk-per-lane kernel.
  *
  * Threading: one ctx per stream/thread, like one Checksum instance per reader or
  * writer in the reference. Distinct contexts share nothing but the device.

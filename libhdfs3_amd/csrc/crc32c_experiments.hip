@@ -14,6 +14,7 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
                       hipStream_t s) {
     if constexpr (BPC > kRoundBytes) {
         if (variant == 115) return launch_r3<BPC, V, 1, true, true>(a, tab, fold, grid_cap, s);  // s_setprio
+        if (variant == 123) return launch_r3<BPC, V, 1, true>(a, tab, fold, grid_cap, s);  // multi-round kernel
     }
     if constexpr (BPC <= kRoundBytes) {
         switch (variant) {
@@ -50,6 +51,8 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabNoStore>(a, tab, fold, grid_cap, s);
         case 119:  // diagnostic, compute: held words stored over the wave's first round's words (wrong results)
             return launch_wave3<BPC, V, false, true, kLabNearStore>(a, tab, fold, grid_cap, s);
+        case 123:  // (chunks above 4 KiB take the multi-round kernel; this size is production)
+            return launch_wave3<BPC, V, false, true>(a, tab, fold, grid_cap, s);
         case 122:  // compute: held stores where production stages the words in LDS (before r3zb)
             return launch_wave3<BPC, V, false, true, kLabNoStage>(a, tab, fold, grid_cap, s);
         case 78:  // diagnostic: 77 without the slice-table LDS fill

@@ -110,8 +110,21 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
                                hipStream_t stream, uint64_t arena_len = 0, size_t *bad_index = nullptr,
                                bool overlap_previous = false, WordScratch *ws = nullptr);
 
+// Chunks of R * 4096 bytes (R >= 2; 8 KiB ... 64 KiB and any other multiple of 4096): the round
+// kernel computes the CRC of every 4096-byte piece into a ctx-owned scratch (two buffers used in
+// turn, so a launch that overlaps its predecessor never writes the words that predecessor's combine
+// still reads), then a combine kernel folds each chunk's R piece CRCs (launch_chunks, pieces != null).
+struct PieceScratch {
+    uint8_t *d[2] = {nullptr, nullptr};
+    uint64_t cap[2] = {0, 0};
+    hipEvent_t used[2] = {nullptr, nullptr};  // recorded after the combine that read buffer i
+    unsigned next = 0;
+    void release();
+};
+
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
-                         const uint32_t *d_fold, int grid_cap, hipStream_t stream);
+                         const uint32_t *d_fold, int grid_cap, hipStream_t stream,
+                         PieceScratch *pieces = nullptr);
 
 hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_t n,
                           uint32_t bpc, bool verify, int check_short_tail,

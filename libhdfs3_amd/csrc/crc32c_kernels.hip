@@ -183,13 +183,123 @@ hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_
     return launch_stream_kernel(a, verify, d_tables, d_fold, grid_cap, stream);
 }
 
+constexpr uint64_t kPiecesMinBytes = uint64_t(256) << 20;
+
+void PieceScratch::release() {
+    for (int i = 0; i < 2; ++i) {
+        if (d[i]) (void)hipFree(d[i]);
+        if (used[i]) (void)hipEventDestroy(used[i]);
+    }
+    *this = PieceScratch();
+}
+
+namespace {
+
+// Chunk c of R 4096-byte pieces from the pieces' CRCs y_i (standard init and final xor, BE words in
+// `piece_be`): with A = the 4096-zero-byte advance (d_fold + kFoldAdvance4096) and crc0 the raw
+// (init 0, no final xor) CRC, crc0(P_i) = y_i ^ K, K = A(~0) ^ ~0, and the chunk's state from init ~0
+// is s = A(... A(A(~0) ^ crc0(P_0)) ...) ^ crc0(P_{R-1}); its CRC is ~s. One chunk per thread.
+template <bool VERIFY>
+__global__ __launch_bounds__(256) void crc32c_combine_pieces_kernel(const uint8_t *__restrict__ piece_be, uint64_t nchunks,
+                                                                    uint32_t R, const uint32_t *__restrict__ g_fold,
+                                                                    const uint8_t *crc_be, uint8_t *out_be,
+                                                                    uint64_t chunk_base,
+                                                                    unsigned long long *result) {
+    uint32_t col[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) col[i] = g_fold[kFoldAdvance4096 + i];
+    const uint32_t K = gf2_apply4(col, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+    const uint32_t *y = reinterpret_cast<const uint32_t *>(piece_be);
+    for (uint64_t c = uint64_t(blockIdx.x) * 256 + threadIdx.x; c < nchunks; c += uint64_t(gridDim.x) * 256) {
+        uint32_t st = 0xFFFFFFFFu;
+        for (uint32_t i = 0; i < R; ++i) st = gf2_apply4(col, st) ^ __builtin_bswap32(y[c * R + i]) ^ K;
+        const uint32_t v = ~st;
+        if constexpr (VERIFY) {
+            if (__builtin_bswap32(reinterpret_cast<const uint32_t *>(crc_be)[c]) != v)
+                atomicMax(result, ~(unsigned long long)(chunk_base + c));
+        } else {
+            reinterpret_cast<uint32_t *>(out_be)[c] = __builtin_bswap32(v);
+        }
+    }
+}
+
+// Whole chunks of R = bpc / 4096 pieces: the round kernel's compute at bpc 4096 into the scratch,
+// then the combine. The short tail chunk (if any) goes to the chunk-per-lane kernel.
+hipError_t launch_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
+                         int grid_cap, hipStream_t stream, PieceScratch *ps) {
+    const uint32_t R = a.bpc / kRoundBytes;
+    const uint64_t nfull = a.len / a.bpc;
+    const unsigned b = ps->next & 1u;
+    const uint64_t need = nfull * R * 4;
+    if (need > ps->cap[b]) {
+        if (ps->used[b]) {  // the buffer may still be read by a combine in flight
+            hipError_t e = hipEventSynchronize(ps->used[b]);
+            if (e != hipSuccess) return e;
+        }
+        if (ps->d[b]) (void)hipFree(ps->d[b]);
+        ps->d[b] = nullptr;
+        ps->cap[b] = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void **>(&ps->d[b]), need);
+        if (e != hipSuccess) return e;
+        ps->cap[b] = need;
+    }
+    if (!ps->used[b]) {
+        hipError_t e = hipEventCreateWithFlags(&ps->used[b], hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    ps->next = b + 1;
+    ChunkLaunch p = a;  // the pieces: a compute at bpc 4096 over the whole chunks
+    p.len = nfull * a.bpc;
+    p.bpc = kRoundBytes;
+    p.out_be = ps->d[b];
+    p.crc_be = nullptr;
+    p.chunk_base = 0;
+    hipError_t e = launch_wave3<kRoundBytes, false, false, true>(p, d_tables, d_fold, grid_cap, stream);
+    if (e != hipSuccess) return e;
+    const uint64_t blocks = (nfull + 255) / 256;
+    const int grid = int(blocks < 1024 ? blocks : 1024);
+    if (verify)
+        hipLaunchKernelGGL(crc32c_combine_pieces_kernel<true>, dim3(grid), dim3(256), 0, stream, ps->d[b], nfull, R,
+                           d_fold, a.crc_be, nullptr, a.chunk_base, a.result);
+    else
+        hipLaunchKernelGGL(crc32c_combine_pieces_kernel<false>, dim3(grid), dim3(256), 0, stream, ps->d[b], nfull, R,
+                           d_fold, nullptr, a.out_be, a.chunk_base, a.result);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(ps->used[b], stream);
+    if (e != hipSuccess) return e;
+    const uint64_t tail = a.len - nfull * a.bpc;
+    if (tail == 0) return hipSuccess;
+    ChunkLaunch t = a;  // the short tail chunk: one lane of the byte-exact kernel
+    t.data = a.data + nfull * a.bpc;
+    t.len = tail;
+    t.chunk_base = a.chunk_base + nfull;
+    t.overlap_previous = false;
+    if (verify) t.crc_be = a.crc_be + 4 * nfull;
+    else t.out_be = a.out_be + 4 * nfull;
+    return verify ? launch_t<0, true>(t, d_tables, 1, stream) : launch_t<0, false>(t, d_tables, 1, stream);
+}
+
+}  // namespace
+
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
-                         const uint32_t *d_fold, int grid_cap, hipStream_t stream) {
+                         const uint32_t *d_fold, int grid_cap, hipStream_t stream, PieceScratch *pieces) {
     const uint64_t chunks = (a.len + a.bpc - 1) / a.bpc;
     if (chunks == 0) return hipSuccess;
     const bool aligned = (reinterpret_cast<uintptr_t>(a.data) & 15u) == 0 &&
                          (reinterpret_cast<uintptr_t>(verify ? a.crc_be : a.out_be) & 3u) == 0;
     const uint64_t unit = a.bpc <= uint32_t(kRoundBytes) ? uint64_t(kRoundBytes) : a.bpc;
+#if HDFS3_LAB
+    if (g_variant == 123) pieces = nullptr;  // A/B: the multi-round kernel (before r3zf)
+#endif
+    // pieces + combine from 256 MiB per launch: 1 GiB at bpc 8192 / 16384 / 65536 172.7 / 173.5 / 174.4 us
+    // against 196.0 / 200.6 / 209.1 for the multi-round kernel, but the combine's own launch (~6 us,
+    // latency-bound) loses 0.9 us at 128 MiB (profiles/r03/reentry/r3zf_*.jsonl); chunk sizes the
+    // multi-round kernel does not cover (12 KiB, 32 KiB, ...) take the pieces at every length
+    const bool multi_round = a.bpc == 8192 || a.bpc == 16384 || a.bpc == 65536;
+    if (pieces && aligned && a.bpc > uint32_t(kRoundBytes) && a.bpc % kRoundBytes == 0 && a.len >= a.bpc &&
+        (!multi_round || a.len >= kPiecesMinBytes))
+        return launch_pieces(a, verify, d_tables, d_fold, grid_cap, stream, pieces);
     if (aligned && a.len >= unit) {
         switch (a.bpc) {
         case 512: return launch_rv<512>(a, verify, d_tables, d_fold, grid_cap, stream);

@@ -106,6 +106,7 @@ struct hdfs3_crc_ctx {
     } seg_ring[4];
     unsigned seg_next = 0;
     hdfs3crc::WordScratch words;  // dense CRC words of compute over in-packet word regions
+    hdfs3crc::PieceScratch pieces;  // 4096-byte piece CRCs of chunks above 4 KiB (launch_chunks)
     hdfs3crc::Slot slot[2];
     std::atomic<uint64_t> launches{0};
     std::mutex arena_mu;                          // guards arena_cache

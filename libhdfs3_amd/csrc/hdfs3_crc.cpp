@@ -139,7 +139,7 @@ int finish_pending(Slot &s) {
 
 int launch(hdfs3_crc_ctx *ctx, const ChunkLaunch &in, bool verify) {
     ChunkLaunch a = in;
-    HIP_TRY(launch_chunks(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream));
+    HIP_TRY(launch_chunks(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, &ctx->pieces));
     ++ctx->launches;
     return 0;
 }
@@ -515,6 +515,7 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx) {
         if (st.done) (void)hipEventDestroy(st.done);
     }
     ctx->words.release();
+    ctx->pieces.release();
     for (int p = 0; p < 2; ++p) {
         if (ctx->d_tables_by[p]) (void)hipFree(ctx->d_tables_by[p]);
         if (ctx->d_fold_by[p]) (void)hipFree(ctx->d_fold_by[p]);

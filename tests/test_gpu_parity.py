@@ -244,6 +244,44 @@ def test_compute_staged_words_boundaries(gpu_ctx, n, overlap):
     assert np.all(got[4 * nc:] == 0xA5)
 
 
+@pytest.mark.parametrize("bpc", [8192, 12288, 32768, 65536])
+def test_chunks_above_4k_pieces_and_combine(gpu_ctx, bpc):
+    """bpc a multiple of 4096 above 4096: the round kernel's 4096-byte piece CRCs into the ctx
+    scratch, then the combine kernel (launch_pieces). Whole chunks, a short tail (verified only with
+    local semantics), a flipped bit in the first / middle / last chunk, and overlapped back-to-back
+    computes of different blocks (the scratch alternates between two buffers): every word against
+    the oracle."""
+    from libhdfs3_amd.engine import DeviceBuffer
+
+    # 8 / 16 / 64 KiB chunks take the pieces from 256 MiB per launch (kPiecesMinBytes), other
+    # multiples of 4096 at every length
+    for n in (bpc * 37, bpc * 37 + 4096 * 2 + 300, bpc * 2, bpc * 5 + 1, (64 << 20) + 5 * bpc + 77,
+              (256 << 20) + 3 * bpc + 100):
+        data = splitmix_bytes(n, 0xC0B1 + bpc + n)
+        want = oracle_compute(data, bpc)
+        d = gpu_ctx.upload(data)
+        dc = gpu_ctx.upload(np.full(want.nbytes, 0xA5, dtype=np.uint8))
+        gpu_ctx.compute_dev(d.ptr, n, bpc, dc.ptr)
+        assert np.array_equal(gpu_ctx.download(dc, want.nbytes), want), (bpc, n)
+        assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, True) == -1
+        nfull = n // bpc
+        for k in (0, nfull // 2, nfull - 1):
+            pos = k * bpc + (k * 977) % bpc
+            gpu_ctx.upload(np.array([data[pos] ^ 0x10], dtype=np.uint8), d, offset=pos)
+            assert gpu_ctx.verify_dev(d.ptr, n, bpc, dc.ptr, False) == k, (bpc, n, k)
+            gpu_ctx.upload(data[pos:pos + 1], d, offset=pos)
+    # overlapped computes of 4 different blocks back to back, then every word
+    blocks = [splitmix_bytes(bpc * 300 + 4096, 0xD0B1 + bpc + i) for i in range(4)]
+    ds = [gpu_ctx.upload(b) for b in blocks]
+    wants = [oracle_compute(b, bpc) for b in blocks]
+    outs = [gpu_ctx.upload(np.full(w.nbytes, 0xA5, dtype=np.uint8)) for w in wants]
+    for rep in range(3):
+        for i in range(4):
+            gpu_ctx.compute_dev(ds[i].ptr, blocks[i].nbytes, bpc, outs[i].ptr, overlap_previous=i > 0)
+    for i in range(4):
+        assert np.array_equal(gpu_ctx.download(outs[i], wants[i].nbytes), wants[i]), (bpc, i)
+
+
 def test_block_128mib_async_result_and_launch_count(gpu_ctx):
     """Config 2: one 128 MiB block, 512 B chunks, device-resident async verify."""
     from libhdfs3_amd.engine import DeviceBuffer
