@@ -118,6 +118,7 @@ struct PieceScratch {
     uint8_t *d[2] = {nullptr, nullptr};
     uint64_t cap[2] = {0, 0};
     hipEvent_t used[2] = {nullptr, nullptr};  // recorded after the combine that read buffer i
+    hipStream_t on[2] = {nullptr, nullptr};   // the stream that combine ran on
     unsigned next = 0;
     void release();
 };

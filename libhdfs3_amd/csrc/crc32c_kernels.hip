@@ -246,7 +246,13 @@ hipError_t launch_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_ta
     if (!ps->used[b]) {
         hipError_t e = hipEventCreateWithFlags(&ps->used[b], hipEventDisableTiming);
         if (e != hipSuccess) return e;
+    } else if (ps->on[b] != stream) {
+        // the last reader of this buffer ran on another stream (the ctx's stream was switched):
+        // order this launch after it; on one stream the launch order already does
+        hipError_t e = hipStreamWaitEvent(stream, ps->used[b], 0);
+        if (e != hipSuccess) return e;
     }
+    ps->on[b] = stream;
     ps->next = b + 1;
     ChunkLaunch p = a;  // the pieces: a compute at bpc 4096 over the whole chunks
     p.len = nfull * a.bpc;
