@@ -95,10 +95,11 @@ int hdfs3_crc_pool_stats_get(hdfs3_crc_pool_stats *out);
  * are not affected. Returns the number destroyed. */
 int hdfs3_crc_pool_trim(void);
 
-/* NUMA-local placement. Every thread the library runs for a device (the multi-device
- * workers, the block readers' receivers, the local readers' loaders) binds itself to the CPUs of
- * that device's NUMA node, intersected with the process's allowed CPUs, and allocates its pinned
- * staging there; HDFS3_NUMA=0 turns this off. hdfs3_device_numa_node: the node of `device` from
+/* NUMA-local placement, opt-in with HDFS3_NUMA=1: every thread the library runs for
+ * a device (the multi-device workers, the block readers' receivers, the local readers' loaders)
+ * binds itself to the CPUs of that device's NUMA node, intersected with the process's allowed CPUs,
+ * and allocates its pinned staging there. Off by default: on a one-GPU box it slowed loopback reads
+ * whose datanode and caller threads were not bound. hdfs3_device_numa_node: the node of `device` from
  * its PCI function (-1 when the platform does not say). hdfs3_numa_cpus: the policy's input for a
  * PCI function under a sysfs tree (sysfs_root "/sys" on a real host): the CPUs of its node, up to
  * max_cpus of them in cpus[]; returns their count, 0 when the node is unknown, or -errno. */

@@ -129,7 +129,12 @@ struct hdfs3_input_stream {
             const Block &b = blocks[size_t(j)];
             if (b.length <= 0 || b.replicas.empty()) continue;
             const int64_t want = std::min<int64_t>(b.length, ahead_bytes > 0 ? ahead_bytes : b.length);
-            const int slots = int(std::min<int64_t>((want + unit - 1) / unit + 1, 64));
+            // the stream's rings (ahead_blocks of them plus the current reader's) fit the pool's pinned
+            // cap, so the pool can keep them for the stream's next blocks and the next stream: with
+            // whole-block rings, read-ahead 7 over a 1 GiB file pinned new rings on every open
+            // (2.8-3.1 GiB/s against 12.6-13.2 with an uncapped pool, profiles/r03/reentry/r3e2e_fix_*)
+            const int64_t fit = int64_t(pool_pinned_cap_bytes() / uint64_t(ahead_blocks + 1)) / unit;
+            const int slots = int(std::max<int64_t>(3, std::min<int64_t>({(want + unit - 1) / unit + 1, 64, fit})));
             hdfs3_crc_ctx *c = nullptr;
             if (ctx_acquire(opts.device, &c, true)) break;  // no context to spare: read on demand
             hdfs3_block_id id = b.id;

@@ -605,6 +605,8 @@ void shed(hdfs3_crc_ctx *ctx, size_t keep_arenas, bool slots) {
 }
 }  // namespace
 
+uint64_t pool_pinned_cap_bytes() { return pool_pinned_cap(); }
+
 int ctx_acquire(int device, hdfs3_crc_ctx **out, bool deep) {
     if (!out) return fail(-EINVAL, "null out");
     {
@@ -650,11 +652,24 @@ void ctx_release(hdfs3_crc_ctx *ctx) {
             size_t deep = 0;
             for (hdfs3_crc_ctx *c : g_ctx_pool) deep += c->arena_cache.size() > kArenaCacheKeep;
             if (deep >= kDeepCtxMax && ctx->arena_cache.size() > kArenaCacheKeep) shed(ctx, kArenaCacheKeep, false);
-            // and the pool as a whole retains at most pool_pinned_cap() pinned bytes: this ctx sheds
-            // arenas, then its staging, and is destroyed if it still does not fit
+            // and the pool as a whole retains at most pool_pinned_cap() pinned bytes. The ctx released
+            // last is the one most likely to be taken again soon (a read-ahead stream releases the
+            // ring of the block it finished and at once acquires a deep ctx for the next block ahead),
+            // so the pooled contexts give back their arenas first, least recently released first
+            // (the pool's front); then this ctx sheds arenas and staging, and is destroyed if it still
+            // does not fit. Shedding this ctx first made every read-ahead block re-pin its ring once
+            // older pooled rings filled the cap: 1 GiB with read-ahead 2 / 7 at 6.6 / 2.3 GiB/s
+            // against 11.8 / 10.6 uncapped (profiles/r03/reentry/r3e2eab_*).
             const uint64_t cap = pool_pinned_cap();
+            const uint64_t mine = footprint(ctx).pinned;
             uint64_t others = 0;
             for (hdfs3_crc_ctx *c : g_ctx_pool) others += footprint(c).pinned;
+            for (const bool slots : {false, true})  // their arenas first, then their staging slots
+                for (size_t i = 0; i < g_ctx_pool.size() && others + mine > cap; ++i) {
+                    const uint64_t before = footprint(g_ctx_pool[i]).pinned;
+                    shed(g_ctx_pool[i], 0, slots);
+                    others -= before - footprint(g_ctx_pool[i]).pinned;
+                }
             if (others + footprint(ctx).pinned > cap) shed(ctx, 0, false);
             if (others + footprint(ctx).pinned > cap) shed(ctx, 0, true);
             if (others + footprint(ctx).pinned <= cap) {

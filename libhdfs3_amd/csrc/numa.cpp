@@ -88,10 +88,15 @@ void lookup(int device) {
     g_have[device] = true;
 }
 
+// Opt-in (HDFS3_NUMA=1). Binding the readers' receiver and loader threads to their GPU's node
+// measured slower on the one-GPU box, whose loopback datanode and caller threads are not bound:
+// 1 GiB through hdfsRead 3.3-7.5 GiB/s with it against 6.4-7.8 without, 8 concurrent hdfsPreads
+// 14.7-17.4 against 24.1-34.3 (profiles/r03/reentry/r3e2eab_*). The benefit it is for (host
+// data crossing the socket interconnect on 2-socket 8-GPU nodes) is unmeasured here.
 bool enabled() {
     static const bool on = [] {
         const char *e = std::getenv("HDFS3_NUMA");
-        return !(e && std::strcmp(e, "0") == 0);
+        return e && std::strcmp(e, "1") == 0;
     }();
     return on;
 }
