@@ -82,7 +82,7 @@ void hdfs3_crc_ctx_release(hdfs3_crc_ctx *ctx);
 /* The pool's retained pinned host memory is capped process-wide: a released context first gives
  * back cached arenas and staging until the pooled total fits, and is destroyed when it still does
  * not. The cap is HDFS3_POOL_PINNED_MAX (bytes, or with a K/M/G suffix; read once) and defaults to
- * 512 MiB; 0 pools nothing. The reference holds one packet buffer per reader
+ * 1 GiB (a read-ahead stream of depth 3 over 128 MiB blocks keeps its rings); 0 pools nothing. The reference holds one packet buffer per reader
  * (RemoteBlockReader.cpp:244) and nothing once it is closed. */
 typedef struct hdfs3_crc_pool_stats {
     uint64_t pooled_contexts;   /* idle contexts in the pool                                  */

@@ -535,7 +535,10 @@ std::vector<hdfs3_crc_ctx *> g_ctx_pool;
 constexpr size_t kCtxPoolMax = 32;
 constexpr size_t kArenaCacheKeep = 6;  // arenas any pooled ctx keeps (block_reader.cpp kArenaCacheMax)
 constexpr size_t kDeepCtxMax = 8;      // pooled contexts allowed to keep a read-ahead ring's worth
-constexpr uint64_t kPoolPinnedDefault = uint64_t(512) << 20;
+// 1 GiB: the rings of a read-ahead stream up to depth 3 (whole 128 MiB blocks) plus the usual
+// shallow contexts; with 512 MiB, depth 2 / 3 read 9.1-10.7 / 5.1-7.0 GiB/s against 13.2-13.9 /
+// 11.1-14.1 (every open re-pinned rings the pool had shed; profiles/r03/reentry/r3e2e_caps_*)
+constexpr uint64_t kPoolPinnedDefault = uint64_t(1) << 30;
 
 // HDFS3_POOL_PINNED_MAX: bytes, or with a K/M/G suffix
 uint64_t pool_pinned_cap() {

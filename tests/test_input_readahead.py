@@ -279,7 +279,7 @@ def test_pool_pinned_memory_stays_under_the_cap(cluster):
                 assert np.array_equal(got, whole)
             assert lib.hdfs3_crc_pool_stats_get(ctypes.byref(st)) == 0
             assert st.pinned_bytes <= st.pinned_cap_bytes, (st.pinned_bytes, st.pinned_cap_bytes)
-    assert st.pinned_cap_bytes == 512 << 20 and st.pooled_contexts > 0
+    assert st.pinned_cap_bytes == 1 << 30 and st.pooled_contexts > 0
     assert lib.hdfs3_crc_pool_trim() == st.pooled_contexts
     assert lib.hdfs3_crc_pool_stats_get(ctypes.byref(st)) == 0
     assert st.pooled_contexts == 0 and st.pinned_bytes == 0
