@@ -329,11 +329,7 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 // The lane's constant byte offset is the only VGPR operand, so no 64-bit VGPR address
 // temporaries exist that the allocator could alias with in-flight load destinations
 // (which made the compiler drain the previous round's loads before each prefetch).
-// MAP (lab A/B of the lane mapping, crc32c_wave.h kLabHalfSwap / kLabDirect): instruction t's byte
-// offset within the round besides lane_off. 0 (production): 1024 t, every instruction 1 KiB contiguous;
-// 1: 2048 (t >> 1) + 16 (t & 1), 32-byte runs per lane pair (one permlane32 stage left); 2: 16 t, each
-// lane its own 64 bytes (no regroup, every 128-byte line touched by all four instructions).
-template <bool NT, int MAP = 0>
+template <bool NT>
 __device__ __forceinline__ void load_round_buf(Round &r, const uint8_t *base, uint32_t lane_off) {
     const uint64_t b = reinterpret_cast<uint64_t>(base);
     const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(b));
@@ -342,8 +338,7 @@ __device__ __forceinline__ void load_round_buf(Round &r, const uint8_t *base, ui
         reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, 4096, 0x00020000);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const uint32_t off = MAP == 0 ? 1024 * t : MAP == 1 ? 2048 * (t >> 1) + 16 * (t & 1) : 16 * t;
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + off, 0, NT ? 2 : 0);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + 1024 * t, 0, NT ? 2 : 0);
         r.w[t][0] = v.x;
         r.w[t][1] = v.y;
         r.w[t][2] = v.z;
@@ -363,23 +358,17 @@ __device__ __forceinline__ void swap16(uint32_t &a, uint32_t &b) {
     b = p[1];
 }
 
-// (row, register) 4x4 transpose, see above. MAP (load_round_buf): 1 keeps only the permlane32
-// stage, 2 has nothing to regroup.
-template <int MAP = 0>
+// (row, register) 4x4 transpose, see above.
 __device__ __forceinline__ void regroup(Round &r) {
-    if constexpr (MAP <= 1) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            swap32(r.w[0][k], r.w[2][k]);
-            swap32(r.w[1][k], r.w[3][k]);
-        }
+    for (int k = 0; k < 4; ++k) {
+        swap32(r.w[0][k], r.w[2][k]);
+        swap32(r.w[1][k], r.w[3][k]);
     }
-    if constexpr (MAP == 0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            swap16(r.w[0][k], r.w[1][k]);
-            swap16(r.w[2][k], r.w[3][k]);
-        }
+    for (int k = 0; k < 4; ++k) {
+        swap16(r.w[0][k], r.w[1][k]);
+        swap16(r.w[2][k], r.w[3][k]);
     }
 }
 

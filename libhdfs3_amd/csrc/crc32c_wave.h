@@ -39,8 +39,6 @@ constexpr int kLabNoPrio = 32;  // no s_setprio at any launch size (the round-3 
 constexpr int kLabNoStore = 64;     // diagnostic, compute: the held words are not stored (wrong results)
 constexpr int kLabNearStore = 128;  // diagnostic, compute: every flush stores to the wave's first round's words
 constexpr int kLabNoStage = 1024;   // compute: held stores even where production stages the words (kStageWords)
-constexpr int kLabHalfSwap = 2048;  // lane mapping with one permlane stage: 32-byte runs per lane pair
-constexpr int kLabDirect = 4096;    // lane mapping without permlanes: each lane loads its own 64 bytes
 // Not a lab bit: launch_wave3 sets it for compute at bpc 512 over a contiguous block whose waves have
 // at most kStageMaxRounds rounds (the words are staged in LDS and written as whole lines, §4.1)
 constexpr int kStageWords = 512;
@@ -204,10 +202,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     constexpr bool kWrong = (LAB & (kLabNoMath | kLabNoFill)) != 0;  // diagnostics: wrong CRCs (verify)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = lane % G;
-    constexpr int MAP = (LAB & kLabDirect) ? 2 : (LAB & kLabHalfSwap) ? 1 : 0;
-    const uint32_t lane_off = MAP == 2   ? 64 * lane
-                              : MAP == 1 ? 1024 * ((lane >> 4) & 1) + 64 * (lane & 15) + 32 * (lane >> 5)
-                                         : 64 * (lane & 15) + 16 * (lane >> 4);
+    const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
     const uint32_t K = walk.K;
 
     // lean fill: each of the image's 1024 slice-table words replicated 32x (TPB threads take 1024 / TPB
@@ -231,8 +226,8 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     WView cv0 = walk.view(0), cv1 = walk.view(1);
     __builtin_amdgcn_sched_barrier(0);
     Round a0, a1, b0, b1;
-    load_round_buf<true, MAP>(a0, cv0.p, lane_off);
-    load_round_buf<true, MAP>(a1, cv1.p, lane_off);
+    load_round_buf<true>(a0, cv0.p, lane_off);
+    load_round_buf<true>(a1, cv1.p, lane_off);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int f = 0; f < kFillIters; ++f) {
@@ -410,16 +405,16 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         prio(k);
         const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
         if constexpr (!LATE) {
-            load_round_buf<true, MAP>(p0, pv0.p, lane_off);
-            load_round_buf<true, MAP>(p1, pv1.p, lane_off);
+            load_round_buf<true>(p0, pv0.p, lane_off);
+            load_round_buf<true>(p1, pv1.p, lane_off);
         }
         __builtin_amdgcn_sched_barrier(0);
-        regroup<MAP>(c0);
-        regroup<MAP>(c1);
+        regroup(c0);
+        regroup(c1);
         if constexpr (LATE) {
             __builtin_amdgcn_sched_barrier(0);
-            load_round_buf<true, MAP>(p0, pv0.p, lane_off);
-            load_round_buf<true, MAP>(p1, pv1.p, lane_off);
+            load_round_buf<true>(p0, pv0.p, lane_off);
+            load_round_buf<true>(p1, pv1.p, lane_off);
             __builtin_amdgcn_sched_barrier(0);
         }
         uint32_t x0, x1;
@@ -447,9 +442,9 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             prio(k);
             const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
             __builtin_amdgcn_sched_barrier(0);
-            regroup<MAP>(c0);
+            regroup(c0);
             solo(c0, cv0, k, w0, std::integral_constant<int, 0>{});
-            regroup<MAP>(c1);
+            regroup(c1);
             solo(c1, cv1, k + 1, w1, std::integral_constant<int, 1>{});
         };
         if (nr != 0) {

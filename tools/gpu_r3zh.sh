@@ -1,6 +1,7 @@
 #!/bin/bash
 # Lane-mapping A/B: production (16 permlane swaps per round) against one permlane stage (124) and
 # direct 64-byte lane loads (125), 128 MiB per launch overlapped / barriered, compute, and 1 GiB.
+# Both lost (+16 % / +72 %); the variants exist only in commit 51b6ce7 (reverted after this run).
 set -o pipefail
 TAG=${1:-r3zh}
 cd "$GRAFT_REPO_ROOT" || exit 1
