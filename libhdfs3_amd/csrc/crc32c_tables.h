@@ -95,7 +95,9 @@ inline void build_fold_nibbles(const uint32_t fold[kFoldWords], int set, uint32_
 //   ~state(init ~0) = crc0 ^ A^C(~0) ^ ~0,   crc0 = XOR_j M_j(x_j) over chains started from 0,
 // so adding the constant K_C = A^C(~0) ^ ~0 to every k = 0 entry of lane G-1 (whose M is the
 // identity) makes the lane fold + group xor return the finished CRC: no init xor per round and
-// no final complement per chunk.
+// no final complement per chunk. Every entry is then byte-swapped: the fold is linear in its entries,
+// so the group xor returns the CRC already in the big-endian order of the stored words (no v_perm per
+// round to compare or store them).
 // The device fold image is the kFoldWords matrix columns followed by the 4 affine sets.
 constexpr int kFoldAffineOff = kFoldWords;
 constexpr int kFoldImageWords = kFoldAffineOff + 4 * kFoldNibbleWords;
@@ -106,6 +108,7 @@ inline void build_fold_affine(const uint32_t t0[kTableEntries], int set, uint32_
     for (int lane = 0; lane < 64; ++lane)
         if (lane % g == g - 1)
             for (uint32_t e = 0; e < 16; ++e) out[e * 64 + lane] ^= kc;  // k = 0
+    for (int i = 0; i < kFoldNibbleWords; ++i) out[i] = __builtin_bswap32(out[i]);
 }
 
 }  // namespace hdfs3crc

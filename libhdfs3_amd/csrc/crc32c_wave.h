@@ -286,19 +286,20 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             // kLabNoStore keeps the words live through a compare that practically never stores
             if (uint32_t(i) < nheld && ((LAB & kLabNoStore) == 0 || hold[i] == 0x9E3779B9u)) {
                 if constexpr ((LAB & kLabNearStore) != 0 && !kAddr) {
-                    *(gu32 *)((gu8 *)walk.view(0).w + 4 * lane) = __builtin_bswap32(hold[i]);
+                    *(gu32 *)((gu8 *)walk.view(0).w + 4 * lane) = hold[i];
                 } else if constexpr (kAddr) {
-                    if (hold_addr[i]) *hold_addr[i] = __builtin_bswap32(hold[i]);
+                    if (hold_addr[i]) *hold_addr[i] = hold[i];
                 } else {
                     const uint32_t kk = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
-                    if (kk < K) *(gu32 *)((gu8 *)walk.view(kk).w + 4 * (lane & 7)) = __builtin_bswap32(hold[i]);
+                    if (kk < K) *(gu32 *)((gu8 *)walk.view(kk).w + 4 * (lane & 7)) = hold[i];
                 }
             }
         }
         hold_base += nheld;
         nheld = 0;
     };
-    // y: the chunk's finished CRC (the affine fold image carries init and final xor)
+    // y: the chunk's finished CRC, byte-swapped (the affine fold image carries init and final xor
+    // and the swap: y is the stored big-endian word as it loads)
     // kStageWords (compute at bpc 512 over a contiguous block, at most kStageMaxRounds rounds per wave):
     // every word waits in the LDS the half fold image leaves free (16 KiB: slot s's round k at word
     // (k * 16 + s) * 8 + c) and the workgroup writes them at its end as whole 512-B runs, since the 16
@@ -342,11 +343,11 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         if constexpr (VERIFY) {
             // the diagnostics compute wrong CRCs: compare inverted so they do not flag every chunk
             // (an atomic per chunk would dominate their time)
-            if ((__builtin_bswap32(want) != c) != kWrong)
+            if ((want != c) != kWrong)
                 __hip_atomic_fetch_max((gu64 *)result, ~(unsigned long long)(v.key + lane / G), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bswap32(c), wrsrc(v), woff, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(c, wrsrc(v), woff, 0, 0);
         }
     };
     auto word = [](const Round &r, int i) -> uint32_t { return r.w[i >> 2][i & 3]; };
@@ -479,8 +480,8 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             const uint32_t t = threadIdx.x + 1024 * p, k = t >> 7, s = (t >> 3) & 15, c = t & 7;
             const uint32_t ks = walk.kq + (wg_first + s < walk.kr ? 1u : 0u);
             if (k < ks)
-                *(gu32 *)((gu8 *)walk.words + 4 * (kRoundBytes / BPC) * (wg_first + s + uint64_t(k) * walk.stride) + 4 * c) =
-                    __builtin_bswap32(stage[t]);
+                *(gu32 *)((gu8 *)walk.words + 4 * (kRoundBytes / BPC) * (wg_first + s + uint64_t(k) * walk.stride) +
+                          4 * c) = stage[t];
         }
     } else if constexpr (kHold) {
         flush();
