@@ -9,75 +9,6 @@
 namespace hdfs3crc {
 namespace {
 
-// Lab: round counts skewed by the wave's slot quartile in its workgroup, against the SIMD arbiter's
-// oldest-first order (slots 0-3 are each SIMD's oldest wave and end first). SKEW 1: quartiles get
-// kq + (1, 0, 0, -1) rounds; SKEW 2: kq + (2, 1, -1, -2). The rounds a young quartile skips (the last
-// columns of the round-robin) go to an old quartile of the same workgroup as its extra columns.
-// Whole rounds only, kr == 0 (every wave kq rounds before the skew).
-template <int CPU, int SKEW>
-struct SkewWalk {
-    static constexpr bool kLaneView = true;
-    static constexpr bool kContiguous = false;
-    const uint8_t *data;
-    uint8_t *words;
-    uint64_t key0, first, stride;
-    uint32_t K, kq, slot;
-    const uint8_t *dummy;
-    __device__ __forceinline__ WView view(uint32_t k) const {
-        uint64_t u = first + uint64_t(k) * stride;
-        if (k >= kq) {  // an old quartile's extra column: a young quartile's skipped round
-            const uint64_t wg = first - slot;
-            uint32_t col, ts;
-            if (SKEW == 1) {
-                col = kq - 1, ts = 12 + slot;
-            } else if (slot < 4) {
-                col = kq - 2 + (k - kq), ts = 12 + slot;
-            } else {
-                col = kq - 1, ts = slot + 4;
-            }
-            u = wg + uint64_t(col) * stride + ts;
-        }
-        const bool in = k < K;
-        return WView{in ? data + u * kRoundBytes : dummy, in ? words + 4 * CPU * u : const_cast<uint8_t *>(dummy),
-                     key0 + CPU * u};
-    }
-};
-
-template <int BPC, int SKEW>
-__global__ __launch_bounds__(kBlockThreads) void crc32c_skew_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
-                                                                    const uint32_t *__restrict__ g_nib) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytesWave / 4];
-    constexpr int kCpu = kRoundBytes / BPC;
-    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
-    const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + slot;
-    const uint32_t q = slot >> 2;
-    const int d = SKEW == 1 ? (q == 0 ? 1 : q == 3 ? -1 : 0) : (q == 0 ? 2 : q == 1 ? 1 : q == 2 ? -1 : -2);
-    SkewWalk<kCpu, SKEW> w{a.data, const_cast<uint8_t *>(a.crc_be), a.chunk_base, wave, nwaves,
-                           uint32_t(int(a.kq) + d), a.kq, slot, reinterpret_cast<const uint8_t *>(g_tab)};
-    wave_rounds<BPC, true, false, false, 0, kBlockThreads>(w, lds, g_tab, g_nib, a.result);
-}
-
-template <int BPC, int SKEW>
-hipError_t launch_skew(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
-    constexpr int G = BPC / 64;
-    constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
-    const uint32_t *nib = fold + kFoldAffineOff + set * kFoldNibbleWords;
-    const uint64_t units = a.len / kRoundBytes;
-    const uint64_t nwaves = uint64_t(grid_cap) * kWavesPerBlock;
-    if (a.len % kRoundBytes || units % nwaves || units / nwaves < 3 || units / nwaves >= (1u << 30))
-        return hipErrorInvalidValue;
-    ChunkLaunch b = a;
-    b.kq = uint32_t(units / nwaves);
-    b.kr = 0;
-    if (a.overlap_previous)
-        hipExtLaunchKernelGGL((crc32c_skew_kernel<BPC, SKEW>), dim3(grid_cap), dim3(kBlockThreads), 0, s, nullptr,
-                              nullptr, hipExtAnyOrderLaunch, b, tab, nib);
-    else
-        hipLaunchKernelGGL((crc32c_skew_kernel<BPC, SKEW>), dim3(grid_cap), dim3(kBlockThreads), 0, s, b, tab, nib);
-    return hipGetLastError();
-}
-
 template <int BPC, bool V>
 hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                       hipStream_t s) {
@@ -124,13 +55,6 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true>(a, tab, fold, grid_cap, s);
         case 122:  // compute: held stores where production stages the words in LDS (before r3zb)
             return launch_wave3<BPC, V, false, true, kLabNoStage>(a, tab, fold, grid_cap, s);
-        case 126:  // verify: round counts skewed +1/0/0/-1 by slot quartile
-        case 127:  // verify: +2/+1/-1/-2
-            if constexpr (V) {
-                return variant == 126 ? launch_skew<BPC, 1>(a, tab, fold, grid_cap, s)
-                                      : launch_skew<BPC, 2>(a, tab, fold, grid_cap, s);
-            }
-            return hipErrorInvalidValue;
         case 78:  // diagnostic: 77 without the slice-table LDS fill
             return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;

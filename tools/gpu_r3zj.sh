@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round counts skewed by slot quartile against the SIMD arbiter's oldest-first order (lab 126/127):
-# coverage check, then in-process A/B at 128 MiB (overlapped, barriered), 2 GiB-sized runs of 8 rounds.
+# coverage check, then in-process A/B at 128 MiB (overlapped, barriered). Both lost; the variants and
+# its coverage check (tools/skew_check.py) exist only in commit 494a7a6 (removed after this run).
 set -o pipefail
 TAG=${1:-r3zj}
 cd "$GRAFT_REPO_ROOT" || exit 1
