@@ -55,10 +55,6 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true>(a, tab, fold, grid_cap, s);
         case 122:  // compute: held stores where production stages the words in LDS (before r3zb)
             return launch_wave3<BPC, V, false, true, kLabNoStage>(a, tab, fold, grid_cap, s);
-        case 128:  // prefetch issued after the chains' 4th word (fewer bytes in flight per wave)
-            return launch_wave3<BPC, V, false, true, kLabPfMid4>(a, tab, fold, grid_cap, s);
-        case 129:  // ... after the 8th word
-            return launch_wave3<BPC, V, false, true, kLabPfMid8>(a, tab, fold, grid_cap, s);
         case 78:  // diagnostic: 77 without the slice-table LDS fill
             return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;

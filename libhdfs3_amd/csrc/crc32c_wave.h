@@ -39,8 +39,6 @@ constexpr int kLabNoPrio = 32;  // no s_setprio at any launch size (the round-3 
 constexpr int kLabNoStore = 64;     // diagnostic, compute: the held words are not stored (wrong results)
 constexpr int kLabNearStore = 128;  // diagnostic, compute: every flush stores to the wave's first round's words
 constexpr int kLabNoStage = 1024;   // compute: held stores even where production stages the words (kStageWords)
-constexpr int kLabPfMid4 = 2048;    // prefetch issued after the chains' 4th word, not before the chains
-constexpr int kLabPfMid8 = 4096;    // ... after the 8th word
 // Not a lab bit: launch_wave3 sets it for compute at bpc 512 over a contiguous block whose waves have
 // at most kStageMaxRounds rounds (the words are staged in LDS and written as whole lines, §4.1)
 constexpr int kStageWords = 512;
@@ -359,18 +357,13 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         return lookups(t, x);
     };
     // two interleaved chains over c0, c1 (chain 1's 4 reads fly while chain 0 folds)
-    constexpr int kPfAt = (LAB & kLabPfMid4) ? 4 : (LAB & kLabPfMid8) ? 8 : -1;
-    auto chains = [&](Round &c0, Round &c1, uint32_t &x0, uint32_t &x1, auto &&pf) {
+    auto chains = [&](Round &c0, Round &c1, uint32_t &x0, uint32_t &x1) {
         x0 = word(c0, 0);
         x1 = word(c1, 0);
         Look l0 = look(x0), l1;
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            if (i == kPfAt) {
-                pf();
-                __builtin_amdgcn_sched_barrier(0);
-            }
             l1 = look(x1);
             __builtin_amdgcn_sched_barrier(0);
             x0 = combine(l0, i < 15 ? word(c0, i < 15 ? i + 1 : 15) : 0u);
@@ -419,17 +412,14 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         __builtin_amdgcn_sched_barrier(0);
         regroup(c0);
         regroup(c1);
-        auto pf = [&]() {
+        if constexpr (LATE) {
+            __builtin_amdgcn_sched_barrier(0);
             load_round_buf<true>(p0, pv0.p, lane_off);
             load_round_buf<true>(p1, pv1.p, lane_off);
-        };
-        if constexpr (LATE && kPfAt < 0) {
-            __builtin_amdgcn_sched_barrier(0);
-            pf();
             __builtin_amdgcn_sched_barrier(0);
         }
         uint32_t x0, x1;
-        chains(c0, c1, x0, x1, pf);
+        chains(c0, c1, x0, x1);
         finish(k, cv0, group_xor<G>(fold(x0)), w0);
         finish(k + 1, cv1, group_xor<G>(fold(x1)), w1);
         __builtin_amdgcn_sched_barrier(0);

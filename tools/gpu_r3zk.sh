@@ -1,6 +1,7 @@
 #!/bin/bash
 # Prefetch issue point A/B: production (before the chains) against after the chains' 4th / 8th word
 # (lab 128 / 129: fewer bytes in flight per wave), 128 MiB overlapped / barriered, bpc 512 / 4096, 1 GiB.
+# Within noise of production; the variants exist only in commit 0e81d7e (removed after this run).
 set -o pipefail
 TAG=${1:-r3zk}
 cd "$GRAFT_REPO_ROOT" || exit 1
