@@ -39,10 +39,13 @@ constexpr int kLabNoPrio = 32;  // no s_setprio at any launch size (the round-3 
 constexpr int kLabNoStore = 64;     // diagnostic, compute: the held words are not stored (wrong results)
 constexpr int kLabNearStore = 128;  // diagnostic, compute: every flush stores to the wave's first round's words
 constexpr int kLabNoStage = 1024;   // compute: held stores even where production stages the words (kStageWords)
-// Not a lab bit: launch_wave3 sets it for compute at bpc 512 over a contiguous block whose waves have
-// at most kStageMaxRounds rounds (the words are staged in LDS and written as whole lines, §4.1)
+// Not a lab bit: launch_wave3 sets it for compute at bpc 512 / 1024 / 2048 over a contiguous block whose
+// waves have at most kStageMaxRounds(bpc) rounds (the words are staged in LDS and written as whole
+// lines, §4.1)
 constexpr int kStageWords = 512;
-constexpr uint32_t kStageMaxRounds = 32;  // 16 waves x 32 rounds x 32 B = the 16 KiB the half fold image leaves
+// 16 waves x R rounds x (4096 / bpc) words = the 4096 words (16 KiB) the half fold image leaves:
+// 32 rounds at bpc 512, 64 at 1024, 128 at 2048
+constexpr uint32_t kStageMaxRounds(int bpc) { return uint32_t(bpc / 16); }
 
 // Waves with at least this many rounds set their priority by the rounds they have left (round 3):
 // the SIMD arbiter favours older waves, so with equal work a workgroup's waves end staggered and its
@@ -300,19 +303,19 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     };
     // y: the chunk's finished CRC, byte-swapped (the affine fold image carries init and final xor
     // and the swap: y is the stored big-endian word as it loads)
-    // kStageWords (compute at bpc 512 over a contiguous block, at most kStageMaxRounds rounds per wave):
-    // every word waits in the LDS the half fold image leaves free (16 KiB: slot s's round k at word
-    // (k * 16 + s) * 8 + c) and the workgroup writes them at its end as whole 512-B runs, since the 16
-    // waves' k-th rounds are 16 consecutive units. The held stores send each wave's words as 32-B
+    // kStageWords (compute at bpc <= 2048 over a contiguous block, at most kStageMaxRounds rounds per
+    // wave): every word waits in the LDS the half fold image leaves free (16 KiB: slot s's round k at
+    // word (k * 16 + s) * CPW + c, CPW = 4096 / bpc words per round) and the workgroup writes them at its
+    // end as whole runs of 16 * CPW words, since the 16 waves' k-th rounds are 16 consecutive units. The held stores send each wave's words as 32-B
     // pieces of lines that three other waves complete later, into a saturated read stream: 0.4 us of
     // the 1.1 us those writes cost an overlapped 128 MiB launch (profiles/r03/reentry/r3zb_c128_*).
-    constexpr bool kStage = kHold && (LAB & kStageWords) != 0 && Walk::kContiguous && kHalfFold && TPB == 1024;
-    static_assert(!kStage || G == 8, "staging holds 8 words per round");
+    constexpr bool kStage = !VERIFY && (LAB & kStageWords) != 0 && Walk::kContiguous && kHalfFold && TPB == 1024;
+    constexpr uint32_t kCpw = 64 / G;  // chunk words per round
     uint32_t *stage = lds + kLdsBytesWave / 4 - 4096;
     const uint32_t slot = threadIdx.x >> 6;
     auto finish = [&](uint32_t k, const WView &v, uint32_t y, uint32_t want) {
         if constexpr (kStage) {
-            if (k < K && j == 0) stage[(k * 16 + slot) * 8 + lane / G] = y;
+            if (k < K && j == 0) stage[(k * 16 + slot) * kCpw + lane / G] = y;
             return;
         }
         if constexpr (kHold) {
@@ -477,7 +480,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         const uint64_t wg_first = walk.first - slot;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const uint32_t t = threadIdx.x + 1024 * p, k = t >> 7, s = (t >> 3) & 15, c = t & 7;
+            const uint32_t t = threadIdx.x + 1024 * p, k = t / (16 * kCpw), s = (t / kCpw) & 15, c = t % kCpw;
             const uint32_t ks = walk.kq + (wg_first + s < walk.kr ? 1u : 0u);
             if (k < ks)
                 *(gu32 *)((gu8 *)walk.words + 4 * (kRoundBytes / BPC) * (wg_first + s + uint64_t(k) * walk.stride) +
@@ -614,9 +617,10 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     ChunkLaunch b = a;
     b.kq = uint32_t(units / nwaves);
     b.kr = uint32_t(units % nwaves);
-    // compute at bpc 512 over one contiguous block with few enough rounds per wave: staged words
-    if constexpr (!V && BPC == 512 && !PITCH && TPB == 1024 && (LAB & (kStageWords | kLabNoStage)) == 0) {
-        if (b.kq + (b.kr ? 1u : 0u) <= kStageMaxRounds)
+    // compute at bpc <= 2048 over one contiguous block with few enough rounds per wave: staged words
+    if constexpr (!V && BPC <= 2048 && !PITCH && TPB == 1024 &&
+                  (LAB & (kStageWords | kLabNoStage | kLabNoHold)) == 0) {
+        if (b.kq + (b.kr ? 1u : 0u) <= kStageMaxRounds(BPC))
             return launch_wave3<BPC, V, PITCH, SOLO, LAB | kStageWords, TPB>(a, tab, fold, grid_cap, s);
     }
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)

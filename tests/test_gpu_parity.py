@@ -219,18 +219,22 @@ def test_compute_held_stores_past_64_rounds_per_wave(gpu_ctx, n):
     assert np.array_equal(gpu_ctx.download(dc, 4 * nc), oracle_compute(data, bpc))
 
 
-@pytest.mark.parametrize("n", [128 << 20, (512 << 20), (512 << 20) + 4096, (128 << 20) + 4096 * 3 + 517,
-                               4096 * 4096 * 7 + 4096 * 5, 4096 * 33 + 100])
+@pytest.mark.parametrize("bpc,n", [(512, 128 << 20), (512, 512 << 20), (512, (512 << 20) + 4096),
+                                   (512, (128 << 20) + 4096 * 3 + 517), (512, 4096 * 4096 * 7 + 4096 * 5),
+                                   (512, 4096 * 33 + 100), (1024, 1 << 30), (1024, (1 << 30) + 4096),
+                                   (1024, (128 << 20) + 4096 * 3 + 517), (1024, 4096 * 33 + 100),
+                                   (2048, 2 << 30), (2048, (2 << 30) + 4096), (2048, (512 << 20) + 4096 * 5 + 1000),
+                                   (2048, 4096 * 33 + 100)])
 @pytest.mark.parametrize("overlap", [False, True])
-def test_compute_staged_words_boundaries(gpu_ctx, n, overlap):
-    """Compute at bpc 512 over a contiguous block whose waves have at most 32 rounds stages every
-    word in LDS and writes them as whole lines when the workgroup ends (kStageWords, crc32c_wave.h).
-    Sizes at exactly 32 rounds per wave (512 MiB), one round past it (held stores), waves with
-    unequal round counts, a slow region and short tail, and a small grid: every word against the
-    oracle, words poisoned first, barriered and overlapped (the solo last step)."""
+def test_compute_staged_words_boundaries(gpu_ctx, bpc, n, overlap):
+    """Compute at bpc 512 / 1024 / 2048 over a contiguous block whose waves have at most bpc / 16
+    rounds (32 / 64 / 128) stages every word in LDS and writes them as whole runs when the workgroup
+    ends (kStageWords, crc32c_wave.h). Sizes at exactly the limit (512 MiB / 1 GiB / 2 GiB), one round
+    past it (held stores at 512, per-round stores above), waves with unequal round counts, a slow
+    region and short tail, and a small grid: every word against the oracle, words poisoned first,
+    barriered and overlapped (the solo last step)."""
     from libhdfs3_amd.engine import DeviceBuffer
 
-    bpc = 512
     data = splitmix_bytes(n, 0x57A6E + n)
     d = gpu_ctx.upload(data)
     nc = (n + bpc - 1) // bpc
