@@ -55,6 +55,8 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true>(a, tab, fold, grid_cap, s);
         case 122:  // compute: held stores where production stages the words in LDS (before r3zb)
             return launch_wave3<BPC, V, false, true, kLabNoStage>(a, tab, fold, grid_cap, s);
+        case 130:  // compute: staged words at every size, written out window by window (kLabStageWin)
+            return launch_wave3<BPC, V, false, true, kLabStageWin>(a, tab, fold, grid_cap, s);
         case 78:  // diagnostic: 77 without the slice-table LDS fill
             return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;

@@ -39,9 +39,10 @@ constexpr int kLabNoPrio = 32;  // no s_setprio at any launch size (the round-3 
 constexpr int kLabNoStore = 64;     // diagnostic, compute: the held words are not stored (wrong results)
 constexpr int kLabNearStore = 128;  // diagnostic, compute: every flush stores to the wave's first round's words
 constexpr int kLabNoStage = 1024;   // compute: held stores even where production stages the words (kStageWords)
-// Not a lab bit: launch_wave3 sets it for compute at bpc 512 / 1024 / 2048 over a contiguous block whose
-// waves have at most kStageMaxRounds(bpc) rounds (the words are staged in LDS and written as whole
-// lines, §4.1)
+constexpr int kLabStageWin = 2048;  // compute at bpc 512: staged words past kStageMaxRounds too, window by window
+// Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
+// bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
+// written as whole lines, §4.1; past the window size in windows)
 constexpr int kStageWords = 512;
 // 16 waves x R rounds x (4096 / bpc) words = the 4096 words (16 KiB) the half fold image leaves:
 // 32 rounds at bpc 512, 64 at 1024, 128 at 2048
@@ -303,19 +304,43 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     };
     // y: the chunk's finished CRC, byte-swapped (the affine fold image carries init and final xor
     // and the swap: y is the stored big-endian word as it loads)
-    // kStageWords (compute at bpc <= 2048 over a contiguous block, at most kStageMaxRounds rounds per
-    // wave): every word waits in the LDS the half fold image leaves free (16 KiB: slot s's round k at
+    // kStageWords (compute at bpc <= 2048 over a contiguous block): every word of a window of
+    // kStageMaxRounds rounds per wave waits in the LDS the half fold image leaves free (16 KiB: slot s's round k at
     // word (k * 16 + s) * CPW + c, CPW = 4096 / bpc words per round) and the workgroup writes them at its
-    // end as whole runs of 16 * CPW words, since the 16 waves' k-th rounds are 16 consecutive units. The held stores send each wave's words as 32-B
-    // pieces of lines that three other waves complete later, into a saturated read stream: 0.4 us of
-    // the 1.1 us those writes cost an overlapped 128 MiB launch (profiles/r03/reentry/r3zb_c128_*).
+    // end as whole runs of 16 * CPW words, since the 16 waves' k-th rounds are 16 consecutive units.
+    // The held stores send each wave's words as 32-B pieces of lines that three other waves complete
+    // later, into a saturated read stream: 0.4 us of the 1.1 us those writes cost an overlapped 128 MiB
+    // launch (profiles/r03/reentry/r3zb_c128_*).
     constexpr bool kStage = !VERIFY && (LAB & kStageWords) != 0 && Walk::kContiguous && kHalfFold && TPB == 1024;
     constexpr uint32_t kCpw = 64 / G;  // chunk words per round
+    constexpr uint32_t kSR = kStageMaxRounds(BPC);  // rounds per staging window
     uint32_t *stage = lds + kLdsBytesWave / 4 - 4096;
     const uint32_t slot = threadIdx.x >> 6;
+    // Past kSR rounds per wave (bpc 1024 / 2048; bpc 512 with kLabStageWin) a window is written out
+    // after the step that finishes round m * kSR - 1, for every m with m * kSR < kq (or m * kSR == kq when
+    // some waves have kq + 1 rounds): every wave of the launch has at least kq rounds, so every wave runs
+    // that step and meets both barriers. The last window goes out at the workgroup's end.
+    uint32_t kq_flush = 0;  // flush at kend <= kq_flush
+    if constexpr (kStage) kq_flush = walk.kq - (walk.kr == 0 ? 1u : 0u);
+    auto stage_flush = [&](uint32_t kend) {
+        if constexpr (kStage) {
+            if (kend % kSR == 0 && kend <= kq_flush && walk.kq != 0) {
+                lds_barrier();
+                const uint64_t wg_first = walk.first - slot;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const uint32_t t = threadIdx.x + 1024 * p, kk = t / (16 * kCpw), s = (t / kCpw) & 15,
+                                   c = t % kCpw;
+                    *(gu32 *)((gu8 *)walk.words +
+                              4 * kCpw * (wg_first + s + uint64_t(kend - kSR + kk) * walk.stride) + 4 * c) = stage[t];
+                }
+                lds_barrier();
+            }
+        }
+    };
     auto finish = [&](uint32_t k, const WView &v, uint32_t y, uint32_t want) {
         if constexpr (kStage) {
-            if (k < K && j == 0) stage[(k * 16 + slot) * kCpw + lane / G] = y;
+            if (k < K && j == 0) stage[((k % kSR) * 16 + slot) * kCpw + lane / G] = y;
             return;
         }
         if constexpr (kHold) {
@@ -425,6 +450,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         chains(c0, c1, x0, x1);
         finish(k, cv0, group_xor<G>(fold(x0)), w0);
         finish(k + 1, cv1, group_xor<G>(fold(x1)), w1);
+        stage_flush(k + 2);
         __builtin_amdgcn_sched_barrier(0);
         cv0 = pv0;
         cv1 = pv1;
@@ -450,6 +476,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             solo(c0, cv0, k, w0, std::integral_constant<int, 0>{});
             regroup(c1);
             solo(c1, cv1, k + 1, w1, std::integral_constant<int, 1>{});
+            stage_flush(k + 2);
         };
         if (nr != 0) {
             const uint32_t kl = nr - 2;  // the last step's first round
@@ -478,9 +505,10 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     if constexpr (kStage) {
         lds_barrier();  // every wave of the workgroup runs wave_rounds to its end
         const uint64_t wg_first = walk.first - slot;
+        const uint32_t wb = walk.kq ? kSR * (kq_flush / kSR) : 0u;  // the last window's first round
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const uint32_t t = threadIdx.x + 1024 * p, k = t / (16 * kCpw), s = (t / kCpw) & 15, c = t % kCpw;
+            const uint32_t t = threadIdx.x + 1024 * p, k = wb + t / (16 * kCpw), s = (t / kCpw) & 15, c = t % kCpw;
             const uint32_t ks = walk.kq + (wg_first + s < walk.kr ? 1u : 0u);
             if (k < ks)
                 *(gu32 *)((gu8 *)walk.words + 4 * (kRoundBytes / BPC) * (wg_first + s + uint64_t(k) * walk.stride) +
@@ -617,10 +645,11 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     ChunkLaunch b = a;
     b.kq = uint32_t(units / nwaves);
     b.kr = uint32_t(units % nwaves);
-    // compute at bpc <= 2048 over one contiguous block with few enough rounds per wave: staged words
+    // compute at bpc <= 2048 over one contiguous block: staged words; at bpc 512 only while they fit one
+    // window (beyond it the held stores measured faster at 1 GiB: 160.4 against 163.1 us in windows)
     if constexpr (!V && BPC <= 2048 && !PITCH && TPB == 1024 &&
                   (LAB & (kStageWords | kLabNoStage | kLabNoHold)) == 0) {
-        if (b.kq + (b.kr ? 1u : 0u) <= kStageMaxRounds(BPC))
+        if (b.kq + (b.kr ? 1u : 0u) <= kStageMaxRounds(BPC) || BPC != 512 || (LAB & kLabStageWin) != 0)
             return launch_wave3<BPC, V, PITCH, SOLO, LAB | kStageWords, TPB>(a, tab, fold, grid_cap, s);
     }
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)

@@ -230,7 +230,7 @@ def test_compute_staged_words_boundaries(gpu_ctx, bpc, n, overlap):
     """Compute at bpc 512 / 1024 / 2048 over a contiguous block whose waves have at most bpc / 16
     rounds (32 / 64 / 128) stages every word in LDS and writes them as whole runs when the workgroup
     ends (kStageWords, crc32c_wave.h). Sizes at exactly the limit (512 MiB / 1 GiB / 2 GiB), one round
-    past it (held stores at 512, per-round stores above), waves with unequal round counts, a slow
+    past it (held stores at 512; at 1024 / 2048 a second window, written out after a workgroup barrier), waves with unequal round counts, a slow
     region and short tail, and a small grid: every word against the oracle, words poisoned first,
     barriered and overlapped (the solo last step)."""
     from libhdfs3_amd.engine import DeviceBuffer
@@ -320,6 +320,31 @@ def test_bit_flip_every_position_in_one_chunk(gpu_ctx):
             bad = data.copy()
             bad[3 * 512 + byte] ^= 1 << bit
             assert gpu_ctx.verify(bad, 512, crc, True) == 3
+
+
+@pytest.mark.parametrize("bpc,n", [(512, (512 << 20) + 4096 * 3 + 100), (512, 768 << 20), (512, 1 << 30),
+                                   (512, (1 << 30) + 4096 * 4097 + 517), (1024, (1 << 30) + 4096 * 5),
+                                   (1024, 1536 << 20), (2048, (2 << 30) + 4096)])
+def test_compute_staged_windows_lab(lab_ctx, bpc, n):
+    """Lab 130 (kLabStageWin): compute words staged in LDS past kStageMaxRounds too, each window of
+    bpc / 16 rounds written out after the step that finishes it (two workgroup barriers), the last
+    window at the workgroup's end. Launches one round past the limit, whole windows, partial last
+    windows, unequal round counts and a short tail: every word against the oracle, poison kept."""
+    from libhdfs3_amd import _native
+
+    lib = _native.lab()
+    try:
+        lib.hdfs3x_set_variant(130)
+        data = splitmix_bytes(n, 0x3A17 + bpc + n)
+        d = lab_ctx.upload(data)
+        nc = (n + bpc - 1) // bpc
+        dc = lab_ctx.upload(np.full(4 * nc + 64, 0xA5, dtype=np.uint8))
+        lab_ctx.compute_dev(d.ptr, n, bpc, dc.ptr)
+        got = lab_ctx.download(dc, 4 * nc + 64)
+        assert np.array_equal(got[:4 * nc], oracle_compute(data, bpc)), (bpc, n)
+        assert np.all(got[4 * nc:] == 0xA5)
+    finally:
+        lib.hdfs3x_set_variant(0)
 
 
 # every bit-exact variant (the diagnostic variant 77 gives wrong results on purpose); the lab
