@@ -24,7 +24,7 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, false>(a, tab, fold, grid_cap, s);
         case 94:  // the solo last step for overlapped verifies only (round-3 production before r3i)
             return launch_wave3<BPC, V, false, V>(a, tab, fold, grid_cap, s);
-        case 95:  // compute at bpc 512 without held stores (each round's words stored at once)
+        case 95:  // compute at bpc 512 / 4096 without held stores (each round's words stored at once)
             return launch_wave3<BPC, V, false, true, kLabNoHold>(a, tab, fold, grid_cap, s);
         case 77:  // diagnostic: production with the table lookups replaced by an XOR (wrong results)
             return launch_wave3<BPC, V, false, true, kLabNoMath>(a, tab, fold, grid_cap, s);

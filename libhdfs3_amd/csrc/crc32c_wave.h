@@ -32,7 +32,7 @@ namespace {
 // Lab-only bits of the round kernel (crc32c_experiments.hip; production passes 0):
 constexpr int kLabEarly = 1;   // prefetch issued at the start of each step, not after its rounds landed
 constexpr int kLabNoMath = 2;  // diagnostic: table lookups replaced by an XOR of the words (wrong results)
-constexpr int kLabNoHold = 4;  // compute at bpc 512: store each round's words at once (no held stores)
+constexpr int kLabNoHold = 4;  // compute at bpc 512 / 4096: store each round's words at once (no held stores)
 constexpr int kLabNoFill = 8;  // diagnostic: the slice tables are not written to LDS (wrong results)
 constexpr int kLabPrio = 16;    // s_setprio by rounds left at every launch size (production: >= kPrioMinRounds)
 constexpr int kLabNoPrio = 32;  // no s_setprio at any launch size (the round-3 production before r3y)
@@ -338,7 +338,24 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             }
         }
     };
+    // compute at bpc 4096 (one word per round) over one contiguous block: lane k % 64 keeps round k's
+    // word, and one store per 64 rounds writes them, instead of a 4-byte store per round into the read
+    // stream: 128 MiB 23.63 -> 22.54 us overlapped, 25.24 -> 24.51 barriered, 1 GiB 160.6 -> 158.8
+    // (verify 157.7; profiles/r03/reentry/r3zq_*)
+    constexpr bool kHold64 = !VERIFY && G == 64 && Walk::kContiguous && (LAB & kLabNoHold) == 0;
+    uint32_t line64 = 0;
     auto finish = [&](uint32_t k, const WView &v, uint32_t y, uint32_t want) {
+        if constexpr (kHold64) {
+            // lane 0 holds the chunk's word (group_xor)
+            if (k >= K) return;
+            const uint32_t yy = __builtin_amdgcn_readfirstlane(y);
+            line64 = lane == (k & 63) ? yy : line64;
+            if ((k & 63) == 63 || k + 1 == K) {
+                const uint32_t kk = (k & ~63u) + lane;
+                if (lane <= (k & 63)) *(gu32 *)((gu8 *)walk.view(kk).w) = line64;
+            }
+            return;
+        }
         if constexpr (kStage) {
             if (k < K && j == 0) stage[((k % kSR) * 16 + slot) * kCpw + lane / G] = y;
             return;
