@@ -513,17 +513,24 @@ def cpu_quota_cores():
 
 
 def cpu_baseline(work, seconds, bpc):
-    """Reference CPU path on this host, bounded sample of the same workload (one block): on
-    every CPU this process may run on (os.sched_getaffinity, one block range per thread) and on
-    one core."""
+    """Reference CPU path on this host, a bounded streaming sample of the same workload: the
+    rank's whole block set (8 x 128 MiB = 1 GiB, host copies of the blocks and their CRC arrays),
+    each thread verifying its own contiguous part, so every rep streams ~1 GiB from DRAM (more
+    than the host's last-level caches) instead of re-reading a cache-resident slice. Threads = the
+    cores this process may actually use (min of os.sched_getaffinity and the cgroup CPU quota),
+    and one core; each leg is sized from a two-rep pilot to run >= seconds / 3, and reports the
+    process CPU seconds it consumed (getrusage) beside its thread count."""
     import ctypes
+    import resource
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from util import PCL, oracle, ref_lib  # test infrastructure: baseline leg only
 
-    data = np.ascontiguousarray(work.data[0].cpu().numpy())
-    crc = np.ascontiguousarray(work.crc[0].cpu().numpy())
-    threads = max(1, len(os.sched_getaffinity(0)))
+    data = np.ascontiguousarray(work.data.cpu().numpy()).reshape(-1)  # [blocks, bytes] -> one stream
+    crc = np.ascontiguousarray(work.crc.cpu().numpy()).reshape(-1)    # the blocks' CRC arrays, in order
+    affinity = max(1, len(os.sched_getaffinity(0)))
+    quota = cpu_quota_cores()
+    threads = max(1, min(affinity, int(quota))) if quota else affinity
     ref = ref_lib()
     bad = ctypes.c_int64(0)
     if ref is not None and ref.ref_hw_available():
@@ -535,41 +542,44 @@ def cpu_baseline(work, seconds, bpc):
         run = lambda nthreads, reps: oracle().oracle_bench_verify(PCL, data.ctypes.data, data.nbytes, bpc,
                                                                  crc.ctypes.data, nthreads, reps, ctypes.byref(bad))
 
-    def timed(nthreads, budget):
-        t1 = run(nthreads, 1)
-        reps = max(1, int(budget / max(t1, 1e-6)))
-        t = run(nthreads, reps)
-        if bad.value != -1:
-            raise SystemExit(f"cpu baseline reported a bad chunk {bad.value} on a clean block")
-        return data.nbytes * reps / t / 2**30, reps, t
+    def cpu_s():
+        u = resource.getrusage(resource.RUSAGE_SELF)
+        return u.ru_utime + u.ru_stime
 
-    gib, reps, t = timed(threads, seconds)
-    quota = cpu_quota_cores()
-    out = {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-           "sample": f"{reps} x verify of one {data.nbytes >> 20} MiB block ({bpc} B chunks, "
-                     f"RemoteBlockReader::verifyChecksum loop) split over {threads} threads "
-                     f"(= len(os.sched_getaffinity(0))), {t:.1f} s; engine: {engine}",
-           "nproc": os.cpu_count(), "cgroup_cpu_quota_cores": quota,
-           # the threads share the cgroup's CPU quota: the rate is that many cores' worth of CPU time
-           "effective_cores": min(threads, quota) if quota else threads}
-    g1, r1, t1 = timed(1, seconds / 3)
-    out["one_core"] = {"value": round(g1, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
-                       "sample": f"{r1} x verify of the same block on 1 thread, {t1:.1f} s"}
+    def timed(fn, nthreads, budget):
+        t2 = fn(nthreads, 2)  # pilot: two reps, so thread start-up does not size the sample
+        reps = max(2, int(budget * 2 / max(t2, 1e-6)))
+        for _ in range(3):  # the pilot ran cold: resize until the sample fills its budget
+            c0 = cpu_s()
+            t = fn(nthreads, reps)
+            used = cpu_s() - c0
+            if t >= 0.8 * budget:
+                break
+            reps = max(reps + 1, int(reps * budget / max(t, 1e-6) * 1.1))
+        if bad.value != -1:
+            raise SystemExit(f"cpu baseline reported a bad chunk {bad.value} on a clean block set")
+        return {"value": round(data.nbytes * reps / t / 2**30, 3), "unit": "GiB/s", "cores": nthreads,
+                "wall_s": round(t, 2), "cpu_s": round(used, 2), "reps": reps}
+
+    budget = seconds / 3
+    allc = timed(run, threads, budget)
+    out = dict(allc, kind=kind,
+               sample=(f"{allc['reps']} x verify of the rank's {data.nbytes >> 20} MiB block set ({bpc} B chunks, "
+                       f"RemoteBlockReader::verifyChecksum loop), one contiguous part per thread, {threads} threads, "
+                       f"{allc['wall_s']} s wall, {allc['cpu_s']} CPU s; engine: {engine}"),
+               nproc=os.cpu_count(), affinity_cpus=affinity, cgroup_cpu_quota_cores=quota,
+               effective_cores=threads)
+    one = timed(run, 1, budget)
+    out["one_core"] = dict(one, kind=kind, sample=f"{one['reps']} x the same block set on 1 thread, {one['wall_s']} s")
     # the reference's production x86 engine is IntelAsmCrc32c (crc_pcl, 3-way crc32q + pclmul;
     # needs yasm, not buildable here): time its restatement too, the stronger CPU baseline
     if kind == "reference":
-        bad2 = ctypes.c_int64(0)
         fp = lambda n, reps: oracle().oracle_bench_verify(PCL, data.ctypes.data, data.nbytes, bpc, crc.ctypes.data,
-                                                          n, reps, ctypes.byref(bad2))
-        pcl = {}
-        for name, n in (("all_cores", threads), ("one_core", 1)):
-            r2 = max(1, int(seconds / 4 / max(fp(n, 1), 1e-6)))
-            t2 = fp(n, r2)
-            if bad2.value == -1:
-                pcl[name] = {"value": round(data.nbytes * r2 / t2 / 2**30, 3), "unit": "GiB/s", "cores": n}
-        out["pcl_port"] = dict(pcl, kind="port",
-                               engine="oracle crc_pcl restatement (IntelAsmCrc32c behaviour, "
-                                      "src/common/crc_iscsi_v_pcl.asm:93-340)")
+                                                          n, reps, ctypes.byref(bad))
+        out["pcl_port"] = {"all_cores": timed(fp, threads, budget / 2), "one_core": timed(fp, 1, budget / 2),
+                           "kind": "port",
+                           "engine": "oracle crc_pcl restatement (IntelAsmCrc32c behaviour, "
+                                     "src/common/crc_iscsi_v_pcl.asm:93-340)"}
     # BASELINE.json configs[0]: one 64 KiB packet (128 x 512 B chunks) through the reference
     # CPU path on one core, 10^4 repetitions timed inside the C loop
     if ref is not None and ref.ref_hw_available():
@@ -832,9 +842,9 @@ def main():
         line["compute"] = extra["compute"]
     if cpu:
         line["gpu_over_cpu"] = round(value / cpu["value"], 1)
-        line["gpu_over_cpu_note"] = (f"against {cpu['effective_cores']} effective cores "
-                                     f"({cpu['cores']} threads under a cgroup quota of {cpu['cgroup_cpu_quota_cores']})"
-                                     if cpu.get("cgroup_cpu_quota_cores") else f"against {cpu['cores']} cores")
+        line["gpu_over_cpu_note"] = (f"against the reference engine on {cpu['cores']} threads = the effective cores "
+                                     f"(affinity {cpu['affinity_cpus']} CPUs, cgroup quota "
+                                     f"{cpu['cgroup_cpu_quota_cores']}), streaming the 1 GiB block set")
         if "pcl_port" in cpu and "all_cores" in cpu["pcl_port"]:
             line["gpu_over_cpu_pcl"] = round(value / cpu["pcl_port"]["all_cores"]["value"], 1)
     print(json.dumps(line), flush=True)

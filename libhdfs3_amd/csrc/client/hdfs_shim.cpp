@@ -225,10 +225,48 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
             errno = ENOENT;  // FileNotFoundException -> ENOENT (Hdfs.cpp:243-327)
             return nullptr;
         }
-        const FileEntry &e = it->second;
+        FileEntry &e = it->second;
         if (write) {
             hdfs3_writer_opts o = fs->wopts;
             if (blocksize > 0) o.block_size = blocksize;
+            if (append) {
+                // the reference appends with the file's own block size (FileStatus::getBlockSize,
+                // OutputStreamImpl.cpp:196-230): every block but the last is full, so a file of two
+                // or more blocks states it; a caller's size that disagrees is refused, and no
+                // registered block may hold more than the size the stream will use
+                const auto &lbs = e.located_blocks.blocks;
+                if (lbs.size() >= 2) {
+                    const int64_t fbs = int64_t(lbs[0].block.num_bytes);
+                    if (blocksize > 0 && blocksize != fbs) {
+                        delete file;
+                        set_msg("append: block size differs from the file's block size");
+                        errno = EINVAL;
+                        return nullptr;
+                    }
+                    o.block_size = fbs;
+                }
+                for (size_t i = 0; i < lbs.size(); ++i) {
+                    const int64_t nb = int64_t(lbs[i].block.num_bytes);
+                    if (nb > o.block_size || (i + 1 < lbs.size() && nb != o.block_size)) {
+                        delete file;
+                        set_msg("append: the file's blocks do not match its block size");
+                        errno = EINVAL;
+                        return nullptr;
+                    }
+                }
+                // addBlock never hands out a block the file already has: a pipeline table still
+                // naming one of the file's blocks was left from an earlier write (the table is
+                // consumed by each write, so appends register fresh blocks)
+                if (e.pipeline)
+                    for (const hdfs3_located_block &pbk : e.pipeline_blocks.blocks)
+                        for (const hdfs3_located_block &fb : lbs)
+                            if (pbk.block.block_id == fb.block.block_id) {
+                                delete file;
+                                set_msg("append: the registered pipeline names a block the file already has");
+                                errno = EINVAL;
+                                return nullptr;
+                            }
+            }
             // OutputStreamImpl::open rejects a block size that is not a multiple of the chunk
             // size (Hdfs.cpp:686-696) before anything reaches the pipeline
             if (o.bytes_per_checksum == 0 || o.block_size % o.bytes_per_checksum != 0) {
@@ -268,6 +306,13 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
                                              fs->client_name.c_str(), o.bytes_per_checksum, nullptr, &file->pipe);
                 }
                 if (rc == 0) rc = hdfs3_output_open_pipeline_append(&o, append ? &ai : nullptr, file->pipe, &file->out);
+                if (rc == 0) {
+                    // addBlock's blocks and updateBlockForPipeline's stamp are one write's: the next
+                    // write or append registers its own (hdfs3_fs_set_pipeline / _set_append_stamp)
+                    e.pipeline = false;
+                    e.pipeline_blocks = BlockTable();
+                    if (last) e.append_gs = 0;
+                }
             } else {
                 rc = hdfs3_output_open_append(&o, append ? &ai : nullptr, e.sink, e.user, &file->out);
             }

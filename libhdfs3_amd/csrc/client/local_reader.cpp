@@ -29,6 +29,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <climits>
 #include <atomic>
 #include <cerrno>
 #include <condition_variable>
@@ -37,6 +38,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -186,7 +188,9 @@ struct hdfs3_local_reader {
         default:
             return sticky(-EIO, "LocalBlockReader cannot recognize checksum type: " + std::to_string(checksum_type));
         }
-        if (verify && (chunk_size == 0 || chunk_size > (64u << 20)))
+        // LocalBlockReader.cpp:100-115 reads bytesPerChecksum as a signed int and rejects only
+        // chunkSize <= 0; a chunk above 1 GiB then fails the local buffer bound at open
+        if (verify && (chunk_size == 0 || chunk_size > uint32_t(INT32_MAX)))
             return sticky(-EIO, "LocalBlockReader get an invalid checksum parameter, bytes per check: " +
                                     std::to_string(chunk_size));
         return 0;
@@ -465,9 +469,7 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
         // the windows are pinned from a thread bound to the GPU's NUMA node (numa.h), so the
         // block file's pages are read into memory next to the GPU that DMAs them
         bool ok = true;
-        std::thread([&] {
-            (void)hipSetDevice(device);
-            bind_thread_to_device(device);
+        auto alloc_windows = [&] {
             for (Window &w : r->slot) {
                 PacketArena &a = w.a;
                 if (hipHostMalloc(reinterpret_cast<void **>(&a.h), r->cap_data + crc_bytes, pinned_host_flags()) !=
@@ -482,7 +484,20 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
                 }
                 a.cap = r->cap_data + crc_bytes;
             }
-        }).join();
+        };
+        if (!numa_binding_enabled()) {
+            alloc_windows();  // binding off (the default): the caller's thread, under the guard
+        } else {
+            try {
+                std::thread([&] {
+                    (void)hipSetDevice(device);
+                    bind_thread_to_device(device);
+                    alloc_windows();
+                }).join();
+            } catch (const std::system_error &) {
+                ok = false;  // no thread: never let the exception cross the extern "C" entry point
+            }
+        }
         if (!ok) return bail(fail(-ENOMEM, "LocalBlockReader: window allocation failed"));
     }
     if (int rc = hdfs3_crc_ctx_set_checksum_type(r->ctx, r->engine_type())) return bail(rc);

@@ -314,6 +314,13 @@ struct hdfs3_output_stream {
     int init_append(int64_t file_length, int64_t last_block_bytes) {
         cursor = last_flushed = file_length;
         if (last_block_bytes < 0) return 0;
+        // The reference takes blockSize from the file's FileStatus, so bytesWritten < blockSize
+        // and the last block holds file_length % blockSize bytes by construction. Here both come
+        // from the caller: a block size that disagrees with the file's would make the block's
+        // remaining room negative (and the copy length wrap), so it is refused up front.
+        if (last_block_bytes >= block_size || last_block_bytes % block_size != file_length % block_size)
+            return fail(-EINVAL, "OutputStreamImpl: the last block's length does not match the file "
+                                 "length and block size.");
         const int64_t free_in_block = block_size - file_length % block_size;
         if (free_in_block == block_size)
             return fail(-EIO, "OutputStreamImpl: the last block for the file is full.");

@@ -375,6 +375,7 @@ static std::string encode_datanode(const DatanodeAddr &d) {
     put_uint(id, 6, d.ipc_port);
     std::string info;
     put_bytes(info, 1, id);
+    put_bytes(info, 8, d.location);  // always set by the reference (DataTransferProtocolSender.cpp:89)
     return info;
 }
 
@@ -398,6 +399,8 @@ static bool decode_datanode(const std::string &s, DatanodeAddr &d) {
                 else i.skip(w2);
             }
             if (!i.ok) return false;
+        } else if (field == 8 && wt == 2) {
+            d.location = r.bytes();
         } else {
             r.skip(wt);
         }

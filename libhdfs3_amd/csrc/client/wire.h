@@ -128,6 +128,7 @@ struct DatanodeAddr {              // DatanodeInfoProto.id (hdfs.proto:49-60,72-
     uint32_t xfer_port = 0;
     uint32_t info_port = 0;
     uint32_t ipc_port = 0;
+    std::string location;          // DatanodeInfoProto.location (field 8), set by BuildNodeInfo
 };
 // BlockConstructionStage (Pipeline.h:50-70)
 enum BlockConstructionStage : int {

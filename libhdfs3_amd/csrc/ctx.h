@@ -81,7 +81,7 @@ namespace hdfs3crc {
 int ctx_acquire(int device, hdfs3_crc_ctx **out, bool deep = false);
 // release: synchronizes the ctx's stream; pooled when that succeeds and the pool has room.
 void ctx_release(hdfs3_crc_ctx *ctx);
-// the pinned bytes the pool may retain (HDFS3_POOL_PINNED_MAX, default 512 MiB)
+// the pinned bytes the pool may retain (HDFS3_POOL_PINNED_MAX, default 1 GiB)
 uint64_t pool_pinned_cap_bytes();
 }  // namespace hdfs3crc
 

@@ -547,9 +547,17 @@ uint64_t pool_pinned_cap() {
         if (!e || !*e) return kPoolPinnedDefault;
         char *end = nullptr;
         const unsigned long long v = std::strtoull(e, &end, 10);
-        if (end == e) return kPoolPinnedDefault;
         const int shift = *end == 'K' || *end == 'k' ? 10 : *end == 'M' || *end == 'm' ? 20
                           : *end == 'G' || *end == 'g' ? 30 : 0;
+        // a whole number with at most one K/M/G suffix; anything else ("1.5G", "64MiB", "-1")
+        // is not silently read as a prefix of itself: the default stays and a warning says so
+        const char *rest = end + (shift ? 1 : 0);
+        if (end == e || *e == '-' || *rest != '\0' || (shift && v > (~0ull >> shift))) {
+            std::fprintf(stderr, "libhdfs3_crc: HDFS3_POOL_PINNED_MAX=\"%s\" is not a byte count "
+                                 "(digits with an optional K/M/G suffix); using the default %llu bytes\n",
+                         e, (unsigned long long)kPoolPinnedDefault);
+            return kPoolPinnedDefault;
+        }
         return uint64_t(v) << shift;
     }();
     return cap;

@@ -18,6 +18,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -171,7 +172,12 @@ int hdfs3_multi_create(const int *devices, int n_devices, hdfs3_multi **out) {
             hdfs3_multi_destroy(m);
             return rc;
         }
-        wk->th = std::thread([wk] { wk->run(); });
+        try {
+            wk->th = std::thread([wk] { wk->run(); });
+        } catch (const std::system_error &) {  // never across the extern "C" boundary
+            hdfs3_multi_destroy(m);
+            return fail(-EAGAIN, "worker thread for device %d could not be started", devices[i]);
+        }
     }
     *out = m;
     return 0;
@@ -189,7 +195,7 @@ void hdfs3_multi_destroy(hdfs3_multi *m) {
             wk->th.join();
         }
         if (wk->ctx) {
-            (void)hipSetDevice(wk->device);
+            hdfs3crc::DeviceGuard guard(wk->device);  // the caller's current device is left as it was
             hdfs3_crc_ctx_destroy(wk->ctx);
             if (wk->d_res) (void)hipFree(wk->d_res);
             if (wk->h_res) (void)hipHostFree(wk->h_res);

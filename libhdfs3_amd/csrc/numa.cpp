@@ -131,6 +131,8 @@ int bind_thread_to_device(int device) {
 
 unsigned pinned_host_flags() { return enabled() ? hipHostMallocNumaUser : hipHostMallocDefault; }
 
+bool numa_binding_enabled() { return enabled(); }
+
 }  // namespace hdfs3crc
 
 extern "C" {

@@ -5,7 +5,7 @@
 // GPU's own node. The worker thread of each device (multi_device.cpp), the block readers' receiver
 // threads and the local readers' loader threads bind themselves to the CPUs of their device's node
 // (intersected with the process's allowed CPUs) before they allocate pinned staging, which then
-// follows the thread's node (hipHostMallocNumaUser). HDFS3_NUMA=0 turns it off. Not installed.
+// follows the thread's node (hipHostMallocNumaUser). Opt-in: only HDFS3_NUMA=1 turns it on. Not installed.
 #pragma once
 
 #include <sched.h>
@@ -22,5 +22,7 @@ bool node_cpus(const char *sysfs_root, int node, cpu_set_t *out);
 int bind_thread_to_device(int device);
 // hipHostMalloc flags for pinned staging allocated by a thread bound as above
 unsigned pinned_host_flags();
+// HDFS3_NUMA=1: binding is on (off by default)
+bool numa_binding_enabled();
 
 }  // namespace hdfs3crc

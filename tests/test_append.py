@@ -283,3 +283,86 @@ def test_gpu_hdfs_append_missing_file_is_enoent():
         assert not f and ctypes.get_errno() == errno.ENOENT
     finally:
         h.close()
+
+
+@pytest.mark.gpu
+def test_gpu_hdfs_append_block_size_must_match_the_file(nodes):
+    """ADVICE r3 (high): the block size an append uses is the file's (FileStatus::getBlockSize in
+    OutputStreamImpl.cpp:196-230). A caller's size that disagrees with a file of two or more
+    blocks, or a file whose only block is larger than the stream's block size, is refused with
+    EINVAL before anything is written (the copy length into the packet arena used to wrap); a
+    filesystem whose default block size differs from the file's appends with the file's."""
+    import errno
+
+    chain = [(HOST, d.port) for d in nodes]
+    blocks, data = existing_file(nodes, 2 * BS + 700, 900, 21)
+    h = Hdfs(block_size=BS // 2)  # the fs default disagrees with the file's BS
+    try:
+        path = b"/append/bs"
+        h.add_file(path, [(bid, n, chain) for bid, n in blocks])
+        f = h.lib.hdfsOpenFile(h.fs, path, os.O_WRONLY | os.O_APPEND, 0, 0, 2 * BS)
+        assert not f and ctypes.get_errno() == errno.EINVAL
+        extra = splitmix_bytes(5000, 22)
+        assert h.write_file(path, os.O_WRONLY | os.O_APPEND, [extra]) == data.size  # the file's BS
+        whole = np.concatenate([data, extra])
+        assert np.array_equal(h.read_file(path, whole.size), whole)
+        # one block bigger than the stream's block size: refused, nothing sent
+        one, _ = existing_file(nodes, BS - 100, 950, 23)
+        h2 = Hdfs(block_size=BS // 4)
+        try:
+            h2.add_file(b"/append/one", [(bid, n, chain) for bid, n in one])
+            f = h2.lib.hdfsOpenFile(h2.fs, b"/append/one", os.O_WRONLY | os.O_APPEND, 0, 0, 0)
+            assert not f and ctypes.get_errno() == errno.EINVAL
+        finally:
+            h2.close()
+    finally:
+        h.close()
+
+
+@pytest.mark.gpu
+def test_gpu_output_open_append_rejects_last_block_beyond_block_size():
+    """hdfs3_output_open_append: last_block_bytes must be < block_size and agree with
+    file_length mod block_size (-EINVAL otherwise), so a block's remaining room is never negative."""
+    import errno
+
+    from libhdfs3_amd import _native
+
+    lib = _native.lib()
+    opts = _native.WriterOpts(0, 512, 65536, BS, 8)
+    sink = _native.PACKET_SINK(lambda u, p, n, i: 0)
+    for file_length, last in ((3 * BS + 10, BS + 10), (BS + 10, 30), (5 * BS, BS)):
+        ai = _native.AppendInfo(file_length, last)
+        out = ctypes.c_void_p()
+        rc = lib.hdfs3_output_open_append(ctypes.byref(opts), ctypes.byref(ai), sink, None, ctypes.byref(out))
+        assert rc == -errno.EINVAL, (file_length, last, rc)
+        assert not out.value
+
+
+@pytest.mark.gpu
+def test_gpu_hdfs_second_append_without_new_stamp_or_pipeline(nodes):
+    """ADVICE r3 (medium/low): a write consumes the pipeline table and the append stamp it used.
+    A second append that registers neither continues the last block with the last stamp + 1 and
+    no block id is reused; a stale table naming one of the file's blocks is refused."""
+    import errno
+
+    h = Hdfs()
+    try:
+        chain = [(HOST, d.port) for d in nodes]
+        path = b"/append/twice"
+        first = splitmix_bytes(BS + 300, 31)
+        h.set_pipeline(path, [(830 + i, chain) for i in range(2)])
+        h.write_file(path, os.O_WRONLY | os.O_CREAT, [first])
+        a1, a2 = splitmix_bytes(900, 32), splitmix_bytes(1500, 33)
+        assert h.lib.hdfs3_fs_set_append_stamp(h.fs, path, 40) == 0
+        assert h.write_file(path, os.O_WRONLY | os.O_APPEND, [a1]) == first.size
+        # neither a stamp nor a pipeline registered: the last block, stamp 41
+        assert h.write_file(path, os.O_WRONLY | os.O_APPEND, [a2]) == first.size + a1.size
+        assert all(d.block_gs(831) == 41 for d in nodes)
+        whole = np.concatenate([first, a1, a2])
+        assert np.array_equal(h.read_file(path, whole.size), whole)
+        # a table naming the file's own block 831 is an addBlock that cannot happen
+        h.set_pipeline(path, [(831, chain)])
+        f = h.lib.hdfsOpenFile(h.fs, path, os.O_WRONLY | os.O_APPEND, 0, 0, 0)
+        assert not f and ctypes.get_errno() == errno.EINVAL
+    finally:
+        h.close()

@@ -224,7 +224,13 @@ def test_compute_held_stores_past_64_rounds_per_wave(gpu_ctx, n):
                                    (512, 4096 * 33 + 100), (1024, 1 << 30), (1024, (1 << 30) + 4096),
                                    (1024, (128 << 20) + 4096 * 3 + 517), (1024, 4096 * 33 + 100),
                                    (2048, 2 << 30), (2048, (2 << 30) + 4096), (2048, (512 << 20) + 4096 * 5 + 1000),
-                                   (2048, 4096 * 33 + 100)])
+                                   (2048, 4096 * 33 + 100),
+                                   # bpc 4096 holds one word per round in lane k % 64 of one VGPR and
+                                   # stores a line per 64 rounds (crc32c_wave.h:341-357): exactly
+                                   # 64 / 128 rounds per wave, waves of 65 (kr > 0, a partial second
+                                   # line) and 129 rounds with a slow region and a short tail
+                                   (4096, 1 << 30), (4096, (1 << 30) + 4096 * 5 + 300), (4096, 2 << 30),
+                                   (4096, (2 << 30) + 4096 * 13), (4096, 4096 * 33 + 100)])
 @pytest.mark.parametrize("overlap", [False, True])
 def test_compute_staged_words_boundaries(gpu_ctx, bpc, n, overlap):
     """Compute at bpc 512 / 1024 / 2048 over a contiguous block whose waves have at most bpc / 16

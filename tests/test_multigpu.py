@@ -170,3 +170,39 @@ def test_config4_sharding_at_size_on_one_gpu(gpu_ctx):
         assert list(bad) == [k for _, k in flips]
     finally:
         lib.hdfs3_multi_destroy(m)
+
+
+@pytest.mark.gpu
+def test_bench_gpus_8_driver_command_rehearsed_on_one_gpu():
+    """The driver's 8-GPU command (`bench.py --gpus 8 --steps 20 --warmup 5`) at its default size,
+    8 ranks x 8 x 128 MiB each, rehearsed on the one-GPU box: all 8 ranks on cuda:0, gloo for the
+    timing collectives. The line proves its world (8 ranks, 8 distinct block sets) and value is
+    8 x the slowest rank's rate (weak scaling: every rank verifies its own K blocks). The unit
+    sharded is the reference's per-block verify (InputStreamImpl.cpp:616-708)."""
+    j = _bench("--gpus", "8", "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--no-pmc", timeout=540)
+    assert j["n_gpus"] == 8 and j["world_size"] == 8 and j["backend"] == "gloo"
+    ranks = j["per_rank"]
+    assert sorted(r["rank"] for r in ranks) == list(range(8))
+    assert len({r["seed"] for r in ranks}) == 8
+    assert all(r["current_device"] == 0 for r in ranks)  # one GPU here
+    assert j["config"]["block_bytes"] == 128 << 20 and j["config"]["blocks_rotated_per_gpu"] == 8
+    slowest = max(r["ms_per_step"] for r in ranks)
+    assert j["ms_per_step"] == pytest.approx(slowest, rel=1e-3)
+    assert j["value"] == pytest.approx(8 * min(r["value"] for r in ranks), rel=1e-3)
+
+
+@pytest.mark.gpu
+def test_multi_create_destroy_keeps_callers_device():
+    """hdfs3_multi_create / _destroy leave the calling thread's current device as it was (VERDICT r3:
+    destroy used to switch to each worker's device and never switch back). On a node every visible
+    device is tried as the caller's, with the workers on all of them; on the one-GPU box device 0."""
+    import torch
+
+    n = torch.cuda.device_count()
+    for cur in range(n):
+        torch.cuda.set_device(cur)
+        lib, m = _multi(list(range(n))[::-1] + [cur])
+        assert torch.cuda.current_device() == cur
+        lib.hdfs3_multi_destroy(m)
+        assert torch.cuda.current_device() == cur
+    torch.cuda.set_device(0)
