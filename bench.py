@@ -64,6 +64,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-compute", action="store_true", help="skip the compute-on-write block of the line")
+    p.add_argument("--no-packets", action="store_true", help="skip the packet-stream block of the line")
     p.add_argument("--sweep", action="store_true", help="extra diagnostics on stderr")
     p.add_argument("--graph", action="store_true",
                    help="replay the K steps from captured HIP graphs instead of launching them eagerly "
@@ -381,6 +382,94 @@ def compute_block(torch, work, ctx, K, warm, stream, read_ceilings):
             raise SystemExit(f"PARITY FAILURE: compute block {b} chunk {bad} differs from the oracle")
     res["checked"] = f"every CRC word of {min(K, work.blocks)} blocks against the oracle after the timed region"
     return res
+
+
+def packets_block(torch, work, ctx, K, W, stream, reps=3):
+    """Verify-on-read over synthetic DATA-TRANSFER PACKET STREAMS (north_star: "device-resident
+    throughput on synthetic packet streams"; RemoteBlockReader.cpp:240-245, 306-326). The same 1 GiB
+    payload as `value`, laid out as the block reader lays packets into its device arenas
+    (block_reader.cpp: the 31-byte header is parsed on the host, each packet's 128 BE32 words then
+    its 64 KiB of data, 16 B aligned): 16,384 packets at a 66,048-byte pitch. One launch verifies
+    2,048 packets = 128 MiB of payload (one block's worth, the unit of `value`) through
+    hdfs3_crc32c_verify_packet_stream_dev_async, rotating over the 8 streams of the arena. Timed in
+    `value`'s form (W warmup, settle, K launches between HIP events, the first barriered, the rest
+    overlapped; and all barriered), and paired with contiguous-block verifies in identical regions
+    (`reps` x (packets, contiguous); medians), so frac_vs_contiguous carries no box drift. Every
+    launch's result slot is checked after timing; before it, one flipped bit must come back as its
+    (packet, chunk)."""
+    npk, pitch, cpp, bpc = 2048, 512 + 65536, 128, work.bpc
+    if bpc != 512 or work.block_bytes != npk * 65536:
+        return None
+    nstreams = work.blocks
+    arena = torch.empty((nstreams * npk, pitch), dtype=torch.uint8, device=work.data.device)
+    arena[:, 512:] = work.data.view(-1, 65536)
+    arena[:, :512] = work.crc.view(-1, 4 * cpp)
+    torch.cuda.synchronize()
+    base = arena.data_ptr()
+    span = npk * pitch
+    ps = ctx.packet_stream(0, 512, pitch, npk, 65536)
+    res = torch.zeros(max(K, 256), dtype=torch.int64, device=work.data.device)
+    rp = res.data_ptr()
+    # the gate: a flipped bit in packet 777 chunk 45 of stream 3
+    pk_, ch_ = 777, 45
+    pos = (3 * npk + pk_, 512 + ch_ * 512 + 100)
+    orig = int(arena[pos].item())
+    arena[pos] = orig ^ 0x10
+    torch.cuda.synchronize()
+    ctx.verify_packet_stream_async(base + 3 * span, span, ps, bpc, rp)
+    torch.cuda.synchronize()
+    got = int(res[0].item())
+    arena[pos] = orig
+    res.zero_()
+    torch.cuda.synchronize()
+    if got == 0 or ((~got) & (2**64 - 1)) != (pk_ << 32) | ch_:
+        raise SystemExit(f"PARITY FAILURE: packet stream reported {got:#x} for a flip in packet {pk_} chunk {ch_}")
+    dp, cp, nb, bb = work._dp, work._cp, work.blocks, work.block_bytes
+    alg = work.nchunks * (bpc + 4)
+
+    def pk_launch(i, slot, overlap):
+        ctx.verify_packet_stream_async(base + (i % nstreams) * span, span, ps, bpc, rp + 8 * slot,
+                                       overlap_previous=overlap and i > 0)
+
+    def blk_launch(i, slot, overlap):
+        ctx.verify_dev_async(dp[i % nb], bb, bpc, cp[i % nb], rp + 8 * slot, overlap_previous=overlap and i > 0)
+
+    def region(fn, n, warm, overlap):
+        for i in range(warm):
+            fn(i, i % res.numel(), overlap)
+        settle(torch, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(n):
+            fn(i, i % res.numel(), overlap)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e-3 / n
+
+    out = {"api": "hdfs3_crc32c_verify_packet_stream_dev_async",
+           "layout": f"{nstreams * npk} packets of 64 KiB, [128 BE32 words][64 KiB data] at a {pitch}-byte pitch "
+                     f"(the block reader's device arena), {npk} packets (128 MiB payload) per launch",
+           "alg_bytes_per_launch": alg,
+           "timing": "HIP events on the launch stream around K launches (the clock of value)"}
+    for name, overlap in (("overlapped", True), ("barriered", False)):
+        t = region(pk_launch, K, max(W, 1), overlap)
+        r = {"value": round(bb / t / 2**30, 2), "unit": "GiB/s", "avg_launch_us": round(t * 1e6, 2),
+             "achieved_GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}
+        n = max(K, 200)
+        pk, bl = [], []
+        for _ in range(reps):
+            pk.append(region(pk_launch, n, 50, overlap))
+            bl.append(region(blk_launch, n, 50, overlap))
+        pm, bm = sorted(pk)[reps // 2], sorted(bl)[reps // 2]
+        r["paired"] = {"launches": n, "packets_us": round(pm * 1e6, 2), "contiguous_us": round(bm * 1e6, 2),
+                       "how": f"{reps} x (packet region, contiguous region), 50 warmup + settle + {n} timed each; medians"}
+        r["frac_vs_contiguous"] = round(bm / pm, 4)
+        out[name] = r
+    if bool((res != 0).any().item()):
+        raise SystemExit("PARITY FAILURE: clean packets reported a bad chunk in the packet-stream regions")
+    out["checked"] = "every launch's result slot after the timed regions; a flipped bit located before them"
+    del arena
+    return out
 
 
 def paired_regions(torch, work, ctx, stream, n, overlap, dst, reps=3):
@@ -796,6 +885,11 @@ def main():
                 v = roofline["frac"] if m == "overlapped" else (barriered or {}).get("frac")
                 if v:
                     extra["compute"][m]["frac_vs_verify"] = round(extra["compute"][m]["frac"] / v, 4)
+        if args.mode == "verify" and not args.no_packets:
+            pk = packets_block(torch, work, ctx, K, W, stream)
+            if pk:
+                pk["overlapped"]["frac_vs_value"] = round(pk["overlapped"]["frac"] / roofline["frac"], 4)
+                extra["packets"] = pk
         try:
             extra["batched"] = batched_rate(torch, work, ctx, args.mode)
         except SystemExit:
@@ -838,6 +932,8 @@ def main():
         line["barriered"] = extra["barriered"]
     if "batched" in extra:
         line["batched"] = extra["batched"]
+    if "packets" in extra:
+        line["packets"] = extra["packets"]
     if "compute" in extra:
         line["compute"] = extra["compute"]
     if cpu:

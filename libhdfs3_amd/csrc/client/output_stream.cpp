@@ -318,12 +318,12 @@ struct hdfs3_output_stream {
         // and the last block holds file_length % blockSize bytes by construction. Here both come
         // from the caller: a block size that disagrees with the file's would make the block's
         // remaining room negative (and the copy length wrap), so it is refused up front.
-        if (last_block_bytes >= block_size || last_block_bytes % block_size != file_length % block_size)
-            return fail(-EINVAL, "OutputStreamImpl: the last block's length does not match the file "
-                                 "length and block size.");
         const int64_t free_in_block = block_size - file_length % block_size;
         if (free_in_block == block_size)
             return fail(-EIO, "OutputStreamImpl: the last block for the file is full.");
+        if (last_block_bytes >= block_size || last_block_bytes != file_length % block_size)
+            return fail(-EINVAL, "OutputStreamImpl: the last block's length does not match the file "
+                                 "length and block size.");
         is_append = true;
         bytes_written = last_block_bytes;
         const uint32_t used_in_cksum = uint32_t(file_length % bpc);

@@ -693,6 +693,38 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_packets_kernel(
 
 // Coalesced streaming read (1 KiB per wave-instruction): the achievable HBM read
 // ceiling the CRC kernel is compared with.
+#if HDFS3_LAB
+// Lab-only clock stamps (hdfs3x_clock_stamps, tools/clock_ramp.py): thread 0 of workgroup 0 of every
+// launch of a stamping kernel records {s_memtime, s_memrealtime} at its start and end into the next
+// slot of g_lab_clk (4 words per launch). s_memtime counts the shader clock and s_memrealtime a fixed
+// 100 MHz, so the ratio of their deltas is the shader clock over that workgroup's lifetime. Vector
+// stores and a vector atomic only; nothing when no buffer is set.
+__device__ unsigned long long *g_lab_clk = nullptr;
+__device__ unsigned int g_lab_clk_cap = 0;
+__device__ unsigned int g_lab_clk_n = 0;
+struct LabClock {
+    unsigned long long t0 = 0, r0 = 0;
+    __device__ __forceinline__ void start() {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            t0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    __device__ __forceinline__ void end() {
+        if (blockIdx.x == 0 && threadIdx.x == 0 && g_lab_clk) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            const unsigned int i = atomicAdd(&g_lab_clk_n, 1u);
+            if (i < g_lab_clk_cap) {
+                g_lab_clk[4 * i] = t0;
+                g_lab_clk[4 * i + 1] = r0;
+                g_lab_clk[4 * i + 2] = t1;
+                g_lab_clk[4 * i + 3] = r1;
+            }
+        }
+    }
+};
+#endif
+
 template <bool NT>
 __global__ __launch_bounds__(256) void stream_read_kernel(const uint8_t *__restrict__ d,
                                                           uint64_t n16, uint32_t *sink) {
@@ -700,6 +732,10 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const uint8_t *__restr
         if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
         return ld16(p);
     };
+#if HDFS3_LAB
+    LabClock clk;
+    clk.start();
+#endif
     uint32_t acc = 0;
     const uint64_t stride = uint64_t(gridDim.x) * 256;
     uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -714,6 +750,9 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const uint8_t *__restr
         acc ^= a.x ^ a.y ^ a.z ^ a.w;
     }
     if (acc == 0x9E3779B9u) sink[0] = acc;  // keep the loads live
+#if HDFS3_LAB
+    clk.end();
+#endif
 }
 
 // Access-pattern probes (xor instead of table arithmetic), selected by `variant`:

@@ -57,6 +57,8 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabNoStage>(a, tab, fold, grid_cap, s);
         case 130:  // compute: staged words at every size, written out window by window (kLabStageWin)
             return launch_wave3<BPC, V, false, true, kLabStageWin>(a, tab, fold, grid_cap, s);
+        case 125:  // production with clock stamps of workgroup 0 (kLabClock; tools/clock_ramp.py)
+            return launch_wave3<BPC, V, false, true, kLabClock>(a, tab, fold, grid_cap, s);
         case 78:  // diagnostic: 77 without the slice-table LDS fill
             return launch_wave3<BPC, V, false, true, kLabNoMath | kLabNoFill>(a, tab, fold, grid_cap, s);
         default: return hipErrorInvalidValue;
@@ -89,6 +91,18 @@ hipError_t launch_experiment(int variant, const ChunkLaunch &a, bool verify, con
 }
 
 void set_variant(int v) { g_variant = v; }
+
+hipError_t lab_clock_buffer(unsigned long long *d, unsigned int cap, unsigned int *n_out) {
+    // read the count of the previous buffer first, then install the new one with a zero count
+    unsigned int n = 0;
+    hipError_t e = hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_lab_clk_n), sizeof n);
+    if (e != hipSuccess) return e;
+    if (n_out) *n_out = n;
+    const unsigned int zero = 0;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_lab_clk), &d, sizeof d)) != hipSuccess) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_lab_clk_cap), &cap, sizeof cap)) != hipSuccess) return e;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_lab_clk_n), &zero, sizeof zero);
+}
 
 hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,
                               hipStream_t stream, bool overlap_previous) {

@@ -38,6 +38,7 @@ hipError_t launch_p(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
 #if HDFS3_LAB
     if (g_variant == 115) return launch_wave3<BPC, V, true, false, kLabPrio>(a, tab, fold, grid_cap, s);
     if (g_variant == 117) return launch_wave3<BPC, V, true, false, kLabNoPrio>(a, tab, fold, grid_cap, s);
+    if (g_variant == 124) return launch_wave3<BPC, V, true, true>(a, tab, fold, grid_cap, s);  // solo last step
 #endif
     return launch_wave3<BPC, V, true, false>(a, tab, fold, grid_cap, s);
 }

@@ -40,6 +40,7 @@ constexpr int kLabNoStore = 64;     // diagnostic, compute: the held words are n
 constexpr int kLabNearStore = 128;  // diagnostic, compute: every flush stores to the wave's first round's words
 constexpr int kLabNoStage = 1024;   // compute: held stores even where production stages the words (kStageWords)
 constexpr int kLabStageWin = 2048;  // compute at bpc 512: staged words past kStageMaxRounds too, window by window
+constexpr int kLabClock = 4096;     // clock stamps of workgroup 0 (LabClock, crc32c_device.h; lab builds only)
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
 // written as whole lines, §4.1; past the window size in windows)
@@ -576,6 +577,10 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
     constexpr bool kHold = !VERIFY && BPC == 512 && (LAB & kLabNoHold) == 0;
     // the wave's round count from the host's split (ChunkLaunch::kq/kr): SALU only
     const uint32_t K = a.kq + (wave < a.kr ? 1u : 0u);
+#if HDFS3_LAB
+    LabClock clk;
+    if constexpr ((LAB & kLabClock) != 0) clk.start();
+#endif
     if constexpr (PITCH) {
         PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves, K, a.upp_log2,
                           dummy};
@@ -590,6 +595,9 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
         if (a.len % kRoundBytes)  // wave-uniform: a block of whole rounds has no slow region
             slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     }
+#if HDFS3_LAB
+    if constexpr ((LAB & kLabClock) != 0) clk.end();
+#endif
 }
 
 // A list of segments (blocks of a batch, packets of a descriptor list): the core over a SegWalk,
@@ -670,7 +678,7 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
             return launch_wave3<BPC, V, PITCH, SOLO, LAB | kStageWords, TPB>(a, tab, fold, grid_cap, s);
     }
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
-        if constexpr (SOLO && !PITCH) {
+        if constexpr (SOLO) {
             if (units * kRoundBytes <= kSoloTailMaxBytes) {
                 hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LAB, TPB>), dim3(grid),
                                       dim3(TPB), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, b, tab, nib);

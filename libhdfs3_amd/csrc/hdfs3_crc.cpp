@@ -1091,5 +1091,14 @@ int hdfs3x_grid_cap(hdfs3_crc_ctx *ctx) { return ctx ? ctx->grid_cap : 0; }
 // Process-wide kernel-variant knob for in-process A/B measurements (tools/ab.py).
 void hdfs3x_set_variant(int v) { set_variant(v); }
 
+// Clock stamps of variant 125 and the stream-read kernel (tools/clock_ramp.py): installs a device
+// buffer of cap x 4 u64 ({s_memtime, s_memrealtime} at workgroup 0's start and end, one slot per
+// launch); returns the number of stamps written into the previous buffer, or a negative errno.
+int hdfs3x_clock_stamps(void *d_buf, unsigned int cap) {
+    unsigned int n = 0;
+    HIP_TRY(lab_clock_buffer(static_cast<unsigned long long *>(d_buf), cap, &n));
+    return int(n);
+}
+
 }  // extern "C"
 #endif  // HDFS3_LAB

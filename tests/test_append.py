@@ -322,7 +322,9 @@ def test_gpu_hdfs_append_block_size_must_match_the_file(nodes):
 @pytest.mark.gpu
 def test_gpu_output_open_append_rejects_last_block_beyond_block_size():
     """hdfs3_output_open_append: last_block_bytes must be < block_size and agree with
-    file_length mod block_size (-EINVAL otherwise), so a block's remaining room is never negative."""
+    file_length mod block_size (-EINVAL otherwise), so a block's remaining room is never negative.
+    A file that ends on a block boundary keeps the reference's "last block is full" EIO first
+    (OutputStreamImpl.cpp:192-199; test_output_stream.py::test_append_to_full_last_block_is_eio)."""
     import errno
 
     from libhdfs3_amd import _native
@@ -330,7 +332,7 @@ def test_gpu_output_open_append_rejects_last_block_beyond_block_size():
     lib = _native.lib()
     opts = _native.WriterOpts(0, 512, 65536, BS, 8)
     sink = _native.PACKET_SINK(lambda u, p, n, i: 0)
-    for file_length, last in ((3 * BS + 10, BS + 10), (BS + 10, 30), (5 * BS, BS)):
+    for file_length, last in ((3 * BS + 10, BS + 10), (BS + 10, 30), (5 * BS + 7, 2 * BS + 7)):
         ai = _native.AppendInfo(file_length, last)
         out = ctypes.c_void_p()
         rc = lib.hdfs3_output_open_append(ctypes.byref(opts), ctypes.byref(ai), sink, None, ctypes.byref(out))

@@ -198,3 +198,45 @@ def test_compute_word_scratch_grows_across_calls(gpu_ctx):
         want[(n - 1) * pitch + crc_off + lw:(n - 1) * pitch + data_off] = 0xA5
         assert np.array_equal(got, want), (n, last)
 
+
+
+@pytest.mark.parametrize("variant", [0, 124])
+def test_packet_stream_solo_variant_overlapped_chain(lab_ctx, variant):
+    """The pitch walk with the solo last step (lab variant 124; overlapped launches up to 256 MiB) as
+    the bench's packets block runs it: 128 MiB of 64 KiB packets at the block reader's 66,048-byte
+    pitch, and a 37-packet stream with a short last packet (slow region), chained overlapped
+    verifies each into its own result word, one arena corrupted: every word its first bad key."""
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import CrcContext, DeviceBuffer
+
+    lib = _native.lab()
+    bpc, plen = 512, 65536
+    pitch, crc_off, data_off = 512 + plen, 0, 512
+    try:
+        lib.hdfs3x_set_variant(variant)
+        for n, last in ((2048, plen), (37, 4096 * 5 + 300)):
+            host = np.random.default_rng(n + variant).integers(0, 256, size=n * pitch, dtype=np.uint8)
+            for i in range(n):
+                dl = plen if i + 1 < n else last
+                host[i * pitch + crc_off:i * pitch + crc_off + 4 * (-(-dl // bpc))] = \
+                    oracle_compute(host[i * pitch + data_off:i * pitch + data_off + dl], bpc)
+            ps = CrcContext.packet_stream(crc_off, data_off, pitch, n, plen, last)
+            arenas = [lab_ctx.upload(host) for _ in range(3)]
+            p_bad = n - 1 if n < 100 else 1500
+            q_bad = last - 7 if n < 100 else 33333
+            lab_ctx.upload(np.array([host[p_bad * pitch + data_off + q_bad] ^ 0x40], np.uint8), arenas[1],
+                           offset=p_bad * pitch + data_off + q_bad)
+            res = DeviceBuffer(12 * 8)
+            lab_ctx.memset(res, 0, 12 * 8)
+            for i in range(12):
+                lab_ctx.verify_packet_stream_async(arenas[i % 3].ptr, n * pitch, ps, bpc, res.ptr + 8 * i,
+                                                   overlap_previous=i > 0)
+            lab_ctx.synchronize()
+            for i, w in enumerate(lab_ctx.download(res, 12 * 8).view(np.uint64).tolist()):
+                if i % 3 == 1:
+                    key = lab_ctx.decode_result(int(w))
+                    assert (key >> 32, key & 0xFFFFFFFF) == (p_bad, q_bad // bpc), (variant, n, i)
+                else:
+                    assert w == 0, (variant, n, i)
+    finally:
+        lib.hdfs3x_set_variant(0)
