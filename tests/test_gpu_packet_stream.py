@@ -202,8 +202,8 @@ def test_compute_word_scratch_grows_across_calls(gpu_ctx):
 
 @pytest.mark.parametrize("variant", [0, 124])
 def test_packet_stream_solo_variant_overlapped_chain(lab_ctx, variant):
-    """The pitch walk with the solo last step (lab variant 124; overlapped launches up to 256 MiB) as
-    the bench's packets block runs it: 128 MiB of 64 KiB packets at the block reader's 66,048-byte
+    """The pitch walk with the solo last step (production since round 4 for overlapped launches up to
+    256 MiB; lab variant 124 runs it without, as before) as the bench's packets block runs it: 128 MiB of 64 KiB packets at the block reader's 66,048-byte
     pitch, and a 37-packet stream with a short last packet (slow region), chained overlapped
     verifies each into its own result word, one arena corrupted: every word its first bad key."""
     from libhdfs3_amd import _native
@@ -214,7 +214,10 @@ def test_packet_stream_solo_variant_overlapped_chain(lab_ctx, variant):
     pitch, crc_off, data_off = 512 + plen, 0, 512
     try:
         lib.hdfs3x_set_variant(variant)
-        for n, last in ((2048, plen), (37, 4096 * 5 + 300)):
+        # the 37-packet stream's last packet: 5 whole rounds, 3 whole chunks in the slow region and a
+        # short tail (which remote semantics do not check, RemoteBlockReader.cpp:319); the flip sits
+        # in the slow region's second chunk
+        for n, last in ((2048, plen), (37, 4096 * 5 + 512 * 3 + 300)):
             host = np.random.default_rng(n + variant).integers(0, 256, size=n * pitch, dtype=np.uint8)
             for i in range(n):
                 dl = plen if i + 1 < n else last
@@ -223,7 +226,7 @@ def test_packet_stream_solo_variant_overlapped_chain(lab_ctx, variant):
             ps = CrcContext.packet_stream(crc_off, data_off, pitch, n, plen, last)
             arenas = [lab_ctx.upload(host) for _ in range(3)]
             p_bad = n - 1 if n < 100 else 1500
-            q_bad = last - 7 if n < 100 else 33333
+            q_bad = 4096 * 5 + 512 + 100 if n < 100 else 33333
             lab_ctx.upload(np.array([host[p_bad * pitch + data_off + q_bad] ^ 0x40], np.uint8), arenas[1],
                            offset=p_bad * pitch + data_off + q_bad)
             res = DeviceBuffer(12 * 8)

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--spin-us", type=float, default=300.0)
     ap.add_argument("--read-grid", type=int, default=-512)
+    ap.add_argument("--kinds", default="crc,read", help="comma list of crc (verify), compute, read")
+    ap.add_argument("--phases", default="bench,steady,busy,queued")
     args = ap.parse_args()
 
     import numpy as np
@@ -69,6 +71,12 @@ def main():
     def crc_launch(i, overlap):
         ctx.verify_dev_async(dp[i % nb], bb, bpc, cp[i % nb], rp + 8 * (i % 8192), overlap_previous=overlap and i > 0)
 
+    scratch = torch.empty_like(crc)
+    sp = [scratch[b].data_ptr() for b in range(nb)]
+
+    def compute_launch(i, overlap):
+        ctx.compute_dev(dp[i % nb], bb, bpc, sp[i % nb], overlap_previous=overlap and i > 0)
+
     def read_launch(i, overlap):
         lib.hdfs3x_stream_read_ex(ctx.ctx, dp[i % nb], bb, args.read_grid, sink.data_ptr(), int(overlap and i > 0))
 
@@ -103,8 +111,10 @@ def main():
     out = []
     K, W = args.k, args.w
     for rep in range(args.reps):
-        for kind, fn in (("crc", crc_launch), ("read", read_launch)):
-            lib.hdfs3x_set_variant(125 if kind == "crc" else 0)
+        kinds = {"crc": crc_launch, "compute": compute_launch, "read": read_launch}
+        for kind in args.kinds.split(","):
+            fn = kinds[kind]
+            lib.hdfs3x_set_variant(0 if kind == "read" else 125)
 
             def pre_bench():
                 for i in range(2000):
@@ -129,6 +139,8 @@ def main():
 
             for phase, pre, k in (("bench", pre_bench, K), ("steady", pre_steady, max(K, 200)),
                                   ("busy", pre_busy, K), ("queued", pre_queued, K)):
+                if phase not in args.phases.split(","):
+                    continue
                 if phase in ("busy", "queued"):
                     # no host sync between pre() and the region: region() syncs after pre(), so inline
                     lib.hdfs3x_clock_stamps(None, 0)
