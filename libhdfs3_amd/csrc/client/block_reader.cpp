@@ -47,7 +47,11 @@ constexpr int kSlots = 3;                  // receiving / verifying / delivering
 constexpr int kMaxSlots = 64;              // deepest ring (read-ahead of a whole block)
 constexpr int32_t kMaxPacketData = 16 << 20;  // PacketReceiver.MAX_PACKET_SIZE (Hadoop)
 constexpr size_t kArenaCacheMax = 6;       // arenas a ctx keeps for its next reader
-constexpr size_t kPacketGuess = 64 * 1024 + 16 * 1024;  // 64 KiB payload + CRCs + alignment
+// a batch arena's room per packet: the datanode's default 64 KiB packet, its 128 words at bpc 512 and
+// the 16-byte alignment of its data (larger packets close a batch early; one that does not fit an
+// empty arena grows it). Round 4: 80 KiB before, so a 64-packet arena pinned 5 MiB for 4.03 MiB of
+// packets and a read-ahead stream's rings overran the pool's pinned cap by a ring (config 5)
+constexpr size_t kPacketGuess = 64 * 1024 + 512 + 16;
 
 struct PacketRef {
     uint64_t data_off, crc_off;  // inside the arena
@@ -519,6 +523,12 @@ bool block_reader_local_fault(const hdfs3_block_reader *r) { return r && r->loca
 int64_t block_reader_batch_bytes(const hdfs3_reader_opts *opts) {
     const int bp = opts && opts->batch_packets > 0 ? opts->batch_packets : kDefaultBatchPackets;
     return int64_t(bp) * 64 * 1024;  // payload of a batch of 64 KiB datanode packets
+}
+
+int64_t block_reader_arena_bytes(const hdfs3_reader_opts *opts) {
+    const int bp = opts && opts->batch_packets > 0 ? opts->batch_packets : kDefaultBatchPackets;
+    // what acquire()/grow() pin for one batch: the arena, its descriptor staging and result word
+    return int64_t(bp) * int64_t(kPacketGuess + sizeof(DevSegment)) + int64_t(sizeof(unsigned long long));
 }
 
 int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int64_t start, int64_t len,

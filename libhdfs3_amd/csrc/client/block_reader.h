@@ -16,6 +16,8 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
 
 // bytes of one batch arena of a reader with these options (the read-ahead ring depth unit)
 int64_t block_reader_batch_bytes(const hdfs3_reader_opts *opts);
+// pinned bytes of one batch arena (arena + descriptor staging + result word)
+int64_t block_reader_arena_bytes(const hdfs3_reader_opts *opts);
 
 // true when the reader's failure came from this host's GPU or pinned memory (a HIP error),
 // not from the datanode: InputStreamImpl's replica failover must not run on it

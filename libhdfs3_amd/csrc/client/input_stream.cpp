@@ -26,6 +26,7 @@ using namespace hdfs3crc;
 namespace {
 
 constexpr int64_t kMaxSkip = 128 * 1024;  // InputStreamImpl.cpp:1146
+constexpr int kShallowArenas = 6;  // arenas any pooled ctx keeps (hdfs3_crc.cpp kArenaCacheKeep)
 
 struct Node {
     std::string host;
@@ -133,7 +134,12 @@ struct hdfs3_input_stream {
             // cap, so the pool can keep them for the stream's next blocks and the next stream: with
             // whole-block rings, read-ahead 7 over a 1 GiB file pinned new rings on every open
             // (2.8-3.1 GiB/s against 12.6-13.2 with an uncapped pool, profiles/r03/reentry/r3e2e_fix_*)
-            const int64_t fit = int64_t(pool_pinned_cap_bytes() / uint64_t(ahead_blocks + 1)) / unit;
+            // counted in the arenas' real pinned size (block_reader_arena_bytes), after the few arenas
+            // every shallow pooled ctx keeps (the stream's own on-demand reader's among them)
+            const int64_t arena = block_reader_arena_bytes(&opts);
+            const int64_t cap = int64_t(pool_pinned_cap_bytes());
+            const int64_t fit = std::max<int64_t>(0, cap - int64_t(kShallowArenas) * arena) /
+                                int64_t(ahead_blocks + 1) / arena;
             const int slots = int(std::max<int64_t>(3, std::min<int64_t>({(want + unit - 1) / unit + 1, 64, fit})));
             hdfs3_crc_ctx *c = nullptr;
             if (ctx_acquire(opts.device, &c, true)) break;  // no context to spare: read on demand

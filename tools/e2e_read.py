@@ -139,6 +139,7 @@ def local_reads(data, crc, args, line):
         for verify in (True, False):
             for streams in (1, args.blocks):
                 best = 0.0
+                rates = []
                 for _ in range(args.reps):
                     errors: list[str] = []
                     t0 = time.perf_counter()
@@ -154,11 +155,18 @@ def local_reads(data, crc, args, line):
                     dt = time.perf_counter() - t0
                     assert not errors, errors
                     best = max(best, out.nbytes / dt / GIB)
+                    rates.append(round(out.nbytes / dt / GIB, 2))
                 assert np.array_equal(out, data[:out.nbytes])
                 out[:] = 0
                 staging = {"0": "pread", "1": "mmap"}.get(os.environ.get("HDFS3_LOCAL_MMAP", ""), "default")
+                from libhdfs3_amd import _native
+                st = _native.PoolStats()
+                _native.check("pool_stats", _native.lib().hdfs3_crc_pool_stats_get(ctypes.byref(st)))
                 print(json.dumps({**line, "mode": "local_read", "verify": verify, "streams": streams,
-                                  "read_mib": args.read_mib, "staging": staging, "gib_s": round(best, 2)}),
+                                  "read_mib": args.read_mib, "staging": staging, "gib_s": round(best, 2),
+                                  "gib_s_median": sorted(rates)[len(rates) // 2], "gib_s_all": rates,
+                                  "pool_retained_pinned_mib": round(st.pinned_bytes / 2**20, 1),
+                                  "pool_cap_mib": round(st.pinned_cap_bytes / 2**20, 1)}),
                       flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -258,8 +266,14 @@ def main():
                                   "gib_s": round(best, 2)}), flush=True)
         # single-stream hdfsRead with block read-ahead (hdfs3_input_set_readahead): blocks
         # i+1 .. i+D read and verified by background threads while block i is consumed
+        def pool_mib():
+            st = _native.PoolStats()
+            _native.check("pool_stats", _native.lib().hdfs3_crc_pool_stats_get(ctypes.byref(st)))
+            return round(st.pinned_bytes / 2**20, 1), round(st.pinned_cap_bytes / 2**20, 1)
+
         for ahead in [int(x) for x in args.readahead.split(",") if x]:
             best = 0.0
+            rates = []
             for _ in range(args.reps):
                 t0 = time.perf_counter()
                 with InputStream([(b, n, [("127.0.0.1", dn.port)]) for b, n in blocks], verify=True,
@@ -272,11 +286,15 @@ def main():
                         pos += got
                 dt = time.perf_counter() - t0
                 best = max(best, total / dt / GIB)
+                rates.append(round(total / dt / GIB, 2))
             assert np.array_equal(out, data)
             out[:] = 0
+            retained, cap = pool_mib()
             print(json.dumps({**line, "mode": "hdfsRead_readahead", "verify": True, "streams": 1,
                               "readahead_blocks": ahead, "batch_packets": args.batch,
-                              "packet_kib": args.packet_kib, "gib_s": round(best, 2)}), flush=True)
+                              "packet_kib": args.packet_kib, "gib_s": round(best, 2),
+                              "gib_s_median": sorted(rates)[len(rates) // 2], "gib_s_all": rates,
+                              "pool_retained_pinned_mib": retained, "pool_cap_mib": cap}), flush=True)
     finally:
         dn.stop()
     local_reads(data, crc, args, line)
