@@ -29,13 +29,18 @@ def main():
     ap.add_argument("--npk", type=int, default=2048, help="packets per launch")
     ap.add_argument("--warm", type=int, default=2000)
     ap.add_argument("--mode", default="verify", choices=["verify", "compute"])
+    ap.add_argument("--product", action="store_true", help="the product library (variant 0 only)")
+    ap.add_argument("--warm-each", type=int, default=20, help="launches before each timed sample")
+    ap.add_argument("--settle", action="store_true", help="settle (poll, then sync) before each timed sample")
     args = ap.parse_args()
 
     import torch
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import CrcContext
 
-    lib = _native.lab()
+    lib = _native.lib() if args.product else _native.lab()
+    if args.product:
+        lib.hdfs3x_set_variant = lambda v: None
     dev = torch.device("cuda", 0)
     ctx = CrcContext(0, lib=lib)
     stream = torch.cuda.Stream(device=dev)
@@ -86,8 +91,13 @@ def main():
     samples = {n: [] for n, _ in cases}
     for _ in range(args.rounds):
         for name, fn in cases:
-            for i in range(20):
+            for i in range(args.warm_each):
                 fn(i)
+            if args.settle:
+                done = torch.cuda.Event()
+                done.record(stream)
+                while not done.query():
+                    pass
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
