@@ -42,6 +42,7 @@ constexpr int kLabNoStage = 1024;   // compute: held stores even where productio
 constexpr int kLabStageWin = 2048;  // compute at bpc 512: staged words past kStageMaxRounds too, window by window
 constexpr int kLabClock = 4096;     // clock stamps of workgroup 0 (LabClock, crc32c_device.h; lab builds only)
 constexpr int kLabStorePlain = 8192;  // compute, staged words: plain global stores (production before round 4)
+constexpr int kLabHoldSys = 16384;   // compute, held words (bpc 512 past the staging window, bpc 4096): system-scope nt stores
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
 // written as whole lines, §4.1; past the window size in windows)
@@ -281,6 +282,18 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // burst. With a lane view their addresses come from the walk at flush time (one VGPR per held
     // octet); otherwise each lane keeps its word's address beside it (a segment walk's rounds may
     // belong to different segments).
+    // a held word's store: plain, or (kLabHoldSys) system-scope nt through a buffer resource on the
+    // walk's uniform word base (block and pitch walks)
+    auto held_store = [&](gu8 *p, uint32_t v) {
+        if constexpr ((LAB & kLabHoldSys) != 0 && Walk::kLaneView) {
+            const uint64_t wb = rfl64(reinterpret_cast<uint64_t>(walk.words));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<void *>(wb), 0, 0x7FFFFFFF, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs, uint32_t(reinterpret_cast<uint64_t>(p) - wb), 0, 1 | 2 | 16);
+        } else {
+            *(gu32 *)p = v;
+        }
+    };
     uint32_t line = 0;
     uint32_t hold[kHold ? 8 : 1];
     gu32 *laddr = nullptr;
@@ -297,7 +310,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
                     if (hold_addr[i]) *hold_addr[i] = hold[i];
                 } else {
                     const uint32_t kk = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
-                    if (kk < K) *(gu32 *)((gu8 *)walk.view(kk).w + 4 * (lane & 7)) = hold[i];
+                    if (kk < K) held_store((gu8 *)walk.view(kk).w + 4 * (lane & 7), hold[i]);
                 }
             }
         }
@@ -372,7 +385,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             line64 = lane == (k & 63) ? yy : line64;
             if ((k & 63) == 63 || k + 1 == K) {
                 const uint32_t kk = (k & ~63u) + lane;
-                if (lane <= (k & 63)) *(gu32 *)((gu8 *)walk.view(kk).w) = line64;
+                if (lane <= (k & 63)) held_store((gu8 *)walk.view(kk).w, line64);
             }
             return;
         }
