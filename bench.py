@@ -327,13 +327,19 @@ class StepGraphs:
             self.graphs[1].replay()
 
 
-def compute_block(torch, work, ctx, K, warm, stream, read_ceilings):
+PRE_PASS = 2000  # launches of `value`'s pre-passes before its warmup (the diagnostic pass, then the barriered one)
+
+
+def compute_block(torch, work, ctx, K, W, stream, read_ceilings):
     """Compute-on-write at the bench's shape (BASELINE.json configs[2]'s write half at configs[1]'s
     block): `hdfs3_crc32c_compute_dev` over the same rotated blocks, one 128 MiB block per launch,
     on the same clock as `value` (HIP events on the launch stream around K launches), overlapped
-    (HDFS3_LAUNCH_OVERLAP_PREVIOUS after the first) and barriered. The words go to fresh arrays
-    (poisoned before the timed run) and every word of every block is checked against the oracle
-    after the timed region. read_ceilings: (overlapped, barriered) same-shape plain-read GB/s."""
+    (HDFS3_LAUNCH_OVERLAP_PREVIOUS after the first) and barriered, each in `value`'s own form:
+    PRE_PASS barriered launches, W warmup launches, settle, K timed launches (round 4; until then
+    500 warmup launches and no pre-pass, so the compute region started from a different power state
+    than the verify region it is compared with). The words go to fresh arrays (poisoned before the
+    pre-pass) and every word of every block is checked against the oracle after the timed region.
+    read_ceilings: (overlapped, barriered) same-shape plain-read GB/s."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from util import oracle_compute  # test infrastructure: the checker only, after timing
@@ -354,11 +360,12 @@ def compute_block(torch, work, ctx, K, warm, stream, read_ceilings):
     res = {"api": "hdfs3_crc32c_compute_dev", "alg_bytes_per_launch": alg,
            "timing": "HIP events on the launch stream around K launches (the clock of value)"}
     for name, overlap in (("overlapped", True), ("barriered", False)):
-        # poison first, then the warmup (into scratch): the poison's 8 MiB of dirty lines leave the
-        # caches during the warmup, not inside a short timed region (a fill right before it cost the
-        # driver's K = 20 form ~2.5 us per launch, profiles/r03/reentry/r3zc_bench_k20.json)
+        # poison first, then the pre-pass and warmup (into scratch): the poison's 8 MiB of dirty lines
+        # leave the caches before the timed region (a fill right before it cost the driver's K = 20
+        # form ~2.5 us per launch, profiles/r03/reentry/r3zc_bench_k20.json)
         out.fill_(0xA5)
-        launches(warm, overlap, sp)
+        launches(PRE_PASS, False, sp)
+        launches(W, overlap, sp)
         settle(torch, stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
@@ -392,8 +399,8 @@ def packets_block(torch, work, ctx, K, W, stream, reps=3):
     its 64 KiB of data, 16 B aligned): 16,384 packets at a 66,048-byte pitch. One launch verifies
     2,048 packets = 128 MiB of payload (one block's worth, the unit of `value`) through
     hdfs3_crc32c_verify_packet_stream_dev_async, rotating over the 8 streams of the arena. Timed in
-    `value`'s form (W warmup, settle, K launches between HIP events, the first barriered, the rest
-    overlapped; and all barriered), and paired with contiguous-block verifies in identical regions
+    `value`'s form (PRE_PASS barriered launches, W warmup, settle, K launches between HIP events, the
+    first barriered, the rest overlapped; and all barriered), and paired with contiguous-block verifies in identical regions
     (`reps` x (packets, contiguous); medians), so frac_vs_contiguous carries no box drift. Every
     launch's result slot is checked after timing; before it, one flipped bit must come back as its
     (packet, chunk)."""
@@ -452,7 +459,9 @@ def packets_block(torch, work, ctx, K, W, stream, reps=3):
            "alg_bytes_per_launch": alg,
            "timing": "HIP events on the launch stream around K launches (the clock of value)"}
     for name, overlap in (("overlapped", True), ("barriered", False)):
-        t = region(pk_launch, K, max(W, 1), overlap)
+        for i in range(PRE_PASS):  # `value`'s form: its pre-pass, W warmup, settle, K timed
+            pk_launch(i, i % res.numel(), False)
+        t = region(pk_launch, K, W, overlap)
         r = {"value": round(bb / t / 2**30, 2), "unit": "GiB/s", "avg_launch_us": round(t * 1e6, 2),
              "achieved_GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}
         n = max(K, 200)
@@ -880,7 +889,7 @@ def main():
         if barriered is not None:
             extra["barriered"] = barriered
         if args.mode == "verify" and not args.no_compute:
-            extra["compute"] = compute_block(torch, work, ctx, K, max(W, 500), stream, ceilings)
+            extra["compute"] = compute_block(torch, work, ctx, K, W, stream, ceilings)
             for m in ("overlapped", "barriered"):
                 v = roofline["frac"] if m == "overlapped" else (barriered or {}).get("frac")
                 if v:

@@ -5,6 +5,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -128,3 +129,21 @@ def test_missing_library_raises(tmp_path):
 
     with pytest.raises(ImportError):
         _native.load(str(tmp_path / "nope.so"))
+
+
+@pytest.mark.parametrize("value,want_mib,warns", [("64M", 64, False), ("2G", 2048, False), ("1048576", 1, False),
+                                                   ("1.5G", 1024, True), ("64MiB", 1024, True), ("-1", 1024, True),
+                                                   ("junk", 1024, True), ("", 1024, False)])
+def test_pool_pinned_cap_parser(value, want_mib, warns):
+    """HDFS3_POOL_PINNED_MAX: digits with an optional K/M/G suffix; anything else keeps the 1 GiB
+    default and says so on stderr instead of being read as a prefix of itself ("1.5G" was
+    read as 1 byte). hdfs3_crc_pool_stats_get reports the cap without touching a GPU."""
+    code = ("import ctypes, sys; sys.path.insert(0, %r)\n"
+            "from libhdfs3_amd import _native\n"
+            "st = _native.PoolStats(); assert _native.lib().hdfs3_crc_pool_stats_get(ctypes.byref(st)) == 0\n"
+            "print(st.pinned_cap_bytes)\n") % REPO
+    env = dict(os.environ, HDFS3_POOL_PINNED_MAX=value)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert int(out.stdout.strip().splitlines()[-1]) == want_mib << 20
+    assert ("HDFS3_POOL_PINNED_MAX" in out.stderr) == warns, out.stderr
