@@ -59,14 +59,10 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabStageWin>(a, tab, fold, grid_cap, s);
         case 128:  // compute: staged words through plain global stores (production before round 4)
             return launch_wave3<BPC, V, false, true, kLabStorePlain>(a, tab, fold, grid_cap, s);
-        case 133:  // compute: held words (bpc 512 past the staging window, bpc 4096) as system-scope nt stores
-            return launch_wave3<BPC, V, false, true, kLabHoldSys>(a, tab, fold, grid_cap, s);
+        case 137:  // verify: 1024-thread workgroups at every launch size (production before round 4)
+            return launch_wave3<BPC, V, false, true, kLabWg1024>(a, tab, fold, grid_cap, s);
         case 132:  // 256-thread workgroups (4 waves each): small launches spread over 4x the CUs
             return launch_wave3<BPC, V, false, true, 0, 256>(a, tab, fold, grid_cap, s);
-        case 135:  // a grid of 15/16 of the CUs: the next overlapped launch starts on the idle ones at once
-            return launch_wave3<BPC, V, false, true>(a, tab, fold, grid_cap - grid_cap / 16, s);
-        case 136:  // a grid of 31/32 of the CUs
-            return launch_wave3<BPC, V, false, true>(a, tab, fold, grid_cap - grid_cap / 32, s);
         case 134:  // 512-thread workgroups (8 waves each)
             return launch_wave3<BPC, V, false, true, 0, 512>(a, tab, fold, grid_cap, s);
         case 125:  // production with clock stamps of workgroup 0 (kLabClock; tools/clock_ramp.py)

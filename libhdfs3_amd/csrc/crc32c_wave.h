@@ -42,7 +42,7 @@ constexpr int kLabNoStage = 1024;   // compute: held stores even where productio
 constexpr int kLabStageWin = 2048;  // compute at bpc 512: staged words past kStageMaxRounds too, window by window
 constexpr int kLabClock = 4096;     // clock stamps of workgroup 0 (LabClock, crc32c_device.h; lab builds only)
 constexpr int kLabStorePlain = 8192;  // compute, staged words: plain global stores (production before round 4)
-constexpr int kLabHoldSys = 16384;   // compute, held words (bpc 512 past the staging window, bpc 4096): system-scope nt stores
+constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every launch size (production before round 4)
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
 // written as whole lines, §4.1; past the window size in windows)
@@ -282,18 +282,11 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // burst. With a lane view their addresses come from the walk at flush time (one VGPR per held
     // octet); otherwise each lane keeps its word's address beside it (a segment walk's rounds may
     // belong to different segments).
-    // a held word's store: plain, or (kLabHoldSys) system-scope nt through a buffer resource on the
-    // walk's uniform word base (block and pitch walks)
-    auto held_store = [&](gu8 *p, uint32_t v) {
-        if constexpr ((LAB & kLabHoldSys) != 0 && Walk::kLaneView) {
-            const uint64_t wb = rfl64(reinterpret_cast<uint64_t>(walk.words));
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<void *>(wb), 0, 0x7FFFFFFF, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b32(v, rs, uint32_t(reinterpret_cast<uint64_t>(p) - wb), 0, 1 | 2 | 16);
-        } else {
-            *(gu32 *)p = v;
-        }
-    };
+    // a held word's store. Round 4 measured these as system-scope nt stores too (the staged words'
+    // policy): 1 GiB compute 160.6 -> 175.0 us at bpc 512 and 159.5 -> 182.6 at 4096
+    // (profiles/r04/r4h_cmp_1g*): write-through 4-byte and 32-byte pieces cost what whole staged
+    // lines do not, so they stay plain
+    auto held_store = [&](gu8 *p, uint32_t v) { *(gu32 *)p = v; };
     uint32_t line = 0;
     uint32_t hold[kHold ? 8 : 1];
     gu32 *laddr = nullptr;
@@ -703,6 +696,18 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     ChunkLaunch b = a;
     b.kq = uint32_t(units / nwaves);
     b.kr = uint32_t(units % nwaves);
+    // Verify launches below 64 MiB take smaller workgroups (round 4): a 1024-thread workgroup fills a
+    // CU's LDS, so with 2 rounds per wave a launch of fewer than 8,192 rounds (32 MiB) left CUs idle and
+    // every CU it used paid the whole table fill for few rounds. 256 threads up to 16 MiB, 512 up to
+    // 64 MiB, HBM-resident blocks, wall clock per launch (tools/ab.py, profiles/r04/r4h_*): 4 MiB
+    // 7.38 -> 6.45 us barriered, 7.05 -> 6.43 overlapped; 16 MiB 7.95 -> 6.47 / 7.27 -> 5.81; 32 MiB
+    // 10.16 -> 9.04 / 8.82 -> 8.53; 64 MiB 14.57 -> 13.90 / 13.36 -> 12.56; the block reader's
+    // 64-packet batch (4 MiB, cache-resident) 7.00 -> 4.43. 128 MiB stays at 1024 (256 / 512 threads:
+    // +6.1 / +0.4 us barriered). Compute keeps 1024 threads: its staged words need the whole LDS.
+    if constexpr (V && TPB == 1024 && (LAB & kLabWg1024) == 0) {
+        if (units <= 4096) return launch_wave3<BPC, V, PITCH, SOLO, LAB, 256>(a, tab, fold, grid_cap, s);
+        if (units <= 16384) return launch_wave3<BPC, V, PITCH, SOLO, LAB, 512>(a, tab, fold, grid_cap, s);
+    }
     // compute at bpc <= 2048 over one contiguous block: staged words; at bpc 512 only while they fit one
     // window (beyond it the held stores measured faster at 1 GiB: 160.4 against 163.1 us in windows)
     if constexpr (!V && BPC <= 2048 && !PITCH && TPB == 1024 &&

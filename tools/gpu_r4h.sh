@@ -24,4 +24,7 @@ run ovl_128 --variants 0,132,134 --rounds 5 --reps 50 --overlap || exit 1
 timeout -k 10 300 python -u tools/pkt_ab.py --variants 0,132,134 --npk 64 --reps 400 --rounds 5 \
     > gpurun_out/${TAG}_pkt_4mib_bar.jsonl 2> gpurun_out/${TAG}_pkt_4mib_bar.err && cat gpurun_out/${TAG}_pkt_4mib_bar.jsonl || exit 1
 run cmp_1g --variants 0,133 --rounds 5 --block-mib 1024 --blocks 2 --reps 8 --warm 200 --overlap --mode compute &&
-run cmp_1g_4096 --variants 0,133 --rounds 5 --block-mib 1024 --blocks 2 --reps 8 --warm 200 --overlap --mode compute --bpc 4096
+run cmp_1g_4096 --variants 0,133 --rounds 5 --block-mib 1024 --blocks 2 --reps 8 --warm 200 --overlap --mode compute --bpc 4096 &&
+run grid_short --variants 0,135,136 --rounds 9 --reps 20 --overlap &&
+run grid_long --variants 0,135,136 --rounds 5 --reps 200 --overlap &&
+run grid_bar --variants 0,135,136 --rounds 5 --reps 50
