@@ -92,24 +92,6 @@ struct WordScratch {
     hipEvent_t used = nullptr;  // recorded after the last launch that read the scratch
     void release();
 };
-// word regions at most this long (per packet) take the dense path: 64 KiB = 8 MiB packets at bpc 512
-constexpr uint64_t kDenseWordsMaxRegion = 64 * 1024;
-hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
-                                int grid_cap, hipStream_t stream, WordScratch *ws = nullptr);
-// batches of equal blocks (the last may be shorter) of a power-of-two number of whole rounds
-// whose data and words sit at two constant strides (blocks of one 2-D tensor): the pitch mode
-// with crc_pitch; hipErrorNotSupported = use the segmented kernel
-hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc, bool verify, int check_short_tail,
-                                 unsigned long long *result, const uint32_t *d_tables, const uint32_t *d_fold,
-                                 int grid_cap, hipStream_t stream, WordScratch *ws = nullptr);
-// bad_index != null: every packet is first checked against [0, arena_len) (hipErrorInvalidValue
-// and *bad_index = the first one outside)
-hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
-                               int check_short_tail, unsigned long long *result, DevSegment *h_stage,
-                               DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
-                               hipStream_t stream, uint64_t arena_len = 0, size_t *bad_index = nullptr,
-                               bool overlap_previous = false, WordScratch *ws = nullptr);
-
 // Chunks of R * 4096 bytes (R >= 2; 8 KiB ... 64 KiB and any other multiple of 4096): the round
 // kernel computes the CRC of every 4096-byte piece into a ctx-owned scratch (two buffers used in
 // turn, so a launch that overlaps its predecessor never writes the words that predecessor's combine
@@ -122,6 +104,28 @@ struct PieceScratch {
     unsigned next = 0;
     void release();
 };
+
+// word regions at most this long (per packet) take the dense path: 64 KiB = 8 MiB packets at bpc 512
+constexpr uint64_t kDenseWordsMaxRegion = 64 * 1024;
+// pieces != null: streams at bpc = R * 4096 (R dividing the rounds per packet) take the piece
+// CRCs + combine (round 4); without it they return hipErrorNotSupported (the caller's fallback)
+hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
+                                int grid_cap, hipStream_t stream, WordScratch *ws = nullptr,
+                                PieceScratch *pieces = nullptr);
+// batches of equal blocks (the last may be shorter) of a power-of-two number of whole rounds
+// whose data and words sit at two constant strides (blocks of one 2-D tensor): the pitch mode
+// with crc_pitch; hipErrorNotSupported = use the segmented kernel
+hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc, bool verify, int check_short_tail,
+                                 unsigned long long *result, const uint32_t *d_tables, const uint32_t *d_fold,
+                                 int grid_cap, hipStream_t stream, WordScratch *ws = nullptr);
+// bad_index != null: every packet is first checked against [0, arena_len) (hipErrorInvalidValue
+// and *bad_index = the first one outside)
+hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
+                               int check_short_tail, unsigned long long *result, DevSegment *h_stage,
+                               DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
+                               hipStream_t stream, uint64_t arena_len = 0, size_t *bad_index = nullptr,
+                               bool overlap_previous = false, WordScratch *ws = nullptr,
+                               PieceScratch *pieces = nullptr);
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream,

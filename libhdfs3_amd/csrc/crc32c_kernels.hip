@@ -62,7 +62,11 @@ hipError_t launch_pv(const ChunkLaunch &a, bool verify, const uint32_t *tab, con
 
 bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32_t bpc, const void *data,
                       const void *crc, uint64_t pitch, uint32_t *upp_log2) {
-    if (bpc != 512 && bpc != 1024 && bpc != 2048 && bpc != 4096) return false;
+    // bpc 512..4096: the round kernel's pitch walk; R * 4096 (R >= 2) with R dividing the rounds per
+    // packet: the walk's 4096-byte piece CRCs + the combine (launch_stream_pieces, round 4)
+    const bool pieces = bpc > kRoundBytes && bpc % kRoundBytes == 0;
+    if (bpc != 512 && bpc != 1024 && bpc != 2048 && bpc != 4096 && !pieces) return false;
+    if (pieces && data_len % bpc) return false;
     if (npk == 0 || data_len == 0 || data_len % kRoundBytes || last_len > data_len) return false;
     if (npk > 1 && pitch == 0) return false;
     if (npk >= (uint64_t(1) << 31)) return false;  // keys are (packet << 32) | chunk
@@ -140,6 +144,10 @@ hipError_t launch_stream_kernel(const ChunkLaunch &a, bool verify, const uint32_
 
 }  // namespace
 
+// bpc = R * 4096 packet streams (defined with launch_pieces below)
+hipError_t launch_stream_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
+                                int grid_cap, hipStream_t stream, PieceScratch *ps);
+
 void WordScratch::release() {
     if (d) (void)hipFree(d);
     if (used) (void)hipEventDestroy(used);
@@ -147,11 +155,16 @@ void WordScratch::release() {
 }
 
 hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
-                                int grid_cap, hipStream_t stream, WordScratch *ws) {
+                                int grid_cap, hipStream_t stream, WordScratch *ws, PieceScratch *pieces) {
 #if HDFS3_LAB
     if (g_variant == 52 || g_variant == 53) return hipErrorNotSupported;  // A/B: force the segmented kernel
     if (g_variant == 55) ws = nullptr;  // A/B: words written in place (no dense scratch)
 #endif
+    if (a.bpc > kRoundBytes) {  // chunks of R whole rounds: pieces + combine, or the caller's fallback
+        if (!pieces || a.bpc % kRoundBytes || ((uint64_t(1) << a.upp_log2) % (a.bpc / kRoundBytes)))
+            return hipErrorNotSupported;
+        return launch_stream_pieces(a, verify, d_tables, d_fold, grid_cap, stream, pieces);
+    }
     if (a.bpc != 512 && a.bpc != 1024 && a.bpc != 2048 && a.bpc != 4096) return hipErrorInvalidValue;
     const uint64_t cpitch = a.crc_pitch ? a.crc_pitch : a.pitch;
     const uint64_t wpp = (uint64_t(kRoundBytes) << a.upp_log2) / a.bpc * 4;  // word bytes per packet
@@ -208,12 +221,15 @@ namespace {
 // `piece_be`): with A = the 4096-zero-byte advance (d_fold + kFoldAdvance4096) and crc0 the raw
 // (init 0, no final xor) CRC, crc0(P_i) = y_i ^ K, K = A(~0) ^ ~0, and the chunk's state from init ~0
 // is s = A(... A(A(~0) ^ crc0(P_0)) ...) ^ crc0(P_{R-1}); its CRC is ~s. One chunk per thread.
+// cpp > 0 (packet streams, round 4): chunk k is chunk k % cpp of packet k / cpp, its word at
+// crc + (k / cpp) * cpitch + 4 (k % cpp) and its key (packet << 32) | chunk; the pieces stay dense.
 template <bool VERIFY>
 __global__ __launch_bounds__(256) void crc32c_combine_pieces_kernel(const uint8_t *__restrict__ piece_be, uint64_t nchunks,
                                                                     uint32_t R, const uint32_t *__restrict__ g_fold,
                                                                     const uint8_t *crc_be, uint8_t *out_be,
                                                                     uint64_t chunk_base,
-                                                                    unsigned long long *result) {
+                                                                    unsigned long long *result, uint64_t cpp = 0,
+                                                                    uint64_t cpitch = 0) {
     uint32_t col[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) col[i] = g_fold[kFoldAdvance4096 + i];
@@ -223,23 +239,26 @@ __global__ __launch_bounds__(256) void crc32c_combine_pieces_kernel(const uint8_
         uint32_t st = 0xFFFFFFFFu;
         for (uint32_t i = 0; i < R; ++i) st = gf2_apply4(col, st) ^ __builtin_bswap32(y[c * R + i]) ^ K;
         const uint32_t v = ~st;
+        uint64_t woff = 4 * c, key = chunk_base + c;
+        if (cpp) {
+            const uint64_t pk = c / cpp, ch = c % cpp;
+            woff = pk * cpitch + 4 * ch;
+            key = (pk << 32) | ch;
+        }
         if constexpr (VERIFY) {
-            if (__builtin_bswap32(reinterpret_cast<const uint32_t *>(crc_be)[c]) != v)
-                atomicMax(result, ~(unsigned long long)(chunk_base + c));
+            if (__builtin_bswap32(*reinterpret_cast<const uint32_t *>(crc_be + woff)) != v)
+                atomicMax(result, ~(unsigned long long)key);
         } else {
-            reinterpret_cast<uint32_t *>(out_be)[c] = __builtin_bswap32(v);
+            *reinterpret_cast<uint32_t *>(out_be + woff) = __builtin_bswap32(v);
         }
     }
 }
 
 // Whole chunks of R = bpc / 4096 pieces: the round kernel's compute at bpc 4096 into the scratch,
 // then the combine. The short tail chunk (if any) goes to the chunk-per-lane kernel.
-hipError_t launch_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
-                         int grid_cap, hipStream_t stream, PieceScratch *ps) {
-    const uint32_t R = a.bpc / kRoundBytes;
-    const uint64_t nfull = a.len / a.bpc;
+// The next of the two piece buffers, at least `need` bytes, ordered after its previous reader.
+hipError_t piece_buffer(PieceScratch *ps, uint64_t need, hipStream_t stream, unsigned *out) {
     const unsigned b = ps->next & 1u;
-    const uint64_t need = nfull * R * 4;
     if (need > ps->cap[b]) {
         if (ps->used[b]) {  // the buffer may still be read by a combine in flight
             hipError_t e = hipEventSynchronize(ps->used[b]);
@@ -263,6 +282,16 @@ hipError_t launch_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_ta
     }
     ps->on[b] = stream;
     ps->next = b + 1;
+    *out = b;
+    return hipSuccess;
+}
+
+hipError_t launch_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
+                         int grid_cap, hipStream_t stream, PieceScratch *ps) {
+    const uint32_t R = a.bpc / kRoundBytes;
+    const uint64_t nfull = a.len / a.bpc;
+    unsigned b = 0;
+    if (hipError_t e = piece_buffer(ps, nfull * R * 4, stream, &b); e != hipSuccess) return e;
     ChunkLaunch p = a;  // the pieces: a compute at bpc 4096 over the whole chunks
     p.len = nfull * a.bpc;
     p.bpc = kRoundBytes;
@@ -296,6 +325,60 @@ hipError_t launch_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_ta
 }
 
 }  // namespace
+
+// A packet stream whose chunks are R = bpc / 4096 whole rounds (64 KiB datanode packets at bpc 8192
+// ... 65536; round 4). The pitch walk computes every 4096-byte piece's CRC densely into the piece
+// scratch (packet p's pieces at 4 (p * upp + i)), the combine folds each chunk's R pieces and
+// compares with (verify) or writes (compute) the word in the packet's own CRC region, key
+// (packet << 32) | chunk; the last packet's short chunk, if any, takes the byte-exact kernel.
+// Until round 4 these streams took the chunk-per-lane packet kernel.
+hipError_t launch_stream_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
+                                int grid_cap, hipStream_t stream, PieceScratch *ps) {
+    const uint32_t R = a.bpc / kRoundBytes;
+    const uint64_t upp = uint64_t(1) << a.upp_log2;
+    const uint64_t cpp = upp / R;                            // chunks per packet
+    const uint64_t lfull = a.last_len / a.bpc;               // whole chunks of the last packet
+    const uint64_t nfull = (a.npk - 1) * cpp + lfull;
+    const uint64_t npieces = (a.npk - 1) * upp + (uint64_t(a.last_len) + kRoundBytes - 1) / kRoundBytes;
+    const uint64_t cpitch = a.crc_pitch ? a.crc_pitch : a.pitch;
+    unsigned b = 0;
+    if (hipError_t e = piece_buffer(ps, npieces * 4, stream, &b); e != hipSuccess) return e;
+    ChunkLaunch p = a;  // the pieces: a compute at bpc 4096 over the stream, words dense in the scratch
+    p.bpc = kRoundBytes;
+    p.out_be = ps->d[b];
+    p.crc_be = ps->d[b];
+    p.crc_pitch = upp * 4;
+    p.check_short_tail = 1;
+    hipError_t e = launch_stream_kernel(p, false, d_tables, d_fold, grid_cap, stream);
+    if (e != hipSuccess) return e;
+    if (nfull) {
+        const uint64_t blocks = (nfull + 255) / 256;
+        const int grid = int(blocks < 1024 ? blocks : 1024);
+        if (verify)
+            hipLaunchKernelGGL(crc32c_combine_pieces_kernel<true>, dim3(grid), dim3(256), 0, stream, ps->d[b], nfull,
+                               R, d_fold, a.crc_be, nullptr, 0, a.result, cpp, cpitch);
+        else
+            hipLaunchKernelGGL(crc32c_combine_pieces_kernel<false>, dim3(grid), dim3(256), 0, stream, ps->d[b], nfull,
+                               R, d_fold, nullptr, a.out_be, 0, a.result, cpp, cpitch);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    e = hipEventRecord(ps->used[b], stream);
+    if (e != hipSuccess) return e;
+    const uint64_t tail = a.last_len % a.bpc;
+    if (tail == 0) return hipSuccess;
+    const uint64_t lp = a.npk - 1;
+    ChunkLaunch t{};  // the last packet's short chunk: one lane of the byte-exact kernel
+    t.data = a.data + lp * a.pitch + lfull * a.bpc;
+    t.len = tail;
+    t.bpc = a.bpc;
+    t.chunk_base = (lp << 32) | lfull;
+    t.check_short_tail = a.check_short_tail;
+    t.result = a.result;
+    if (verify) t.crc_be = a.crc_be + lp * cpitch + 4 * lfull;
+    else t.out_be = a.out_be + lp * cpitch + 4 * lfull;
+    return verify ? launch_t<0, true>(t, d_tables, 1, stream) : launch_t<0, false>(t, d_tables, 1, stream);
+}
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream, PieceScratch *pieces) {
@@ -431,11 +514,13 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                hipStream_t stream, uint64_t arena_len, size_t *bad_index, bool overlap_previous,
-                               WordScratch *ws) {
+                               WordScratch *ws, PieceScratch *pieces) {
     if (n == 0) return hipSuccess;
     // one pass: descriptors, the alignment test of segments_fast and the unit plan of
     // plan_segments (16K packets per GiB: the host loop is on the call's critical path)
     bool fast = g_variant != 17 && (bpc == 512 || bpc == 1024 || bpc == 2048 || bpc == 4096);
+    // bpc = R * 4096: the pitch walk's pieces + combine when the batch is a constant-pitch stream
+    bool aligned = g_variant != 17 && (fast || (pieces && bpc > kRoundBytes && bpc % kRoundBytes == 0));
     uint64_t units = 0, u0 = h_pk[0].data_len / kRoundBytes;
     bool same = true;
     // constant pitch: packet i at data_off[0] + i*S, crc_off[0] + i*S, one data length
@@ -455,7 +540,9 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         const uint8_t *data = d_arena + h_pk[i].data_off;
         const uint8_t *crc = d_arena + h_pk[i].crc_off;
         const uint64_t u = h_pk[i].data_len / kRoundBytes;
-        fast = fast && ((reinterpret_cast<uintptr_t>(data) & 15u) | (reinterpret_cast<uintptr_t>(crc) & 3u)) == 0;
+        const bool al = ((reinterpret_cast<uintptr_t>(data) & 15u) | (reinterpret_cast<uintptr_t>(crc) & 3u)) == 0;
+        fast = fast && al;
+        aligned = aligned && al;
         if (i + 1 < n && u != u0) same = false;
         strided = strided && h_pk[i].data_off == h_pk[0].data_off + i * pitch &&
                   h_pk[i].crc_off == h_pk[0].crc_off + i * pitch &&
@@ -463,7 +550,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         units += u;
     }
     uint32_t upp_log2 = 0;
-    if (fast && strided && n > 1 &&
+    if (aligned && strided && n > 1 &&
         packet_stream_ok(h_pk[0].data_len, h_pk[n - 1].data_len, n, bpc, d_arena + h_pk[0].data_off,
                          d_arena + h_pk[0].crc_off, pitch, &upp_log2)) {
         ChunkLaunch a{};
@@ -478,7 +565,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         a.upp_log2 = upp_log2;
         a.last_len = h_pk[n - 1].data_len;
         a.overlap_previous = overlap_previous && verify;
-        const hipError_t e = launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream, ws);
+        const hipError_t e = launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream, ws, pieces);
         if (e != hipErrorNotSupported) return e;
     }
     if (fast && strided && same && u0 > 0 && n > kInlineSegments) {

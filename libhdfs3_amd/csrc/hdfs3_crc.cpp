@@ -250,7 +250,7 @@ int packets_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len, 
     size_t bad = 0;
     const hipError_t e = launch_packet_batch(d_arena, hp, n, bpc, verify, check_short_tail, d_result, st->h, st->d,
                                              ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, arena_len,
-                                             &bad, overlap, &ctx->words);
+                                             &bad, overlap, &ctx->words, &ctx->pieces);
     if (e == hipErrorInvalidValue) return fail(-EINVAL, "packet %zu lies outside the %zu-byte arena", bad, arena_len);
     HIP_TRY(e);
     ++ctx->launches;
@@ -310,7 +310,8 @@ int packet_stream_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena
         a.last_len = ps->last_len;
         a.overlap_previous = overlap && verify;
         const hipError_t e =
-            launch_packet_stream(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, &ctx->words);
+            launch_packet_stream(a, verify, ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, &ctx->words,
+                                 &ctx->pieces);
         if (e != hipErrorNotSupported) {
             HIP_TRY(e);
             ++ctx->launches;

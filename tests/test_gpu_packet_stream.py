@@ -243,3 +243,38 @@ def test_packet_stream_solo_variant_overlapped_chain(lab_ctx, variant):
                     assert w == 0, (variant, n, i)
     finally:
         lib.hdfs3x_set_variant(0)
+
+
+@pytest.mark.parametrize("bpc", [8192, 16384, 32768, 65536])
+@pytest.mark.parametrize("last", [65536, 65536 - 300, 8192 * 3 + 100, 100])
+def test_packet_stream_chunks_above_4k_pieces(gpu_ctx, bpc, last):
+    """Packet streams at bpc = R * 4096 (64 KiB datanode packets at 8 / 16 / 32 / 64 KiB chunks; round
+    4): the pitch walk's 4096-byte piece CRCs, the combine into each packet's own CRC region, the last
+    packet's short chunk on the byte-exact kernel. Keys (packet, chunk) and every computed word against
+    the oracle, remote and local tail semantics, flips in the first, a middle and the last packet, and
+    the descriptor form of the same stream (packets API) gives the same keys."""
+    from libhdfs3_amd.engine import CrcContext
+
+    n, plen = 24, 65536
+    arena, pitch, crc_off, data_off, datas = build_arena(n, plen, last, bpc, 300 + bpc % 977 + last % 13)
+    d = gpu_ctx.upload(arena)
+    ps = CrcContext.packet_stream(crc_off, data_off, pitch, n, plen, last)
+    for local in (False, True):
+        assert run_stream(gpu_ctx, d, arena.nbytes, ps, bpc, local) == (-1, -1)
+    rng = np.random.default_rng(bpc + last)
+    for p, q in [(0, 5), (n // 2, int(rng.integers(0, plen))), (n - 1, last - 1), (n - 1, 0)]:
+        bad = arena.copy()
+        bad[p * pitch + data_off + q] ^= 0x08
+        gpu_ctx.upload(bad, d)
+        for local in (False, True):
+            want = oracle_key([np.frombuffer(bad[i * pitch + data_off:i * pitch + data_off + datas[i].size], np.uint8)
+                               for i in range(n)], bad, pitch, crc_off, bpc, local)
+            assert run_stream(gpu_ctx, d, arena.nbytes, ps, bpc, local) == want, (p, q, local)
+            pk = [(i * pitch + data_off, i * pitch + crc_off, datas[i].size) for i in range(n)]
+            assert gpu_ctx.verify_packets_dev(d.ptr, arena.nbytes, pk, bpc, local) == want, (p, q, local)
+    blank = arena.copy()
+    for i in range(n):
+        blank[i * pitch + crc_off:i * pitch + data_off] = 0
+    gpu_ctx.upload(blank, d)
+    gpu_ctx.compute_packet_stream_async(d.ptr, arena.nbytes, ps, bpc)
+    assert np.array_equal(gpu_ctx.download(d, arena.nbytes), arena)

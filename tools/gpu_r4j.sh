@@ -6,7 +6,7 @@ TAG=${1:-r4j}
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for h in 3 8 12; do
+for h in 0 3 8; do
   HDFS3_COPY_HELPERS=$h timeout -k 10 300 python -u tools/e2e_read.py --local-only --reps 3 \
       > gpurun_out/${TAG}_local_h$h.jsonl 2> gpurun_out/${TAG}_local_h$h.err || { echo "local h=$h failed"; exit 1; }
   echo "helpers=$h"; cat gpurun_out/${TAG}_local_h$h.jsonl
