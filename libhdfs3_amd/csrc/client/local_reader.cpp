@@ -59,6 +59,17 @@ constexpr int32_t kDefaultBuffer = 1 << 20;  // input.localread.default.buffersi
 constexpr int kDefaultWindowBuffers = 4;  // 4 MiB windows: first delivery sooner
 constexpr int32_t kMaxBuffer = 1 << 30;     // largest local buffer / window
 
+// Window events: HDFS3_LOCAL_BLOCKING_SYNC=1 makes the consumer sleep in hipEventSynchronize
+// (hipEventBlockingSync) instead of spinning, leaving the cores to the copies when many readers
+// run at once (round 4 measurement knob; the default keeps the spin)
+unsigned window_event_flags() {
+    static const unsigned f = [] {
+        const char *e = getenv("HDFS3_LOCAL_BLOCKING_SYNC");
+        return unsigned(hipEventDisableTiming) | (e && e[0] == '1' ? unsigned(hipEventBlockingSync) : 0u);
+    }();
+    return f;
+}
+
 int hip_err(hipError_t e, const char *what) {
     return fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
 }
@@ -478,7 +489,7 @@ int hdfs3_local_reader_open(const char *data_path, const char *meta_path, int64_
                     hipMalloc(reinterpret_cast<void **>(&a.d_res), sizeof(unsigned long long)) != hipSuccess ||
                     hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long),
                                   pinned_host_flags()) != hipSuccess ||
-                    hipEventCreateWithFlags(&a.done, hipEventDisableTiming) != hipSuccess) {
+                    hipEventCreateWithFlags(&a.done, window_event_flags()) != hipSuccess) {
                     ok = false;
                     return;
                 }
