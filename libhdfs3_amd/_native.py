@@ -282,6 +282,7 @@ BENCH_API = {
     "hdfs3x_grid_cap": (c_int, [c_void_p]),
     "hdfs3x_set_variant": (None, [c_int]),
     "hdfs3x_clock_stamps": (c_int, [c_void_p, ctypes.c_uint]),
+    "hdfs3x_wave_stamps": (c_int, [c_void_p, ctypes.c_uint]),
     "hdfs3x_block_reader_timing": (c_int, [c_void_p, POINTER(c_uint64)]),
     "hdfs3x_fail_prefetch_arenas": (None, [c_int]),
 }

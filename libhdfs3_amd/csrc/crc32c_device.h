@@ -699,26 +699,46 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_packets_kernel(
 // slot of g_lab_clk (4 words per launch). s_memtime counts the shader clock and s_memrealtime a fixed
 // 100 MHz, so the ratio of their deltas is the shader clock over that workgroup's lifetime. Vector
 // stores and a vector atomic only; nothing when no buffer is set.
+// With a wave buffer installed (hdfs3x_wave_stamps, tools/wave_spread.py) lane 0 of EVERY wave also
+// records {realtime start, realtime end, shader clocks elapsed, HW_ID | XCC_ID << 32 | wave << 40}:
+// where each launch's time goes between its first wave's start and its last wave's end.
 __device__ unsigned long long *g_lab_clk = nullptr;
 __device__ unsigned int g_lab_clk_cap = 0;
 __device__ unsigned int g_lab_clk_n = 0;
+__device__ unsigned long long *g_lab_wave = nullptr;
+__device__ unsigned int g_lab_wave_cap = 0;
+__device__ unsigned int g_lab_wave_n = 0;
 struct LabClock {
     unsigned long long t0 = 0, r0 = 0;
     __device__ __forceinline__ void start() {
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if ((threadIdx.x & 63) == 0) {
             t0 = __builtin_amdgcn_s_memtime();
             r0 = __builtin_amdgcn_s_memrealtime();
         }
     }
     __device__ __forceinline__ void end() {
+        if ((threadIdx.x & 63) != 0) return;
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         if (blockIdx.x == 0 && threadIdx.x == 0 && g_lab_clk) {
-            const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
             const unsigned int i = atomicAdd(&g_lab_clk_n, 1u);
             if (i < g_lab_clk_cap) {
                 g_lab_clk[4 * i] = t0;
                 g_lab_clk[4 * i + 1] = r0;
                 g_lab_clk[4 * i + 2] = t1;
                 g_lab_clk[4 * i + 3] = r1;
+            }
+        }
+        if (g_lab_wave) {
+            // HW_ID (hwreg 4, 32 bits: wave/simd/cu/sh/se) and XCC_ID (hwreg 20, low 4 bits)
+            const unsigned long long hw = uint32_t(__builtin_amdgcn_s_getreg((31 << 11) | 4));
+            const unsigned long long xcc = uint32_t(__builtin_amdgcn_s_getreg((3 << 11) | 20));
+            const unsigned long long wv = uint64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
+            const unsigned int i = atomicAdd(&g_lab_wave_n, 1u);
+            if (i < g_lab_wave_cap) {
+                g_lab_wave[4 * i] = r0;
+                g_lab_wave[4 * i + 1] = r1;
+                g_lab_wave[4 * i + 2] = t1 - t0;
+                g_lab_wave[4 * i + 3] = hw | xcc << 32 | wv << 40;
             }
         }
     }

@@ -112,6 +112,17 @@ hipError_t lab_clock_buffer(unsigned long long *d, unsigned int cap, unsigned in
     return hipMemcpyToSymbol(HIP_SYMBOL(g_lab_clk_n), &zero, sizeof zero);
 }
 
+hipError_t lab_wave_buffer(unsigned long long *d, unsigned int cap, unsigned int *n_out) {
+    unsigned int n = 0;
+    hipError_t e = hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_lab_wave_n), sizeof n);
+    if (e != hipSuccess) return e;
+    if (n_out) *n_out = n;
+    const unsigned int zero = 0;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_lab_wave), &d, sizeof d)) != hipSuccess) return e;
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_lab_wave_cap), &cap, sizeof cap)) != hipSuccess) return e;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_lab_wave_n), &zero, sizeof zero);
+}
+
 hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,
                               hipStream_t stream, bool overlap_previous) {
     // grid < 0: non-temporal loads over |grid| workgroups (the production kernels' policy);

@@ -149,6 +149,8 @@ void set_variant(int v);
 extern int g_variant;
 // clock stamps (LabClock): install a device buffer of cap x 4 words; *n_out = stamps in the previous one
 hipError_t lab_clock_buffer(unsigned long long *d, unsigned int cap, unsigned int *n_out);
+// every wave's stamps (LabClock with a wave buffer): cap x 4 words; *n_out = stamps in the previous one
+hipError_t lab_wave_buffer(unsigned long long *d, unsigned int cap, unsigned int *n_out);
 // The A/B variants (crc32c_experiments.hip): variant != 0, bpc with a whole-round kernel.
 hipError_t launch_experiment(int variant, const ChunkLaunch &a, bool verify, const uint32_t *tab,
                              const uint32_t *fold, int grid_cap, hipStream_t s);

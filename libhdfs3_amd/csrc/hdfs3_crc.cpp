@@ -1101,5 +1101,11 @@ int hdfs3x_clock_stamps(void *d_buf, unsigned int cap) {
     return int(n);
 }
 
+int hdfs3x_wave_stamps(void *d_buf, unsigned int cap) {
+    unsigned int n = 0;
+    HIP_TRY(lab_wave_buffer(static_cast<unsigned long long *>(d_buf), cap, &n));
+    return int(n);
+}
+
 }  // extern "C"
 #endif  // HDFS3_LAB

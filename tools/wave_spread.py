@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""Where a 128 MiB launch's time goes, wave by wave (barriered launches at 0.87 of
+the read kernel's per-block rate). Lane 0 of every wave of the stamping kernels (lab variant 125 =
+production verify + LabClock, and the plain stream read) records its realtime start/end (100 MHz),
+its shader clocks and its XCC (LabClock wave buffer, crc32c_device.h). Per launch (waves sorted by
+start and cut into launches of the grid's wave count; dispatch is in order):
+  gap        previous launch's last wave end -> this launch's first wave start
+  ramp       first -> last wave start (dispatch)
+  body       last wave start -> first wave end
+  tail       first wave end -> last wave end
+  span       first start -> last end
+  xcc_end    per XCC: median wave end - launch start (the XCDs' imbalance)
+Medians over the K launches of a region, barriered and overlapped.
+
+    python tools/wave_spread.py [--k 40] [--kinds crc,read]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--k", type=int, default=40)
+    ap.add_argument("--kinds", default="crc,read")
+    ap.add_argument("--read-grid", type=int, default=-512)
+    ap.add_argument("--variant", type=int, default=125)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import CrcContext
+
+    lib = _native.lab()
+    dev = torch.device("cuda", 0)
+    ctx = CrcContext(0, lib=lib)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    nb, bb, bpc = 8, 128 << 20, 512
+    data = torch.randint(0, 256, (nb, bb), dtype=torch.uint8, device=dev)
+    crc = torch.empty((nb, 4 * (bb // bpc)), dtype=torch.uint8, device=dev)
+    for b in range(nb):
+        ctx.compute_dev(data[b].data_ptr(), bb, bpc, crc[b].data_ptr())
+    res = torch.zeros(8192, dtype=torch.int64, device=dev)
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    cap = 1 << 20
+    stamps = torch.zeros(cap * 4, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    dp = [data[b].data_ptr() for b in range(nb)]
+    cp = [crc[b].data_ptr() for b in range(nb)]
+    rp = res.data_ptr()
+
+    def crc_launch(i, overlap):
+        ctx.verify_dev_async(dp[i % nb], bb, bpc, cp[i % nb], rp + 8 * (i % 8192), overlap_previous=overlap and i > 0)
+
+    def read_launch(i, overlap):
+        lib.hdfs3x_stream_read_ex(ctx.ctx, dp[i % nb], bb, args.read_grid, sink.data_ptr(), int(overlap and i > 0))
+
+    def settle():
+        done = torch.cuda.Event()
+        done.record(stream)
+        while not done.query():
+            pass
+        torch.cuda.synchronize()
+
+    def region(fn, overlap, k):
+        for i in range(2000):
+            fn(i, overlap)
+        settle()
+        stamps.zero_()
+        lib.hdfs3x_wave_stamps(stamps.data_ptr(), cap)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for i in range(k):
+            fn(i, overlap)
+        b.record(stream)
+        torch.cuda.synchronize()
+        n = lib.hdfs3x_wave_stamps(None, 0)
+        st = stamps[:4 * min(n, cap)].view(-1, 4).cpu().numpy()
+        return a.elapsed_time(b) * 1e3 / k, n, st
+
+    out = []
+    for kind in args.kinds.split(","):
+        fn = crc_launch if kind == "crc" else read_launch
+        lib.hdfs3x_set_variant(args.variant if kind == "crc" else 0)
+        for overlap in (False, True):
+            us, n, st = region(fn, overlap, args.k)
+            if n > cap or n % args.k:
+                print(json.dumps({"kind": kind, "overlap": overlap, "error": f"{n} stamps for {args.k} launches"}))
+                continue
+            per = n // args.k
+            st = st[np.argsort(st[:, 0], kind="stable")]
+            r0 = st[:, 0].astype(np.float64) / 100.0  # us
+            r1 = st[:, 1].astype(np.float64) / 100.0
+            clk = st[:, 2].astype(np.float64)
+            xcc = (st[:, 3] >> 32) & 0xFF
+            rows = {"gap": [], "ramp": [], "body": [], "tail": [], "span": [], "mhz": []}
+            xcc_end = {x: [] for x in range(8)}
+            prev_end = None
+            for li in range(args.k):
+                s = slice(li * per, (li + 1) * per)
+                a0, a1 = r0[s].min(), r0[s].max()
+                e0, e1 = r1[s].min(), r1[s].max()
+                if prev_end is not None:
+                    rows["gap"].append(a0 - prev_end)
+                prev_end = e1
+                rows["ramp"].append(a1 - a0)
+                rows["body"].append(e0 - a1)
+                rows["tail"].append(e1 - e0)
+                rows["span"].append(e1 - a0)
+                rows["mhz"].append(float(np.median(clk[s] / np.maximum((r1[s] - r0[s]) * 100.0, 1) * 100.0)))
+                for x in range(8):
+                    m = xcc[s] == x
+                    if m.any():
+                        xcc_end[x].append(float(np.median(r1[s][m])) - a0)
+            rec = {"kind": kind, "overlap": overlap, "k": args.k, "waves_per_launch": per,
+                   "us_per_launch_events": round(us, 2)}
+            for key, xs in rows.items():
+                rec[key + "_us_med"] = round(float(np.median(xs)), 2) if xs else None
+            rec["xcc_end_us_med"] = {x: round(float(np.median(v)), 2) for x, v in xcc_end.items() if v}
+            wave_life = r1 - r0
+            rec["wave_life_us_p10_p50_p90"] = [round(float(np.percentile(wave_life, q)), 2) for q in (10, 50, 90)]
+            out.append(rec)
+            print(json.dumps(rec), flush=True)
+    lib.hdfs3x_set_variant(0)
+    lib.hdfs3x_wave_stamps(None, 0)
+    assert not bool((res != 0).any().item()), "clean blocks reported bad"
+
+
+if __name__ == "__main__":
+    main()
