@@ -700,14 +700,14 @@ __global__ __launch_bounds__(kBlockThreads) void crc32c_packets_kernel(
 // 100 MHz, so the ratio of their deltas is the shader clock over that workgroup's lifetime. Vector
 // stores and a vector atomic only; nothing when no buffer is set.
 // With a wave buffer installed (hdfs3x_wave_stamps, tools/wave_spread.py) lane 0 of EVERY wave also
-// records {realtime start, realtime end, shader clocks elapsed, HW_ID | XCC_ID << 32 | wave << 40}:
+// records {realtime start, realtime end, shader clocks elapsed, HW_ID | XCC_ID << 32 | wave << 36 |
+// launch << 52}:
 // where each launch's time goes between its first wave's start and its last wave's end.
 __device__ unsigned long long *g_lab_clk = nullptr;
 __device__ unsigned int g_lab_clk_cap = 0;
 __device__ unsigned int g_lab_clk_n = 0;
 __device__ unsigned long long *g_lab_wave = nullptr;
 __device__ unsigned int g_lab_wave_cap = 0;
-__device__ unsigned int g_lab_wave_n = 0;
 struct LabClock {
     unsigned long long t0 = 0, r0 = 0;
     __device__ __forceinline__ void start() {
@@ -716,7 +716,10 @@ struct LabClock {
             r0 = __builtin_amdgcn_s_memrealtime();
         }
     }
-    __device__ __forceinline__ void end() {
+    // seq: the launch's number (host counter g_lab_seq): wave w of launch seq owns slot
+    // (seq * waves + w) % cap, so no two waves meet on an atomic (a shared counter serialised
+    // 4,096 waves per launch and stretched a 128 MiB launch 8x)
+    __device__ __forceinline__ void end(uint32_t seq = 0) {
         if ((threadIdx.x & 63) != 0) return;
         const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         if (blockIdx.x == 0 && threadIdx.x == 0 && g_lab_clk) {
@@ -732,14 +735,13 @@ struct LabClock {
             // HW_ID (hwreg 4, 32 bits: wave/simd/cu/sh/se) and XCC_ID (hwreg 20, low 4 bits)
             const unsigned long long hw = uint32_t(__builtin_amdgcn_s_getreg((31 << 11) | 4));
             const unsigned long long xcc = uint32_t(__builtin_amdgcn_s_getreg((3 << 11) | 20));
-            const unsigned long long wv = uint64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
-            const unsigned int i = atomicAdd(&g_lab_wave_n, 1u);
-            if (i < g_lab_wave_cap) {
-                g_lab_wave[4 * i] = r0;
-                g_lab_wave[4 * i + 1] = r1;
-                g_lab_wave[4 * i + 2] = t1 - t0;
-                g_lab_wave[4 * i + 3] = hw | xcc << 32 | wv << 40;
-            }
+            const uint64_t wpl = uint64_t(gridDim.x) * (blockDim.x / 64);
+            const uint64_t wv = uint64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
+            const uint64_t i = (uint64_t(seq) * wpl + wv) % g_lab_wave_cap;
+            g_lab_wave[4 * i] = r0;
+            g_lab_wave[4 * i + 1] = r1;
+            g_lab_wave[4 * i + 2] = t1 - t0;
+            g_lab_wave[4 * i + 3] = hw | (xcc & 15) << 32 | (wv & 0xFFFF) << 36 | uint64_t(seq & 0xFFF) << 52;
         }
     }
 };
@@ -747,7 +749,7 @@ struct LabClock {
 
 template <bool NT>
 __global__ __launch_bounds__(256) void stream_read_kernel(const uint8_t *__restrict__ d,
-                                                          uint64_t n16, uint32_t *sink) {
+                                                          uint64_t n16, uint32_t *sink, uint32_t seq) {
     auto ld = [](const uint8_t *p) -> u32x4 {
         if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
         return ld16(p);
@@ -771,7 +773,9 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const uint8_t *__restr
     }
     if (acc == 0x9E3779B9u) sink[0] = acc;  // keep the loads live
 #if HDFS3_LAB
-    clk.end();
+    clk.end(seq);
+#else
+    (void)seq;
 #endif
 }
 

@@ -113,14 +113,14 @@ hipError_t lab_clock_buffer(unsigned long long *d, unsigned int cap, unsigned in
 }
 
 hipError_t lab_wave_buffer(unsigned long long *d, unsigned int cap, unsigned int *n_out) {
-    unsigned int n = 0;
-    hipError_t e = hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_lab_wave_n), sizeof n);
-    if (e != hipSuccess) return e;
-    if (n_out) *n_out = n;
-    const unsigned int zero = 0;
-    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_lab_wave), &d, sizeof d)) != hipSuccess) return e;
+    // *n_out = launches stamped since the previous install; the launch counter restarts at 0
+    if (n_out) *n_out = g_lab_seq.exchange(0);
+    hipError_t e;
+    const unsigned long long *none = nullptr;  // no stamps while the pair changes
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_lab_wave), &none, sizeof none)) != hipSuccess) return e;
+    if (!d || !cap) return hipSuccess;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_lab_wave_cap), &cap, sizeof cap)) != hipSuccess) return e;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_lab_wave_n), &zero, sizeof zero);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_lab_wave), &d, sizeof d);
 }
 
 hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, int grid,
@@ -131,9 +131,10 @@ hipError_t launch_stream_read(const uint8_t *d, uint64_t len, uint32_t *sink, in
     const dim3 g(nt ? -grid : grid), b(256);
     auto k = nt ? stream_read_kernel<true> : stream_read_kernel<false>;
     if (overlap_previous)
-        hipExtLaunchKernelGGL(k, g, b, 0, stream, nullptr, nullptr, hipExtAnyOrderLaunch, d, len / 16, sink);
+        hipExtLaunchKernelGGL(k, g, b, 0, stream, nullptr, nullptr, hipExtAnyOrderLaunch, d, len / 16, sink,
+                              g_lab_seq++);
     else
-        hipLaunchKernelGGL(k, g, b, 0, stream, d, len / 16, sink);
+        hipLaunchKernelGGL(k, g, b, 0, stream, d, len / 16, sink, g_lab_seq++);
     return hipGetLastError();
 }
 

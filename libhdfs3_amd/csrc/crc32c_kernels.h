@@ -5,6 +5,8 @@
 #include <cstddef>
 #include <cstdint>
 
+#include <atomic>
+
 namespace hdfs3crc {
 
 // Workgroup geometry: the bank-replicated slice-table image takes 128 KiB of
@@ -36,7 +38,11 @@ struct ChunkLaunch {
     // Round kernel (launch_wave3 fills these): a wave's round count is kq + (wave < kr), the units of
     // the launch split over its waves on the host, so no wave divides 64-bit values in its prologue.
     uint32_t kq = 0, kr = 0;
+    uint32_t lab_seq = 0;  // lab clock stamps only (LabClock): the launch's number
 };
+
+// lab clock stamps: launches numbered by the host (kernel argument), see LabClock
+inline std::atomic<uint32_t> g_lab_seq{0};
 
 // Packet-descriptor as seen by the device (mirrors hdfs3_pkt_desc).
 struct DevPacket {
@@ -149,7 +155,8 @@ void set_variant(int v);
 extern int g_variant;
 // clock stamps (LabClock): install a device buffer of cap x 4 words; *n_out = stamps in the previous one
 hipError_t lab_clock_buffer(unsigned long long *d, unsigned int cap, unsigned int *n_out);
-// every wave's stamps (LabClock with a wave buffer): cap x 4 words; *n_out = stamps in the previous one
+// every wave's stamps (LabClock with a wave buffer): cap x 4 words; *n_out = launches stamped into the
+// previous one
 hipError_t lab_wave_buffer(unsigned long long *d, unsigned int cap, unsigned int *n_out);
 // The A/B variants (crc32c_experiments.hip): variant != 0, bpc with a whole-round kernel.
 hipError_t launch_experiment(int variant, const ChunkLaunch &a, bool verify, const uint32_t *tab,

@@ -622,7 +622,7 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
             slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     }
 #if HDFS3_LAB
-    if constexpr ((LAB & kLabClock) != 0) clk.end();
+    if constexpr ((LAB & kLabClock) != 0) clk.end(a.lab_seq);
 #endif
 }
 
@@ -694,6 +694,7 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     const uint64_t nwaves = uint64_t(grid) * (TPB / 64);
     if (units / nwaves >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
     ChunkLaunch b = a;
+    if constexpr ((LAB & kLabClock) != 0) b.lab_seq = g_lab_seq++;
     b.kq = uint32_t(units / nwaves);
     b.kr = uint32_t(units % nwaves);
     // Verify launches below 64 MiB take smaller workgroups (round 4): a 1024-thread workgroup fills a

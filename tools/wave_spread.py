@@ -2,8 +2,8 @@
 """Where a 128 MiB launch's time goes, wave by wave (barriered launches at 0.87 of
 the read kernel's per-block rate). Lane 0 of every wave of the stamping kernels (lab variant 125 =
 production verify + LabClock, and the plain stream read) records its realtime start/end (100 MHz),
-its shader clocks and its XCC (LabClock wave buffer, crc32c_device.h). Per launch (waves sorted by
-start and cut into launches of the grid's wave count; dispatch is in order):
+its shader clocks and its XCC (LabClock wave buffer, crc32c_device.h). Every wave carries its launch's
+number (a kernel argument: no atomics in the stamping path). Per launch:
   gap        previous launch's last wave end -> this launch's first wave start
   ramp       first -> last wave start (dispatch)
   body       last wave start -> first wave end
@@ -82,7 +82,7 @@ def main():
         b.record(stream)
         torch.cuda.synchronize()
         n = lib.hdfs3x_wave_stamps(None, 0)
-        st = stamps[:4 * min(n, cap)].view(-1, 4).cpu().numpy()
+        st = stamps.view(-1, 4).cpu().numpy()
         return a.elapsed_time(b) * 1e3 / k, n, st
 
     out = []
@@ -91,15 +91,17 @@ def main():
         lib.hdfs3x_set_variant(args.variant if kind == "crc" else 0)
         for overlap in (False, True):
             us, n, st = region(fn, overlap, args.k)
-            if n > cap or n % args.k:
-                print(json.dumps({"kind": kind, "overlap": overlap, "error": f"{n} stamps for {args.k} launches"}))
+            st = st[st[:, 1] != 0]  # stamped slots
+            per = len(st) // max(n, 1)
+            if n != args.k or per * n != len(st) or len(st) >= cap:
+                print(json.dumps({"kind": kind, "overlap": overlap, "error": f"{len(st)} stamps, {n} launches"}))
                 continue
-            per = n // args.k
-            st = st[np.argsort(st[:, 0], kind="stable")]
+            seq = (st[:, 3].astype(np.uint64) >> np.uint64(52)).astype(np.int64)
+            st = st[np.lexsort((st[:, 0], seq))]  # by launch, then start
             r0 = st[:, 0].astype(np.float64) / 100.0  # us
             r1 = st[:, 1].astype(np.float64) / 100.0
             clk = st[:, 2].astype(np.float64)
-            xcc = (st[:, 3] >> 32) & 0xFF
+            xcc = (st[:, 3] >> 32) & 0xF
             rows = {"gap": [], "ramp": [], "body": [], "tail": [], "span": [], "mhz": []}
             xcc_end = {x: [] for x in range(8)}
             prev_end = None
@@ -122,7 +124,7 @@ def main():
             rec = {"kind": kind, "overlap": overlap, "k": args.k, "waves_per_launch": per,
                    "us_per_launch_events": round(us, 2)}
             for key, xs in rows.items():
-                rec[key + "_us_med"] = round(float(np.median(xs)), 2) if xs else None
+                rec[key + ("_med" if key == "mhz" else "_us_med")] = round(float(np.median(xs)), 2) if xs else None
             rec["xcc_end_us_med"] = {x: round(float(np.median(v)), 2) for x, v in xcc_end.items() if v}
             wave_life = r1 - r0
             rec["wave_life_us_p10_p50_p90"] = [round(float(np.percentile(wave_life, q)), 2) for q in (10, 50, 90)]
