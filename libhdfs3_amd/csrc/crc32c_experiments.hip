@@ -59,6 +59,16 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabStageWin>(a, tab, fold, grid_cap, s);
         case 128:  // compute: staged words through plain global stores (production before round 4)
             return launch_wave3<BPC, V, false, true, kLabStorePlain>(a, tab, fold, grid_cap, s);
+        case 138:  // verify at bpc <= 2048: rounds claimed from the workgroup's pool (kLabDyn, DynWalk)
+            if constexpr (BPC <= 2048) {
+                if (V) return launch_wave3<BPC, true, false, true, kLabDyn>(a, tab, fold, grid_cap, s);
+            }
+            return hipErrorNotSupported;
+        case 139:  // 138 with clock stamps (tools/wave_spread.py --variant 139)
+            if constexpr (BPC <= 2048) {
+                if (V) return launch_wave3<BPC, true, false, true, kLabDyn | kLabClock>(a, tab, fold, grid_cap, s);
+            }
+            return hipErrorNotSupported;
         case 137:  // verify: 1024-thread workgroups at every launch size (production before round 4)
             return launch_wave3<BPC, V, false, true, kLabWg1024>(a, tab, fold, grid_cap, s);
         case 132:  // 256-thread workgroups (4 waves each): small launches spread over 4x the CUs

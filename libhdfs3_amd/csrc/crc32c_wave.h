@@ -43,6 +43,7 @@ constexpr int kLabStageWin = 2048;  // compute at bpc 512: staged words past kSt
 constexpr int kLabClock = 4096;     // clock stamps of workgroup 0 (LabClock, crc32c_device.h; lab builds only)
 constexpr int kLabStorePlain = 8192;  // compute, staged words: plain global stores (production before round 4)
 constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every launch size (production before round 4)
+constexpr int kLabDyn = 32768;       // verify at bpc <= 2048: rounds claimed at run time from the workgroup's pool (DynWalk)
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
 // written as whole lines, §4.1; past the window size in windows)
@@ -82,6 +83,7 @@ struct WView {
 template <int CPU>
 struct BlockWalk {
     static constexpr bool kLaneView = true;
+    static constexpr bool kDynamic = false;
     static constexpr bool kContiguous = true;  // unit u's words at words + 4 * CPU * u
     const uint8_t *data;
     uint8_t *words;
@@ -97,12 +99,55 @@ struct BlockWalk {
     }
 };
 
+// Rounds of one contiguous block claimed at run time (kLabDyn, verify): the workgroup's rounds under
+// BlockWalk's split -- round k of its wave s is pool entry c = k * WPB + s, unit wgbase + s + k * stride --
+// form a pool [0, total) that its waves take in pairs (c, c + 1: two adjacent units) from a counter in
+// LDS. Every wave's first two pairs are fixed (c = 2s, 2s + 1 and 2 WPB + 2s, + 1); a step claims the
+// pair it will prefetch two steps later (begin_step, one LDS atomic from lane 0, its result read at the
+// step's end). The waves the SIMD arbiter starves take fewer rounds instead of ending the workgroup
+// late: a barriered 128 MiB launch's waves lived 12.4 / 16.3 / 20.3 us (p10 / p50 / p90) with 8 rounds
+// each (tools/wave_spread.py). K stays ~0 until the wave's first claim past the pool.
+template <int CPU>
+struct DynWalk {
+    static constexpr bool kLaneView = false;
+    static constexpr bool kContiguous = true;
+    static constexpr bool kDynamic = true;
+    const uint8_t *data;
+    uint8_t *words;
+    uint64_t key0, wgbase, stride;
+    uint32_t *ctr;  // LDS claim counter
+    uint32_t slot, wpb, total;
+    uint32_t K;
+    const uint8_t *dummy;
+    uint32_t pend = 0, cbase = 0;
+    __device__ __forceinline__ void begin_step() {
+        if ((threadIdx.x & 63) == 0) pend = __hip_atomic_fetch_add(ctr, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ __forceinline__ WView view(uint32_t k) {
+        uint32_t c;
+        if (k < 4) {
+            c = (k >> 1) * 2 * wpb + 2 * slot + (k & 1);
+        } else if ((k & 1) == 0) {
+            cbase = __builtin_amdgcn_readfirstlane(pend);
+            c = cbase;
+        } else {
+            c = cbase + 1;
+        }
+        const bool in = c < total;
+        if (!in && K == ~0u) K = k;  // claims only grow: every later round is past the pool too
+        const uint64_t u = wgbase + c % wpb + uint64_t(c / wpb) * stride;
+        return WView{in ? data + u * kRoundBytes : dummy, in ? words + 4 * CPU * u : const_cast<uint8_t *>(dummy),
+                     key0 + CPU * u};
+    }
+};
+
 // A packet stream at one pitch: every packet but the last holds 1 << L whole rounds; its words sit
 // at words + packet * wpitch (the wire layout: in the packet; a [blocks, words] tensor: their own
 // pitch). Keys are (packet << 32) | chunk.
 template <int CPU>
 struct PitchWalk {
     static constexpr bool kLaneView = true;
+    static constexpr bool kDynamic = false;
     static constexpr bool kContiguous = false;
     const uint8_t *data;
     uint8_t *words;
@@ -127,6 +172,7 @@ struct PitchWalk {
 template <int CPU, bool UNI>
 struct SegWalk {
     static constexpr bool kLaneView = false;
+    static constexpr bool kDynamic = false;
     static constexpr bool kContiguous = false;
     // The launch record and the descriptors through the CONSTANT address space: their fields are
     // wave-uniform, so they load with s_load (lgkmcnt). Through a generic pointer they compiled to
@@ -210,7 +256,8 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = lane % G;
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
-    const uint32_t K = walk.K;
+    const uint32_t K = walk.K;  // Walk::kDynamic: walk.K, read where it is needed (it is set while running)
+    static_assert(!Walk::kDynamic || (VERIFY && G <= 32), "claimed rounds: verify with the half fold image");
 
     // lean fill: each of the image's 1024 slice-table words replicated 32x (TPB threads take 1024 / TPB
     // words each); for G <= 32 the half fold image
@@ -254,6 +301,9 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             dst[0] = n0[f];
             dst[1] = n1[f];
         }
+    }
+    if constexpr (Walk::kDynamic) {
+        if (threadIdx.x == 0) *walk.ctr = 4 * walk.wpb;  // the fixed first two pairs of every wave
     }
     lds_barrier();
     const Lut t(lds);
@@ -409,7 +459,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             }
             return;
         }
-        if (k >= K || j != 0) return;
+        if (k >= (Walk::kDynamic ? walk.K : K) || j != 0) return;
         const uint32_t c = y;
         if constexpr (VERIFY) {
             // the diagnostics compute wrong CRCs: compare inverted so they do not flag every chunk
@@ -463,7 +513,8 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // are in flight per wave (128 KiB per CU), not 16: more requests in flight lower the DRAM
     // efficiency. kLabEarly (lab A/B): issued at the start of the step.
     // priority by rounds left (kPrioMinRounds); wave-uniform, so the branches are SALU
-    const bool use_prio = (LAB & kLabPrio) != 0 || ((LAB & kLabNoPrio) == 0 && K >= kPrioMinRounds);
+    const bool use_prio =
+        !Walk::kDynamic && ((LAB & kLabPrio) != 0 || ((LAB & kLabNoPrio) == 0 && K >= kPrioMinRounds));
     auto prio = [&](uint32_t k) {
         if (use_prio) {
             const uint32_t left = K > k ? K - k : 0;
@@ -475,6 +526,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     };
     auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k) {
         prio(k);
+        if constexpr (Walk::kDynamic) walk.begin_step();
         const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
         if constexpr (!LATE) {
             load_round_buf<true>(p0, pv0.p, lane_off);
@@ -505,7 +557,15 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // in it is the same code: an exit from the middle of the body, or a special last step that values
     // reach from both buffer sets, makes the register allocator copy the rounds (32 v_mov per step).
     const uint32_t nr = (K + 1) & ~1u;  // rounds rounded up to whole steps
-    if constexpr (SOLO) {
+    if constexpr (Walk::kDynamic) {
+        // pair k + 2's views were resolved two steps back: walk.K is final for it
+        for (uint32_t k = 0;; k += 4) {
+            step(a0, a1, b0, b1, k);
+            if (k + 2 >= walk.K) break;
+            step(b0, b1, a0, a1, k + 2);
+            if (k + 4 >= walk.K) break;
+        }
+    } else if constexpr (SOLO) {
         // The last step outside the loop, its two rounds as single chains one after the other: the
         // first chain overlaps the second round's arrival, and only one round's lookups remain once
         // the wave's last data has landed. Its buffers are STATIC: with F = nr / 2 - 1 full steps,
@@ -615,6 +675,14 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
         if (a.last_len % kRoundBytes)  // wave-uniform: a stream of whole rounds has no slow region
             slow_region<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
                                      a.check_short_tail, a.result);
+    } else if constexpr ((LAB & kLabDyn) != 0 && VERIFY && BPC <= 2048) {
+        const uint64_t wgbase = uint64_t(blockIdx.x) * kWpb;
+        const uint32_t extra = a.kr > wgbase ? uint32_t(a.kr - wgbase < kWpb ? a.kr - wgbase : kWpb) : 0u;
+        DynWalk<kCpu> w{a.data, words, a.chunk_base, wgbase, nwaves, lds + kLdsBytesWave / 4 - 1,
+                        uint32_t(wave - wgbase), uint32_t(kWpb), kWpb * a.kq + extra, ~0u, dummy};
+        wave_rounds<BPC, VERIFY, false, false, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
+        if (a.len % kRoundBytes)
+            slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     } else {
         BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, K, dummy, a.kq, a.kr};
         wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
