@@ -64,6 +64,21 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
                 if (V) return launch_wave3<BPC, true, false, true, kLabDyn>(a, tab, fold, grid_cap, s);
             }
             return hipErrorNotSupported;
+        case 140:  // verify at bpc <= 2048: every wave's last 2 rounds claimed from XCD-wide pools (kLabXDyn)
+            if constexpr (BPC <= 2048) {
+                if (V) return launch_wave3<BPC, true, false, true, kLabXDyn>(a, tab, fold, grid_cap, s);
+            }
+            return hipErrorNotSupported;
+        case 141:  // the last 4 rounds
+            if constexpr (BPC <= 2048) {
+                if (V) return launch_wave3<BPC, true, false, true, kLabXDyn | kLabXDyn4>(a, tab, fold, grid_cap, s);
+            }
+            return hipErrorNotSupported;
+        case 142:  // 141 with clock stamps
+            if constexpr (BPC <= 2048) {
+                if (V) return launch_wave3<BPC, true, false, true, kLabXDyn | kLabXDyn4 | kLabClock>(a, tab, fold, grid_cap, s);
+            }
+            return hipErrorNotSupported;
         case 139:  // 138 with clock stamps (tools/wave_spread.py --variant 139)
             if constexpr (BPC <= 2048) {
                 if (V) return launch_wave3<BPC, true, false, true, kLabDyn | kLabClock>(a, tab, fold, grid_cap, s);

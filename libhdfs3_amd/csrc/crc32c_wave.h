@@ -44,6 +44,8 @@ constexpr int kLabClock = 4096;     // clock stamps of workgroup 0 (LabClock, cr
 constexpr int kLabStorePlain = 8192;  // compute, staged words: plain global stores (production before round 4)
 constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every launch size (production before round 4)
 constexpr int kLabDyn = 32768;       // verify at bpc <= 2048: rounds claimed at run time from the workgroup's pool (DynWalk)
+constexpr int kLabXDyn = 65536;      // verify at bpc <= 2048: the last rounds claimed from an XCD-wide pool (XDynWalk)
+constexpr int kLabXDyn4 = 131072;    // with kLabXDyn: the last 4 rounds of every wave instead of 2
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
 // written as whole lines, §4.1; past the window size in windows)
@@ -82,6 +84,7 @@ struct WView {
 // words' addresses at flush time); a walk without it holds each word's address instead.
 template <int CPU>
 struct BlockWalk {
+    static constexpr bool kGlobal = false;
     static constexpr bool kLaneView = true;
     static constexpr bool kDynamic = false;
     static constexpr bool kContiguous = true;  // unit u's words at words + 4 * CPU * u
@@ -112,6 +115,7 @@ struct DynWalk {
     static constexpr bool kLaneView = false;
     static constexpr bool kContiguous = true;
     static constexpr bool kDynamic = true;
+    static constexpr bool kGlobal = false;
     const uint8_t *data;
     uint8_t *words;
     uint64_t key0, wgbase, stride;
@@ -120,7 +124,7 @@ struct DynWalk {
     uint32_t K;
     const uint8_t *dummy;
     uint32_t pend = 0, cbase = 0;
-    __device__ __forceinline__ void begin_step() {
+    __device__ __forceinline__ void begin_step(uint32_t) {
         if ((threadIdx.x & 63) == 0) pend = __hip_atomic_fetch_add(ctr, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __device__ __forceinline__ WView view(uint32_t k) {
@@ -141,11 +145,65 @@ struct DynWalk {
     }
 };
 
+// The first S rounds of every wave as BlockWalk assigns them, the rest of the launch claimed at run
+// time (kLabXDyn, verify): a barriered 128 MiB launch's workgroups -- one per CU -- took 15-21 us for
+// equal work (tools/wave_spread.py: the pool inside a workgroup, DynWalk, evens out its waves but not
+// the CUs). Units past S * W (W = waves of the launch) form 8 pools, pool x = the runs of WPB units
+// that workgroups b = x mod 8 own under the static split (a workgroup of pool x takes from pool x
+// only; with round-robin dispatch that is one XCD). Claims are pairs of adjacent units through an
+// agent-scope atomic on the launch's counter (ctr: 8 counters per launch, zeroed 128 launches ahead
+// by the launch itself), issued two steps before the pair is needed.
+template <int CPU>
+struct XDynWalk {
+    static constexpr bool kLaneView = false;
+    static constexpr bool kContiguous = true;
+    static constexpr bool kDynamic = true;
+    static constexpr bool kGlobal = true;
+    const uint8_t *data;
+    uint8_t *words;
+    uint64_t key0, first, stride, units;
+    uint32_t *ctr;
+    uint32_t S, x, wpb, ngrp;  // ngrp: workgroups per pool per row (grid / 8)
+    uint32_t K;
+    const uint8_t *dummy;
+    bool dyn;  // false: the launch is too short for the pools (S = the wave's own round count)
+    uint32_t pend = 0, cbase = 0;
+    __device__ __forceinline__ void begin_step(uint32_t k) {
+        if (dyn && k + 4 >= S && (threadIdx.x & 63) == 0)
+            pend = __hip_atomic_fetch_add(ctr, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ __forceinline__ WView view(uint32_t k) {
+        uint64_t u;
+        bool in = true;
+        if (k < S) {
+            u = first + uint64_t(k) * stride;
+        } else if (!dyn) {
+            u = 0;
+            in = false;
+        } else {
+            uint32_t c;
+            if (((k - S) & 1) == 0) {
+                cbase = __builtin_amdgcn_readfirstlane(pend);
+                c = cbase;
+            } else {
+                c = cbase + 1;
+            }
+            const uint32_t per_row = ngrp * wpb, row = c / per_row, j = c % per_row;
+            u = uint64_t(S + row) * stride + uint64_t(j / wpb) * (8 * wpb) + x * wpb + j % wpb;
+            in = u < units;
+            if (!in && K == ~0u) K = k;
+        }
+        return WView{in ? data + u * kRoundBytes : dummy, in ? words + 4 * CPU * u : const_cast<uint8_t *>(dummy),
+                     key0 + CPU * u};
+    }
+};
+
 // A packet stream at one pitch: every packet but the last holds 1 << L whole rounds; its words sit
 // at words + packet * wpitch (the wire layout: in the packet; a [blocks, words] tensor: their own
 // pitch). Keys are (packet << 32) | chunk.
 template <int CPU>
 struct PitchWalk {
+    static constexpr bool kGlobal = false;
     static constexpr bool kLaneView = true;
     static constexpr bool kDynamic = false;
     static constexpr bool kContiguous = false;
@@ -171,6 +229,7 @@ struct PitchWalk {
 // increasing round order (the core resolves the next step's views at the end of each step).
 template <int CPU, bool UNI>
 struct SegWalk {
+    static constexpr bool kGlobal = false;
     static constexpr bool kLaneView = false;
     static constexpr bool kDynamic = false;
     static constexpr bool kContiguous = false;
@@ -302,7 +361,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             dst[1] = n1[f];
         }
     }
-    if constexpr (Walk::kDynamic) {
+    if constexpr (Walk::kDynamic && !Walk::kGlobal) {
         if (threadIdx.x == 0) *walk.ctr = 4 * walk.wpb;  // the fixed first two pairs of every wave
     }
     lds_barrier();
@@ -526,7 +585,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     };
     auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k) {
         prio(k);
-        if constexpr (Walk::kDynamic) walk.begin_step();
+        if constexpr (Walk::kDynamic) walk.begin_step(k);
         const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
         if constexpr (!LATE) {
             load_round_buf<true>(p0, pv0.p, lane_off);
@@ -675,6 +734,20 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
         if (a.last_len % kRoundBytes)  // wave-uniform: a stream of whole rounds has no slow region
             slow_region<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
                                      a.check_short_tail, a.result);
+    } else if constexpr ((LAB & kLabXDyn) != 0 && VERIFY && BPC <= 2048) {
+#if HDFS3_LAB
+        // the launch's 8 counters; the launch 128 ahead's zeroed here (no launch runs 128 behind)
+        uint32_t *ctrs = g_lab_claim + 8 * (a.lab_seq % kLabClaimRing);
+        if (blockIdx.x == 0 && threadIdx.x < 8)
+            g_lab_claim[8 * ((a.lab_seq + kLabClaimRing / 2) % kLabClaimRing) + threadIdx.x] = 0u;
+        constexpr uint32_t D = (LAB & kLabXDyn4) ? 4u : 2u;
+        const bool dyn = a.kq >= 4 + D && gridDim.x % 8 == 0;
+        XDynWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, a.len / kRoundBytes, ctrs + blockIdx.x % 8,
+                         dyn ? a.kq - D : K, blockIdx.x % 8, uint32_t(kWpb), gridDim.x / 8, dyn ? ~0u : K, dummy, dyn};
+        wave_rounds<BPC, VERIFY, false, false, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
+        if (a.len % kRoundBytes)
+            slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
+#endif
     } else if constexpr ((LAB & kLabDyn) != 0 && VERIFY && BPC <= 2048) {
         const uint64_t wgbase = uint64_t(blockIdx.x) * kWpb;
         const uint32_t extra = a.kr > wgbase ? uint32_t(a.kr - wgbase < kWpb ? a.kr - wgbase : kWpb) : 0u;
@@ -762,7 +835,7 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     const uint64_t nwaves = uint64_t(grid) * (TPB / 64);
     if (units / nwaves >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
     ChunkLaunch b = a;
-    if constexpr ((LAB & kLabClock) != 0) b.lab_seq = g_lab_seq++;
+    if constexpr ((LAB & (kLabClock | kLabXDyn)) != 0) b.lab_seq = g_lab_seq++;
     b.kq = uint32_t(units / nwaves);
     b.kr = uint32_t(units % nwaves);
     // Verify launches below 64 MiB take smaller workgroups (round 4): a 1024-thread workgroup fills a

@@ -385,18 +385,20 @@ def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
         lib.hdfs3x_set_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93, 94, 115, 117, 125, 132, 134, 137, 138])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 115, 117, 125, 132, 134, 137, 138, 140, 141])
 @pytest.mark.parametrize("bpc", [512, 2048, 4096])
 def test_round_kernel_variants_overlapped_match_oracle(lab_ctx, variant, bpc):
     """The round kernel's prefetch/last-step variants as they run in the bench: overlapped
     launches (the solo last step only runs there), sizes giving 1 to 9 rounds per wave so both
     loop copies of the solo form (an even and an odd number of full steps) run, a bad chunk
     located. 138 (rounds claimed from the workgroup's pool): pools shorter than the fixed first
-    pairs, odd pools (a claimed pair's second round past the end), 256/512/1024-thread groups."""
+    pairs, odd pools (a claimed pair's second round past the end), 256/512/1024-thread groups.
+    140/141 (the last 2/4 rounds of every wave claimed from XCD-wide pools): launches too short for
+    the pools, partial last rows, consecutive launches on their own counters."""
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import DeviceBuffer
 
-    if variant == 138 and bpc > 2048:
+    if variant in (138, 140, 141) and bpc > 2048:
         pytest.skip("claimed rounds need the half fold image (bpc <= 2048)")
 
     lib = _native.lab()
