@@ -79,6 +79,12 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
                 if (V) return launch_wave3<BPC, true, false, true, kLabXDyn | kLabXDyn4 | kLabClock>(a, tab, fold, grid_cap, s);
             }
             return hipErrorNotSupported;
+        case 143:  // verify: a workgroup's waves one grid apart (kLabSpread)
+            if (V) return launch_wave3<BPC, true, false, true, kLabSpread>(a, tab, fold, grid_cap, s);
+            return hipErrorNotSupported;
+        case 144:  // 143 with clock stamps
+            if (V) return launch_wave3<BPC, true, false, true, kLabSpread | kLabClock>(a, tab, fold, grid_cap, s);
+            return hipErrorNotSupported;
         case 139:  // 138 with clock stamps (tools/wave_spread.py --variant 139)
             if constexpr (BPC <= 2048) {
                 if (V) return launch_wave3<BPC, true, false, true, kLabDyn | kLabClock>(a, tab, fold, grid_cap, s);

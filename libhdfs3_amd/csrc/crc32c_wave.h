@@ -46,6 +46,7 @@ constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every 
 constexpr int kLabDyn = 32768;       // verify at bpc <= 2048: rounds claimed at run time from the workgroup's pool (DynWalk)
 constexpr int kLabXDyn = 65536;      // verify at bpc <= 2048: the last rounds claimed from an XCD-wide pool (XDynWalk)
 constexpr int kLabXDyn4 = 131072;    // with kLabXDyn: the last 4 rounds of every wave instead of 2
+constexpr int kLabSpread = 262144;   // verify: a workgroup's waves take rounds one grid apart (not 16 adjacent ones)
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
 // written as whole lines, §4.1; past the window size in windows)
@@ -757,7 +758,15 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
         if (a.len % kRoundBytes)
             slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     } else {
-        BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, K, dummy, a.kq, a.kr};
+        // kLabSpread: wave (b, s) starts at unit s * grid + b, so a step's 16 rounds of one workgroup lie
+        // 1 MiB apart (128 MiB launch) instead of forming one 64 KiB run
+        uint64_t first = wave;
+        uint32_t Kw = K;
+        if constexpr ((LAB & kLabSpread) != 0 && VERIFY) {
+            first = rfl64(uint64_t(threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+            Kw = a.kq + (first < a.kr ? 1u : 0u);
+        }
+        BlockWalk<kCpu> w{a.data, words, a.chunk_base, first, nwaves, Kw, dummy, a.kq, a.kr};
         wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
         if (a.len % kRoundBytes)  // wave-uniform: a block of whole rounds has no slow region
             slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);

@@ -385,7 +385,7 @@ def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
         lib.hdfs3x_set_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93, 94, 115, 117, 125, 132, 134, 137, 138, 140, 141])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 115, 117, 125, 132, 134, 137, 138, 140, 141, 143])
 @pytest.mark.parametrize("bpc", [512, 2048, 4096])
 def test_round_kernel_variants_overlapped_match_oracle(lab_ctx, variant, bpc):
     """The round kernel's prefetch/last-step variants as they run in the bench: overlapped
@@ -394,7 +394,8 @@ def test_round_kernel_variants_overlapped_match_oracle(lab_ctx, variant, bpc):
     located. 138 (rounds claimed from the workgroup's pool): pools shorter than the fixed first
     pairs, odd pools (a claimed pair's second round past the end), 256/512/1024-thread groups.
     140/141 (the last 2/4 rounds of every wave claimed from XCD-wide pools): launches too short for
-    the pools, partial last rows, consecutive launches on their own counters."""
+    the pools, partial last rows, consecutive launches on their own counters. 143 (a workgroup's
+    waves one grid apart): the extra rounds of a partial last row by permuted start."""
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import DeviceBuffer
 

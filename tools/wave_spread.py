@@ -102,6 +102,9 @@ def main():
             r1 = st[:, 1].astype(np.float64) / 100.0
             clk = st[:, 2].astype(np.float64)
             xcc = (st[:, 3] >> 32) & 0xF
+            # the CU each wave ran on: XCC and HW_ID's cu/sh/se fields (bits 8-15)
+            cu = (((st[:, 3] >> 32) & 0xF) << 8) | ((st[:, 3] >> 8) & 0xFF)
+            cu_ends = {}  # CU -> [its last wave end - launch start, per launch]
             rows = {"gap": [], "ramp": [], "body": [], "tail": [], "span": [], "mhz": []}
             xcc_end = {x: [] for x in range(8)}
             prev_end = None
@@ -117,6 +120,11 @@ def main():
                 rows["tail"].append(e1 - e0)
                 rows["span"].append(e1 - a0)
                 rows["mhz"].append(float(np.median(clk[s] / np.maximum((r1[s] - r0[s]) * 100.0, 1) * 100.0)))
+                cs, ends = cu[s], r1[s] - a0
+                order = np.argsort(cs, kind="stable")
+                ucs, first_idx = np.unique(cs[order], return_index=True)
+                for c_id, e in zip(ucs, np.maximum.reduceat(ends[order], first_idx)):
+                    cu_ends.setdefault(int(c_id), []).append(float(e))
                 for x in range(8):
                     m = xcc[s] == x
                     if m.any():
@@ -126,6 +134,17 @@ def main():
             for key, xs in rows.items():
                 rec[key + ("_med" if key == "mhz" else "_us_med")] = round(float(np.median(xs)), 2) if xs else None
             rec["xcc_end_us_med"] = {x: round(float(np.median(v)), 2) for x, v in xcc_end.items() if v}
+            # is a slow CU slow in every launch? the spread of the CUs' mean end over the launches
+            # against the spread inside one launch (equal: the same CUs are late every time)
+            full = [v for v in cu_ends.values() if len(v) == args.k]
+            if full:
+                mat = np.array(full)  # CUs x launches
+                rec["cus"] = len(full)
+                rec["cu_end_within_launch_p10_p90_us"] = [round(float(np.median(np.percentile(mat, q, axis=0))), 2)
+                                                          for q in (10, 90)]
+                rec["cu_mean_end_p10_p90_us"] = [round(float(np.percentile(mat.mean(axis=1), q)), 2) for q in (10, 90)]
+                rec["cu_rank_corr_consecutive"] = round(float(np.median(
+                    [np.corrcoef(mat[:, i], mat[:, i + 1])[0, 1] for i in range(args.k - 1)])), 3)
             wave_life = r1 - r0
             rec["wave_life_us_p10_p50_p90"] = [round(float(np.percentile(wave_life, q)), 2) for q in (10, 50, 90)]
             out.append(rec)
