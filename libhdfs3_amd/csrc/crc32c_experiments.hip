@@ -85,6 +85,8 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
         case 144:  // 143 with clock stamps
             if (V) return launch_wave3<BPC, true, false, true, kLabSpread | kLabClock>(a, tab, fold, grid_cap, s);
             return hipErrorNotSupported;
+        case 145:  // the solo last step on barriered launches too (kLabSoloBar)
+            return launch_wave3<BPC, V, false, true, kLabSoloBar>(a, tab, fold, grid_cap, s);
         case 139:  // 138 with clock stamps (tools/wave_spread.py --variant 139)
             if constexpr (BPC <= 2048) {
                 if (V) return launch_wave3<BPC, true, false, true, kLabDyn | kLabClock>(a, tab, fold, grid_cap, s);

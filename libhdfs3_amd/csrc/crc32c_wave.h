@@ -47,6 +47,7 @@ constexpr int kLabDyn = 32768;       // verify at bpc <= 2048: rounds claimed at
 constexpr int kLabXDyn = 65536;      // verify at bpc <= 2048: the last rounds claimed from an XCD-wide pool (XDynWalk)
 constexpr int kLabXDyn4 = 131072;    // with kLabXDyn: the last 4 rounds of every wave instead of 2
 constexpr int kLabSpread = 262144;   // verify: a workgroup's waves take rounds one grid apart (not 16 adjacent ones)
+constexpr int kLabSoloBar = 524288;  // the solo last step on barriered launches too (production: overlapped only)
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
 // written as whole lines, §4.1; past the window size in windows)
@@ -878,6 +879,13 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
         hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB, TPB>), dim3(grid),
                               dim3(TPB), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, b, tab, nib);
     } else {
+        if constexpr (SOLO && (LAB & kLabSoloBar) != 0) {
+            if (units * kRoundBytes <= kSoloTailMaxBytes) {
+                hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LAB, TPB>), dim3(grid), dim3(TPB), 0, s,
+                                   b, tab, nib);
+                return hipGetLastError();
+            }
+        }
         hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB, TPB>), dim3(grid), dim3(TPB),
                            0, s, b, tab, nib);
     }
