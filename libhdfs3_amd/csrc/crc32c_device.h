@@ -722,7 +722,8 @@ struct LabClock {
     // seq: the launch's number (host counter g_lab_seq): wave w of launch seq owns slot
     // (seq * waves + w) % cap, so no two waves meet on an atomic (a shared counter serialised
     // 4,096 waves per launch and stretched a 128 MiB launch 8x)
-    __device__ __forceinline__ void end(uint32_t seq = 0) {
+    // word2: what word 2 of the wave's stamp holds (default: the shader clocks of its life)
+    __device__ __forceinline__ void end(uint32_t seq = 0, unsigned long long word2 = ~0ull) {
         if ((threadIdx.x & 63) != 0) return;
         const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         if (blockIdx.x == 0 && threadIdx.x == 0 && g_lab_clk) {
@@ -743,7 +744,7 @@ struct LabClock {
             const uint64_t i = (uint64_t(seq) * wpl + wv) % g_lab_wave_cap;
             g_lab_wave[4 * i] = r0;
             g_lab_wave[4 * i + 1] = r1;
-            g_lab_wave[4 * i + 2] = t1 - t0;
+            g_lab_wave[4 * i + 2] = word2 == ~0ull ? t1 - t0 : word2;
             g_lab_wave[4 * i + 3] = hw | (xcc & 15) << 32 | (wv & 0xFFFF) << 36 | uint64_t(seq & 0xFFF) << 52;
         }
     }

@@ -48,6 +48,7 @@ constexpr int kLabXDyn = 65536;      // verify at bpc <= 2048: the last rounds c
 constexpr int kLabXDyn4 = 131072;    // with kLabXDyn: the last 4 rounds of every wave instead of 2
 constexpr int kLabSpread = 262144;   // verify: a workgroup's waves take rounds one grid apart (not 16 adjacent ones)
 constexpr int kLabSoloBar = 524288;  // the solo last step on barriered launches too (production: overlapped only)
+constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = (fill done - start) | (first data - start) << 32
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
 // written as whole lines, §4.1; past the window size in windows)
@@ -309,7 +310,8 @@ struct SegWalk {
 // transposed into one VGPR and up to 8 such VGPRs are stored in one burst. LAB: lab-only bits (kLab*).
 template <int BPC, bool VERIFY, bool SOLO, bool HOLD, int LAB, int TPB, class Walk>
 __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uint32_t *__restrict__ g_tab,
-                                            const uint32_t *__restrict__ g_nib, unsigned long long *result) {
+                                            const uint32_t *__restrict__ g_nib, unsigned long long *result,
+                                            unsigned long long *lab_mid = nullptr) {
     constexpr int G = BPC / 64;
     constexpr bool kHalfFold = G <= 32;
     constexpr bool LATE = (LAB & kLabEarly) == 0, NOMATH = (LAB & kLabNoMath) != 0;
@@ -367,6 +369,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         if (threadIdx.x == 0) *walk.ctr = 4 * walk.wpb;  // the fixed first two pairs of every wave
     }
     lds_barrier();
+    if constexpr ((LAB & kLabMid) != 0) lab_mid[0] = __builtin_amdgcn_s_memrealtime();
     const Lut t(lds);
     const NibFold nf(lds);
     auto fold = [&](uint32_t x) -> uint32_t {
@@ -596,6 +599,9 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         __builtin_amdgcn_sched_barrier(0);
         regroup(c0);
         regroup(c1);
+        if constexpr ((LAB & kLabMid) != 0) {
+            if (k == 0) lab_mid[1] = __builtin_amdgcn_s_memrealtime();  // the first rounds' data landed
+        }
         if constexpr (LATE) {
             __builtin_amdgcn_sched_barrier(0);
             load_round_buf<true>(p0, pv0.p, lane_off);
@@ -724,6 +730,7 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
     constexpr bool kHold = !VERIFY && BPC == 512 && (LAB & kLabNoHold) == 0;
     // the wave's round count from the host's split (ChunkLaunch::kq/kr): SALU only
     const uint32_t K = a.kq + (wave < a.kr ? 1u : 0u);
+    unsigned long long lab_mid[2] = {0, 0};  // kLabMid only
 #if HDFS3_LAB
     LabClock clk;
     if constexpr ((LAB & kLabClock) != 0) clk.start();
@@ -768,12 +775,17 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
             Kw = a.kq + (first < a.kr ? 1u : 0u);
         }
         BlockWalk<kCpu> w{a.data, words, a.chunk_base, first, nwaves, Kw, dummy, a.kq, a.kr};
-        wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
+        wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result, lab_mid);
         if (a.len % kRoundBytes)  // wave-uniform: a block of whole rounds has no slow region
             slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     }
 #if HDFS3_LAB
-    if constexpr ((LAB & kLabClock) != 0) clk.end(a.lab_seq);
+    if constexpr ((LAB & kLabClock) != 0) {
+        if constexpr ((LAB & kLabMid) != 0)
+            clk.end(a.lab_seq, (lab_mid[0] - clk.r0) | (lab_mid[1] - clk.r0) << 32);
+        else
+            clk.end(a.lab_seq);
+    }
 #endif
 }
 

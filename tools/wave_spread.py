@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--kinds", default="crc,read")
     ap.add_argument("--read-grid", type=int, default=-512)
     ap.add_argument("--variant", type=int, default=125)
+    ap.add_argument("--mid", action="store_true", help="variant 146: word 2 holds the fill-done and first-data "
+                    "times of the wave (kLabMid) instead of its shader clocks")
     args = ap.parse_args()
 
     import numpy as np
@@ -145,6 +147,19 @@ def main():
                 rec["cu_mean_end_p10_p90_us"] = [round(float(np.percentile(mat.mean(axis=1), q)), 2) for q in (10, 90)]
                 rec["cu_rank_corr_consecutive"] = round(float(np.median(
                     [np.corrcoef(mat[:, i], mat[:, i + 1])[0, 1] for i in range(args.k - 1)])), 3)
+            if args.mid and kind == "crc":
+                w2 = st[:, 2].astype(np.uint64)
+                fill = (w2 & np.uint64(0xFFFFFFFF)).astype(np.float64) / 100.0
+                first = (w2 >> np.uint64(32)).astype(np.float64) / 100.0
+                rec["fill_done_us_p10_p50_p90"] = [round(float(np.percentile(fill, q)), 2) for q in (10, 50, 90)]
+                rec["first_data_us_p10_p50_p90"] = [round(float(np.percentile(first, q)), 2) for q in (10, 50, 90)]
+                # from the launch's first wave start to every wave's first data
+                lf = []
+                for li in range(args.k):
+                    sl = slice(li * per, (li + 1) * per)
+                    lf.append(np.percentile(r0[sl] + first[sl] - r0[sl].min(), 90))
+                rec["launch_start_to_first_data_p90_us_med"] = round(float(np.median(lf)), 2)
+                rec.pop("mhz_med", None)
             wave_life = r1 - r0
             rec["wave_life_us_p10_p50_p90"] = [round(float(np.percentile(wave_life, q)), 2) for q in (10, 50, 90)]
             out.append(rec)
