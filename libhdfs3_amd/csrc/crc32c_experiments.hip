@@ -89,6 +89,10 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabSoloBar>(a, tab, fold, grid_cap, s);
         case 146:  // production with every wave's fill-done and first-data times (wave_spread.py --variant 146 --mid)
             return launch_wave3<BPC, V, false, true, kLabClock | kLabMid>(a, tab, fold, grid_cap, s);
+        case 147:  // diagnostic: no table loads (wrong results), with fill-done / first-data stamps
+            return launch_wave3<BPC, V, false, true, kLabNoTabLoad | kLabClock | kLabMid>(a, tab, fold, grid_cap, s);
+        case 148:  // diagnostic: no table loads (wrong results)
+            return launch_wave3<BPC, V, false, true, kLabNoTabLoad>(a, tab, fold, grid_cap, s);
         case 139:  // 138 with clock stamps (tools/wave_spread.py --variant 139)
             if constexpr (BPC <= 2048) {
                 if (V) return launch_wave3<BPC, true, false, true, kLabDyn | kLabClock>(a, tab, fold, grid_cap, s);

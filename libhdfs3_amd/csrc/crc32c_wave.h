@@ -48,6 +48,7 @@ constexpr int kLabXDyn = 65536;      // verify at bpc <= 2048: the last rounds c
 constexpr int kLabXDyn4 = 131072;    // with kLabXDyn: the last 4 rounds of every wave instead of 2
 constexpr int kLabSpread = 262144;   // verify: a workgroup's waves take rounds one grid apart (not 16 adjacent ones)
 constexpr int kLabSoloBar = 524288;  // the solo last step on barriered launches too (production: overlapped only)
+constexpr int kLabNoTabLoad = 2097152;  // diagnostic: the table images are not loaded (made up from t: wrong results)
 constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = (fill done - start) | (first data - start) << 32
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
@@ -315,7 +316,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     constexpr int G = BPC / 64;
     constexpr bool kHalfFold = G <= 32;
     constexpr bool LATE = (LAB & kLabEarly) == 0, NOMATH = (LAB & kLabNoMath) != 0;
-    constexpr bool kWrong = (LAB & (kLabNoMath | kLabNoFill)) != 0;  // diagnostics: wrong CRCs (verify)
+    constexpr bool kWrong = (LAB & (kLabNoMath | kLabNoFill | kLabNoTabLoad)) != 0;  // diagnostics: wrong CRCs (verify)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = lane % G;
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
@@ -331,6 +332,12 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
 #pragma unroll
     for (int f = 0; f < kFillIters; ++f) {
         const uint32_t t = threadIdx.x + f * TPB;
+        if constexpr ((LAB & kLabNoTabLoad) != 0) {
+            tw[f] = t * 0x9E3779B9u;
+            n0[f] = u32x4{t, t ^ 1u, t ^ 2u, t ^ 3u};
+            n1[f] = n0[f];
+            continue;
+        }
         tw[f] = g_tab[t];
         if constexpr (kHalfFold) {
             const uint32_t fk = 2 * (t >> 8) + ((t >> 3) & 1), fe = (t >> 4) & 15, fc = 4 * (t & 7);
