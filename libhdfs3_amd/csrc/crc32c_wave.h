@@ -49,7 +49,8 @@ constexpr int kLabXDyn4 = 131072;    // with kLabXDyn: the last 4 rounds of ever
 constexpr int kLabSpread = 262144;   // verify: a workgroup's waves take rounds one grid apart (not 16 adjacent ones)
 constexpr int kLabSoloBar = 524288;  // the solo last step on barriered launches too (production: overlapped only)
 constexpr int kLabNoTabLoad = 2097152;  // diagnostic: the table images are not loaded (made up from t: wrong results)
-constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = (fill done - start) | (first data - start) << 32
+constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = fill done | first data << 21 | kernel
+                                     // arguments landed << 42, each - start, 21 bits of 10 ns
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
 // bpc 512 when its waves have at most kStageMaxRounds(512) rounds (the words are staged in LDS and
 // written as whole lines, §4.1; past the window size in windows)
@@ -737,10 +738,14 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
     constexpr bool kHold = !VERIFY && BPC == 512 && (LAB & kLabNoHold) == 0;
     // the wave's round count from the host's split (ChunkLaunch::kq/kr): SALU only
     const uint32_t K = a.kq + (wave < a.kr ? 1u : 0u);
-    unsigned long long lab_mid[2] = {0, 0};  // kLabMid only
+    unsigned long long lab_mid[3] = {0, 0, 0};  // kLabMid only
 #if HDFS3_LAB
     LabClock clk;
     if constexpr ((LAB & kLabClock) != 0) clk.start();
+    if constexpr ((LAB & kLabMid) != 0) {
+        asm volatile("" ::"s"(a.kq), "s"(a.kr));  // the kernel arguments have landed
+        lab_mid[2] = __builtin_amdgcn_s_memrealtime();
+    }
 #endif
     if constexpr (PITCH) {
         PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves, K, a.upp_log2,
@@ -789,7 +794,8 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
 #if HDFS3_LAB
     if constexpr ((LAB & kLabClock) != 0) {
         if constexpr ((LAB & kLabMid) != 0)
-            clk.end(a.lab_seq, (lab_mid[0] - clk.r0) | (lab_mid[1] - clk.r0) << 32);
+            clk.end(a.lab_seq, ((lab_mid[0] - clk.r0) & 0x1FFFFF) | ((lab_mid[1] - clk.r0) & 0x1FFFFF) << 21 |
+                                   ((lab_mid[2] - clk.r0) & 0x1FFFFF) << 42);
         else
             clk.end(a.lab_seq);
     }

@@ -149,8 +149,11 @@ def main():
                     [np.corrcoef(mat[:, i], mat[:, i + 1])[0, 1] for i in range(args.k - 1)])), 3)
             if args.mid and kind == "crc":
                 w2 = st[:, 2].astype(np.uint64)
-                fill = (w2 & np.uint64(0xFFFFFFFF)).astype(np.float64) / 100.0
-                first = (w2 >> np.uint64(32)).astype(np.float64) / 100.0
+                m21 = np.uint64(0x1FFFFF)
+                fill = (w2 & m21).astype(np.float64) / 100.0
+                first = ((w2 >> np.uint64(21)) & m21).astype(np.float64) / 100.0
+                karg = ((w2 >> np.uint64(42)) & m21).astype(np.float64) / 100.0
+                rec["kernargs_us_p10_p50_p90"] = [round(float(np.percentile(karg, q)), 2) for q in (10, 50, 90)]
                 rec["fill_done_us_p10_p50_p90"] = [round(float(np.percentile(fill, q)), 2) for q in (10, 50, 90)]
                 rec["first_data_us_p10_p50_p90"] = [round(float(np.percentile(first, q)), 2) for q in (10, 50, 90)]
                 # from the launch's first wave start to every wave's first data
