@@ -93,6 +93,10 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabNoTabLoad | kLabClock | kLabMid>(a, tab, fold, grid_cap, s);
         case 148:  // diagnostic: no table loads (wrong results)
             return launch_wave3<BPC, V, false, true, kLabNoTabLoad>(a, tab, fold, grid_cap, s);
+        case 151:  // rounds 2, 3 prefetched in the prologue with rounds 0, 1 (kLabHeadPf)
+            return launch_wave3<BPC, V, false, true, kLabHeadPf>(a, tab, fold, grid_cap, s);
+        case 152:  // 151 with fill-done / first-data stamps
+            return launch_wave3<BPC, V, false, true, kLabHeadPf | kLabClock | kLabMid>(a, tab, fold, grid_cap, s);
         case 139:  // 138 with clock stamps (tools/wave_spread.py --variant 139)
             if constexpr (BPC <= 2048) {
                 if (V) return launch_wave3<BPC, true, false, true, kLabDyn | kLabClock>(a, tab, fold, grid_cap, s);

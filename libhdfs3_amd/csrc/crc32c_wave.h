@@ -48,6 +48,7 @@ constexpr int kLabXDyn = 65536;      // verify at bpc <= 2048: the last rounds c
 constexpr int kLabXDyn4 = 131072;    // with kLabXDyn: the last 4 rounds of every wave instead of 2
 constexpr int kLabSpread = 262144;   // verify: a workgroup's waves take rounds one grid apart (not 16 adjacent ones)
 constexpr int kLabSoloBar = 524288;  // the solo last step on barriered launches too (production: overlapped only)
+constexpr int kLabHeadPf = 4194304;   // the first step's prefetch (rounds 2, 3) issued in the prologue, before the fill
 constexpr int kLabNoTabLoad = 2097152;  // diagnostic: the table images are not loaded (made up from t: wrong results)
 constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = fill done | first data << 21 | kernel
                                      // arguments landed << 42, each - start, 21 bits of 10 ns
@@ -353,6 +354,14 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     Round a0, a1, b0, b1;
     load_round_buf<true>(a0, cv0.p, lane_off);
     load_round_buf<true>(a1, cv1.p, lane_off);
+    // kLabHeadPf: rounds 2, 3 too, so 16 KiB per wave (64 MiB per 128 MiB launch) are in flight while
+    // the tables fill, not 8; step 0 then skips its prefetch
+    constexpr bool kHeadPf = (LAB & kLabHeadPf) != 0 && !Walk::kDynamic;
+    if constexpr (kHeadPf) {
+        const WView h2 = walk.view(2), h3 = walk.view(3);
+        load_round_buf<true>(b0, h2.p, lane_off);
+        load_round_buf<true>(b1, h3.p, lane_off);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int f = 0; f < kFillIters; ++f) {
@@ -612,8 +621,10 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         }
         if constexpr (LATE) {
             __builtin_amdgcn_sched_barrier(0);
-            load_round_buf<true>(p0, pv0.p, lane_off);
-            load_round_buf<true>(p1, pv1.p, lane_off);
+            if (!kHeadPf || k != 0) {
+                load_round_buf<true>(p0, pv0.p, lane_off);
+                load_round_buf<true>(p1, pv1.p, lane_off);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
         uint32_t x0, x1;

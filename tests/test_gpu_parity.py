@@ -385,7 +385,7 @@ def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
         lib.hdfs3x_set_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93, 94, 115, 117, 125, 132, 134, 137, 138, 140, 141, 143, 145])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 115, 117, 125, 132, 134, 137, 138, 140, 141, 143, 145, 151])
 @pytest.mark.parametrize("bpc", [512, 2048, 4096])
 def test_round_kernel_variants_overlapped_match_oracle(lab_ctx, variant, bpc):
     """The round kernel's prefetch/last-step variants as they run in the bench: overlapped
@@ -600,7 +600,7 @@ def test_host_api_random_sizes_and_offsets(gpu_ctx):
         assert gpu_ctx.verify(bad, bpc, want, True) == pos // bpc, (n, off, bpc, pos)
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95, 122, 128, 145])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95, 122, 128, 145, 151])
 @pytest.mark.parametrize("bpc", [512, 4096])
 def test_round_kernel_variants_overlapped_compute_match_oracle(lab_ctx, variant, bpc):
     """Compute-mode variants of the round kernel (held stores or not, solo last step or not) as
