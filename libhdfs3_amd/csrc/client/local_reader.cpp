@@ -110,15 +110,44 @@ void free_resources(LocalResources &r) {
     r.ctx = nullptr;
 }
 
+// pinned / device bytes of a pooled entry: its windows and what its ctx holds
+LocalPoolStats entry_bytes(const LocalResources &r) {
+    LocalPoolStats st;
+    ctx_footprint(r.ctx, &st.pinned, &st.device);
+    for (const PacketArena &a : r.a) {
+        const uint64_t n = a.cap + (a.h_res ? sizeof(unsigned long long) : 0);
+        st.pinned += n;
+        st.device += n;
+    }
+    st.entries = 1;
+    return st;
+}
+
+// Pooled unless that would take the retained pinned bytes of both pools past the cap
+// (HDFS3_POOL_PINNED_MAX): the oldest pooled entries are freed first, then this one.
 void give_back(LocalResources r) {
+    std::vector<LocalResources> evict;
+    bool keep = false;
+    // the ctx pool's bytes first, outside g_pool_mu: ctx_release takes the two locks the other way round
+    const uint64_t cap = pool_pinned_cap_bytes(), ctxs = ctx_pool_pinned_bytes(), mine = entry_bytes(r).pinned;
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
         if (g_pool.size() < kPoolMax) {
-            g_pool.push_back(r);
-            return;
+            uint64_t local = 0;
+            for (const LocalResources &e : g_pool) local += entry_bytes(e).pinned;
+            while (!g_pool.empty() && ctxs + local + mine > cap) {
+                local -= entry_bytes(g_pool.front()).pinned;
+                evict.push_back(g_pool.front());
+                g_pool.erase(g_pool.begin());
+            }
+            if (ctxs + local + mine <= cap) {
+                g_pool.push_back(r);
+                keep = true;
+            }
         }
     }
-    free_resources(r);
+    for (LocalResources &e : evict) free_resources(e);
+    if (!keep) free_resources(r);
 }
 
 // Copies out of a verified window (one thread ~11 GiB/s) and the window preads (one thread
@@ -138,6 +167,30 @@ struct Window {
 constexpr int64_t kPage = 4096;
 
 }  // namespace
+
+namespace hdfs3crc {
+LocalPoolStats local_pool_stats() {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    LocalPoolStats st;
+    for (const LocalResources &e : g_pool) {
+        const LocalPoolStats b = entry_bytes(e);
+        st.pinned += b.pinned;
+        st.device += b.device;
+        st.entries += 1;
+    }
+    return st;
+}
+
+int local_pool_trim() {
+    std::vector<LocalResources> idle;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        idle.swap(g_pool);
+    }
+    for (LocalResources &e : idle) free_resources(e);
+    return int(idle.size());
+}
+}  // namespace hdfs3crc
 
 struct hdfs3_local_reader {
     int data_fd = -1, meta_fd = -1;

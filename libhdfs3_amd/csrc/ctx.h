@@ -83,6 +83,17 @@ int ctx_acquire(int device, hdfs3_crc_ctx **out, bool deep = false);
 void ctx_release(hdfs3_crc_ctx *ctx);
 // the pinned bytes the pool may retain (HDFS3_POOL_PINNED_MAX, default 1 GiB)
 uint64_t pool_pinned_cap_bytes();
+// pinned / device bytes a ctx holds beyond its tables (staging, cached arenas), and the pinned
+// bytes the ctx pool retains now
+void ctx_footprint(hdfs3_crc_ctx *ctx, uint64_t *pinned, uint64_t *device);
+uint64_t ctx_pool_pinned_bytes();
+// The short-circuit readers' own pool (local_reader.cpp: a ctx and its windows per entry) counts
+// against the same cap: its retained bytes, pooled entries, and a trim that frees them all
+struct LocalPoolStats {
+    uint64_t pinned = 0, device = 0, entries = 0;
+};
+LocalPoolStats local_pool_stats();
+int local_pool_trim();
 }  // namespace hdfs3crc
 
 struct hdfs3_crc_ctx {

@@ -619,6 +619,19 @@ void shed(hdfs3_crc_ctx *ctx, size_t keep_arenas, bool slots) {
 
 uint64_t pool_pinned_cap_bytes() { return pool_pinned_cap(); }
 
+void ctx_footprint(hdfs3_crc_ctx *ctx, uint64_t *pinned, uint64_t *device) {
+    const Footprint f = footprint(ctx);
+    if (pinned) *pinned = f.pinned;
+    if (device) *device = f.device;
+}
+
+uint64_t ctx_pool_pinned_bytes() {
+    std::lock_guard<std::mutex> lk(g_ctx_pool_mu);
+    uint64_t n = 0;
+    for (hdfs3_crc_ctx *c : g_ctx_pool) n += footprint(c).pinned;
+    return n;
+}
+
 int ctx_acquire(int device, hdfs3_crc_ctx **out, bool deep) {
     if (!out) return fail(-EINVAL, "null out");
     {
@@ -655,6 +668,9 @@ void ctx_release(hdfs3_crc_ctx *ctx) {
         ok = hipStreamSynchronize(ctx->stream) == hipSuccess;
     }
     for (Slot &s : ctx->slot) s.pending_out = nullptr;
+    // the short-circuit readers' pool counts against the same cap (taken before g_ctx_pool_mu: the
+    // local pool locks its own mutex first and then this one)
+    const uint64_t local = ok ? local_pool_stats().pinned : 0;
     if (ok) {
         std::lock_guard<std::mutex> lk(g_ctx_pool_mu);
         if (g_ctx_pool.size() < kCtxPoolMax) {
@@ -672,7 +688,7 @@ void ctx_release(hdfs3_crc_ctx *ctx) {
             // does not fit. Shedding this ctx first made every read-ahead block re-pin its ring once
             // older pooled rings filled the cap: 1 GiB with read-ahead 2 / 7 at 6.6 / 2.3 GiB/s
             // against 11.8 / 10.6 uncapped (profiles/r03/reentry/r3e2eab_*).
-            const uint64_t cap = pool_pinned_cap();
+            const uint64_t cap = pool_pinned_cap() > local ? pool_pinned_cap() - local : 0;
             const uint64_t mine = footprint(ctx).pinned;
             uint64_t others = 0;
             for (hdfs3_crc_ctx *c : g_ctx_pool) others += footprint(c).pinned;
@@ -703,13 +719,17 @@ void hdfs3_crc_ctx_release(hdfs3_crc_ctx *ctx) { hdfs3crc::ctx_release(ctx); }
 int hdfs3_crc_pool_stats_get(hdfs3_crc_pool_stats *out) {
     if (!out) return fail(-EINVAL, "null out");
     hdfs3_crc_pool_stats st{};
+    // the short-circuit readers' pooled contexts and windows are part of the same budget
+    const hdfs3crc::LocalPoolStats lp = hdfs3crc::local_pool_stats();
     std::lock_guard<std::mutex> lk(hdfs3crc::g_ctx_pool_mu);
     for (hdfs3_crc_ctx *c : hdfs3crc::g_ctx_pool) {
         const hdfs3crc::Footprint f = hdfs3crc::footprint(c);
         st.pinned_bytes += f.pinned;
         st.device_bytes += f.device;
     }
-    st.pooled_contexts = hdfs3crc::g_ctx_pool.size();
+    st.pinned_bytes += lp.pinned;
+    st.device_bytes += lp.device;
+    st.pooled_contexts = hdfs3crc::g_ctx_pool.size() + lp.entries;
     st.pinned_cap_bytes = hdfs3crc::pool_pinned_cap();
     *out = st;
     return 0;
@@ -722,7 +742,7 @@ int hdfs3_crc_pool_trim(void) {
         idle.swap(hdfs3crc::g_ctx_pool);
     }
     for (hdfs3_crc_ctx *c : idle) hdfs3_crc_ctx_destroy(c);
-    return int(idle.size());
+    return int(idle.size()) + hdfs3crc::local_pool_trim();
 }
 
 int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream) {

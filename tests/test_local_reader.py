@@ -254,3 +254,53 @@ def test_random_offsets_and_read_sizes(tmp_path):
                     assert got > 0
                     pos += got
                 assert np.array_equal(out, data[start:]), (case, verify, start)
+
+
+_POOL_CHILD = r"""
+import ctypes, sys
+sys.path.insert(0, sys.argv[1])
+from libhdfs3_amd import _native
+from libhdfs3_amd.engine import LocalBlockReader
+lib = _native.lib()
+st = _native.PoolStats()
+files = sys.argv[2:]
+readers = [LocalBlockReader(files[i], files[i + 1]) for i in range(0, len(files), 2)]
+for r in readers:
+    r.read_all(1 << 30)
+for r in readers:
+    r.close()
+assert lib.hdfs3_crc_pool_stats_get(ctypes.byref(st)) == 0
+print(st.pinned_bytes, st.pinned_cap_bytes, st.pooled_contexts)
+n = lib.hdfs3_crc_pool_trim()
+assert n == st.pooled_contexts, (n, st.pooled_contexts)
+assert lib.hdfs3_crc_pool_stats_get(ctypes.byref(st)) == 0
+print(st.pinned_bytes, st.pinned_cap_bytes, st.pooled_contexts)
+"""
+
+
+@pytest.mark.parametrize("cap_mib", [24, 1024])
+def test_pooled_readers_count_against_the_pinned_cap(tmp_path, cap_mib):
+    """Closed short-circuit readers keep their ctx and windows in the library's pool; those bytes
+    are reported by hdfs3_crc_pool_stats_get, kept under HDFS3_POOL_PINNED_MAX together with the
+    contexts' pool (24 MiB: two readers' 3 x 4 MiB windows do not fit, so one reader's stay), and
+    freed by hdfs3_crc_pool_trim. The cap is read once per process: a child process per cap."""
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = []
+    for i in range(6):
+        args += write_block(tmp_path, f"blk{i}", splitmix_bytes((9 << 20) + 300 * i, 900 + i))
+    env = dict(os.environ, HDFS3_POOL_PINNED_MAX=f"{cap_mib}M")
+    out = subprocess.run([sys.executable, "-c", _POOL_CHILD, repo] + args, env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    (pinned, cap, pooled), (p2, _, n2) = [tuple(int(x) for x in ln.split()) for ln in out.stdout.split("\n")[:2]]
+    assert cap == cap_mib << 20
+    assert pinned <= cap, (pinned, cap)
+    # a reader's windows: 3 x (4 MiB + its CRC words); one reader's worth fits 24 MiB, six fit 1 GiB
+    windows = 3 * ((4 << 20) + 4 * ((4 << 20) // 512))
+    assert pinned >= (windows if cap_mib == 24 else 6 * windows), (pinned, windows)
+    assert pooled >= 1
+    assert p2 == 0 and n2 == 0
