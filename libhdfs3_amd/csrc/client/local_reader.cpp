@@ -187,7 +187,11 @@ int local_pool_trim() {
         std::lock_guard<std::mutex> lk(g_pool_mu);
         idle.swap(g_pool);
     }
-    for (LocalResources &e : idle) free_resources(e);
+    // destroyed outright, not released: a trim leaves no context behind in either pool
+    for (LocalResources &e : idle) {
+        for (PacketArena &a : e.a) a.release();
+        hdfs3_crc_ctx_destroy(e.ctx);
+    }
     return int(idle.size());
 }
 }  // namespace hdfs3crc

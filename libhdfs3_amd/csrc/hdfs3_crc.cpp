@@ -736,13 +736,14 @@ int hdfs3_crc_pool_stats_get(hdfs3_crc_pool_stats *out) {
 }
 
 int hdfs3_crc_pool_trim(void) {
+    const int local = hdfs3crc::local_pool_trim();
     std::vector<hdfs3_crc_ctx *> idle;
     {
         std::lock_guard<std::mutex> lk(hdfs3crc::g_ctx_pool_mu);
         idle.swap(hdfs3crc::g_ctx_pool);
     }
     for (hdfs3_crc_ctx *c : idle) hdfs3_crc_ctx_destroy(c);
-    return int(idle.size()) + hdfs3crc::local_pool_trim();
+    return int(idle.size()) + local;
 }
 
 int hdfs3_crc_ctx_set_stream(hdfs3_crc_ctx *ctx, void *hip_stream) {
