@@ -707,9 +707,6 @@ __device__ unsigned long long *g_lab_clk = nullptr;
 __device__ unsigned int g_lab_clk_cap = 0;
 __device__ unsigned int g_lab_clk_n = 0;
 __device__ unsigned long long *g_lab_wave = nullptr;
-// claim counters of the XCD-wide round pools (kLabXDyn): 8 per launch, a ring of kLabClaimRing launches
-constexpr uint32_t kLabClaimRing = 256;
-__device__ uint32_t g_lab_claim[8 * kLabClaimRing];
 __device__ unsigned int g_lab_wave_cap = 0;
 struct LabClock {
     unsigned long long t0 = 0, r0 = 0;

@@ -59,49 +59,12 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabStageWin>(a, tab, fold, grid_cap, s);
         case 128:  // compute: staged words through plain global stores (production before round 4)
             return launch_wave3<BPC, V, false, true, kLabStorePlain>(a, tab, fold, grid_cap, s);
-        case 138:  // verify at bpc <= 2048: rounds claimed from the workgroup's pool (kLabDyn, DynWalk)
-            if constexpr (BPC <= 2048) {
-                if (V) return launch_wave3<BPC, true, false, true, kLabDyn>(a, tab, fold, grid_cap, s);
-            }
-            return hipErrorNotSupported;
-        case 140:  // verify at bpc <= 2048: every wave's last 2 rounds claimed from XCD-wide pools (kLabXDyn)
-            if constexpr (BPC <= 2048) {
-                if (V) return launch_wave3<BPC, true, false, true, kLabXDyn>(a, tab, fold, grid_cap, s);
-            }
-            return hipErrorNotSupported;
-        case 141:  // the last 4 rounds
-            if constexpr (BPC <= 2048) {
-                if (V) return launch_wave3<BPC, true, false, true, kLabXDyn | kLabXDyn4>(a, tab, fold, grid_cap, s);
-            }
-            return hipErrorNotSupported;
-        case 142:  // 141 with clock stamps
-            if constexpr (BPC <= 2048) {
-                if (V) return launch_wave3<BPC, true, false, true, kLabXDyn | kLabXDyn4 | kLabClock>(a, tab, fold, grid_cap, s);
-            }
-            return hipErrorNotSupported;
-        case 143:  // verify: a workgroup's waves one grid apart (kLabSpread)
-            if (V) return launch_wave3<BPC, true, false, true, kLabSpread>(a, tab, fold, grid_cap, s);
-            return hipErrorNotSupported;
-        case 144:  // 143 with clock stamps
-            if (V) return launch_wave3<BPC, true, false, true, kLabSpread | kLabClock>(a, tab, fold, grid_cap, s);
-            return hipErrorNotSupported;
-        case 145:  // the solo last step on barriered launches too (kLabSoloBar)
-            return launch_wave3<BPC, V, false, true, kLabSoloBar>(a, tab, fold, grid_cap, s);
         case 146:  // production with every wave's fill-done and first-data times (wave_spread.py --variant 146 --mid)
             return launch_wave3<BPC, V, false, true, kLabClock | kLabMid>(a, tab, fold, grid_cap, s);
         case 147:  // diagnostic: no table loads (wrong results), with fill-done / first-data stamps
             return launch_wave3<BPC, V, false, true, kLabNoTabLoad | kLabClock | kLabMid>(a, tab, fold, grid_cap, s);
         case 148:  // diagnostic: no table loads (wrong results)
             return launch_wave3<BPC, V, false, true, kLabNoTabLoad>(a, tab, fold, grid_cap, s);
-        case 151:  // rounds 2, 3 prefetched in the prologue with rounds 0, 1 (kLabHeadPf)
-            return launch_wave3<BPC, V, false, true, kLabHeadPf>(a, tab, fold, grid_cap, s);
-        case 152:  // 151 with fill-done / first-data stamps
-            return launch_wave3<BPC, V, false, true, kLabHeadPf | kLabClock | kLabMid>(a, tab, fold, grid_cap, s);
-        case 139:  // 138 with clock stamps (tools/wave_spread.py --variant 139)
-            if constexpr (BPC <= 2048) {
-                if (V) return launch_wave3<BPC, true, false, true, kLabDyn | kLabClock>(a, tab, fold, grid_cap, s);
-            }
-            return hipErrorNotSupported;
         case 137:  // verify: 1024-thread workgroups at every launch size (production before round 4)
             return launch_wave3<BPC, V, false, true, kLabWg1024>(a, tab, fold, grid_cap, s);
         case 132:  // 256-thread workgroups (4 waves each): small launches spread over 4x the CUs

@@ -43,12 +43,6 @@ constexpr int kLabStageWin = 2048;  // compute at bpc 512: staged words past kSt
 constexpr int kLabClock = 4096;     // clock stamps of workgroup 0 (LabClock, crc32c_device.h; lab builds only)
 constexpr int kLabStorePlain = 8192;  // compute, staged words: plain global stores (production before round 4)
 constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every launch size (production before round 4)
-constexpr int kLabDyn = 32768;       // verify at bpc <= 2048: rounds claimed at run time from the workgroup's pool (DynWalk)
-constexpr int kLabXDyn = 65536;      // verify at bpc <= 2048: the last rounds claimed from an XCD-wide pool (XDynWalk)
-constexpr int kLabXDyn4 = 131072;    // with kLabXDyn: the last 4 rounds of every wave instead of 2
-constexpr int kLabSpread = 262144;   // verify: a workgroup's waves take rounds one grid apart (not 16 adjacent ones)
-constexpr int kLabSoloBar = 524288;  // the solo last step on barriered launches too (production: overlapped only)
-constexpr int kLabHeadPf = 4194304;   // the first step's prefetch (rounds 2, 3) issued in the prologue, before the fill
 constexpr int kLabNoTabLoad = 2097152;  // diagnostic: the table images are not loaded (made up from t: wrong results)
 constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = fill done | first data << 21 | kernel
                                      // arguments landed << 42, each - start, 21 bits of 10 ns
@@ -90,9 +84,7 @@ struct WView {
 // words' addresses at flush time); a walk without it holds each word's address instead.
 template <int CPU>
 struct BlockWalk {
-    static constexpr bool kGlobal = false;
     static constexpr bool kLaneView = true;
-    static constexpr bool kDynamic = false;
     static constexpr bool kContiguous = true;  // unit u's words at words + 4 * CPU * u
     const uint8_t *data;
     uint8_t *words;
@@ -108,110 +100,12 @@ struct BlockWalk {
     }
 };
 
-// Rounds of one contiguous block claimed at run time (kLabDyn, verify): the workgroup's rounds under
-// BlockWalk's split -- round k of its wave s is pool entry c = k * WPB + s, unit wgbase + s + k * stride --
-// form a pool [0, total) that its waves take in pairs (c, c + 1: two adjacent units) from a counter in
-// LDS. Every wave's first two pairs are fixed (c = 2s, 2s + 1 and 2 WPB + 2s, + 1); a step claims the
-// pair it will prefetch two steps later (begin_step, one LDS atomic from lane 0, its result read at the
-// step's end). The waves the SIMD arbiter starves take fewer rounds instead of ending the workgroup
-// late: a barriered 128 MiB launch's waves lived 12.4 / 16.3 / 20.3 us (p10 / p50 / p90) with 8 rounds
-// each (tools/wave_spread.py). K stays ~0 until the wave's first claim past the pool.
-template <int CPU>
-struct DynWalk {
-    static constexpr bool kLaneView = false;
-    static constexpr bool kContiguous = true;
-    static constexpr bool kDynamic = true;
-    static constexpr bool kGlobal = false;
-    const uint8_t *data;
-    uint8_t *words;
-    uint64_t key0, wgbase, stride;
-    uint32_t *ctr;  // LDS claim counter
-    uint32_t slot, wpb, total;
-    uint32_t K;
-    const uint8_t *dummy;
-    uint32_t pend = 0, cbase = 0;
-    __device__ __forceinline__ void begin_step(uint32_t) {
-        if ((threadIdx.x & 63) == 0) pend = __hip_atomic_fetch_add(ctr, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    __device__ __forceinline__ WView view(uint32_t k) {
-        uint32_t c;
-        if (k < 4) {
-            c = (k >> 1) * 2 * wpb + 2 * slot + (k & 1);
-        } else if ((k & 1) == 0) {
-            cbase = __builtin_amdgcn_readfirstlane(pend);
-            c = cbase;
-        } else {
-            c = cbase + 1;
-        }
-        const bool in = c < total;
-        if (!in && K == ~0u) K = k;  // claims only grow: every later round is past the pool too
-        const uint64_t u = wgbase + c % wpb + uint64_t(c / wpb) * stride;
-        return WView{in ? data + u * kRoundBytes : dummy, in ? words + 4 * CPU * u : const_cast<uint8_t *>(dummy),
-                     key0 + CPU * u};
-    }
-};
-
-// The first S rounds of every wave as BlockWalk assigns them, the rest of the launch claimed at run
-// time (kLabXDyn, verify): a barriered 128 MiB launch's workgroups -- one per CU -- took 15-21 us for
-// equal work (tools/wave_spread.py: the pool inside a workgroup, DynWalk, evens out its waves but not
-// the CUs). Units past S * W (W = waves of the launch) form 8 pools, pool x = the runs of WPB units
-// that workgroups b = x mod 8 own under the static split (a workgroup of pool x takes from pool x
-// only; with round-robin dispatch that is one XCD). Claims are pairs of adjacent units through an
-// agent-scope atomic on the launch's counter (ctr: 8 counters per launch, zeroed 128 launches ahead
-// by the launch itself), issued two steps before the pair is needed.
-template <int CPU>
-struct XDynWalk {
-    static constexpr bool kLaneView = false;
-    static constexpr bool kContiguous = true;
-    static constexpr bool kDynamic = true;
-    static constexpr bool kGlobal = true;
-    const uint8_t *data;
-    uint8_t *words;
-    uint64_t key0, first, stride, units;
-    uint32_t *ctr;
-    uint32_t S, x, wpb, ngrp;  // ngrp: workgroups per pool per row (grid / 8)
-    uint32_t K;
-    const uint8_t *dummy;
-    bool dyn;  // false: the launch is too short for the pools (S = the wave's own round count)
-    uint32_t pend = 0, cbase = 0;
-    __device__ __forceinline__ void begin_step(uint32_t k) {
-        if (dyn && k + 4 >= S && (threadIdx.x & 63) == 0)
-            pend = __hip_atomic_fetch_add(ctr, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __device__ __forceinline__ WView view(uint32_t k) {
-        uint64_t u;
-        bool in = true;
-        if (k < S) {
-            u = first + uint64_t(k) * stride;
-        } else if (!dyn) {
-            u = 0;
-            in = false;
-        } else {
-            uint32_t c;
-            if (((k - S) & 1) == 0) {
-                cbase = __builtin_amdgcn_readfirstlane(pend);
-                c = cbase;
-            } else {
-                c = cbase + 1;
-            }
-            const uint32_t per_row = ngrp * wpb, row = c / per_row, j = c % per_row;
-            u = uint64_t(S + row) * stride + uint64_t(j / wpb) * (8 * wpb) + x * wpb + j % wpb;
-            in = u < units;
-            if (!in && K == ~0u) K = k;
-        }
-        return WView{in ? data + u * kRoundBytes : dummy, in ? words + 4 * CPU * u : const_cast<uint8_t *>(dummy),
-                     key0 + CPU * u};
-    }
-};
-
 // A packet stream at one pitch: every packet but the last holds 1 << L whole rounds; its words sit
 // at words + packet * wpitch (the wire layout: in the packet; a [blocks, words] tensor: their own
 // pitch). Keys are (packet << 32) | chunk.
 template <int CPU>
 struct PitchWalk {
-    static constexpr bool kGlobal = false;
     static constexpr bool kLaneView = true;
-    static constexpr bool kDynamic = false;
     static constexpr bool kContiguous = false;
     const uint8_t *data;
     uint8_t *words;
@@ -235,9 +129,7 @@ struct PitchWalk {
 // increasing round order (the core resolves the next step's views at the end of each step).
 template <int CPU, bool UNI>
 struct SegWalk {
-    static constexpr bool kGlobal = false;
     static constexpr bool kLaneView = false;
-    static constexpr bool kDynamic = false;
     static constexpr bool kContiguous = false;
     // The launch record and the descriptors through the CONSTANT address space: their fields are
     // wave-uniform, so they load with s_load (lgkmcnt). Through a generic pointer they compiled to
@@ -322,8 +214,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = lane % G;
     const uint32_t lane_off = 64 * (lane & 15) + 16 * (lane >> 4);
-    const uint32_t K = walk.K;  // Walk::kDynamic: walk.K, read where it is needed (it is set while running)
-    static_assert(!Walk::kDynamic || (VERIFY && G <= 32), "claimed rounds: verify with the half fold image");
+    const uint32_t K = walk.K;
 
     // lean fill: each of the image's 1024 slice-table words replicated 32x (TPB threads take 1024 / TPB
     // words each); for G <= 32 the half fold image
@@ -354,14 +245,6 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     Round a0, a1, b0, b1;
     load_round_buf<true>(a0, cv0.p, lane_off);
     load_round_buf<true>(a1, cv1.p, lane_off);
-    // kLabHeadPf: rounds 2, 3 too, so 16 KiB per wave (64 MiB per 128 MiB launch) are in flight while
-    // the tables fill, not 8; step 0 then skips its prefetch
-    constexpr bool kHeadPf = (LAB & kLabHeadPf) != 0 && !Walk::kDynamic;
-    if constexpr (kHeadPf) {
-        const WView h2 = walk.view(2), h3 = walk.view(3);
-        load_round_buf<true>(b0, h2.p, lane_off);
-        load_round_buf<true>(b1, h3.p, lane_off);
-    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int f = 0; f < kFillIters; ++f) {
@@ -381,9 +264,6 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             dst[0] = n0[f];
             dst[1] = n1[f];
         }
-    }
-    if constexpr (Walk::kDynamic && !Walk::kGlobal) {
-        if (threadIdx.x == 0) *walk.ctr = 4 * walk.wpb;  // the fixed first two pairs of every wave
     }
     lds_barrier();
     if constexpr ((LAB & kLabMid) != 0) lab_mid[0] = __builtin_amdgcn_s_memrealtime();
@@ -540,7 +420,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             }
             return;
         }
-        if (k >= (Walk::kDynamic ? walk.K : K) || j != 0) return;
+        if (k >= K || j != 0) return;
         const uint32_t c = y;
         if constexpr (VERIFY) {
             // the diagnostics compute wrong CRCs: compare inverted so they do not flag every chunk
@@ -594,8 +474,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // are in flight per wave (128 KiB per CU), not 16: more requests in flight lower the DRAM
     // efficiency. kLabEarly (lab A/B): issued at the start of the step.
     // priority by rounds left (kPrioMinRounds); wave-uniform, so the branches are SALU
-    const bool use_prio =
-        !Walk::kDynamic && ((LAB & kLabPrio) != 0 || ((LAB & kLabNoPrio) == 0 && K >= kPrioMinRounds));
+    const bool use_prio = (LAB & kLabPrio) != 0 || ((LAB & kLabNoPrio) == 0 && K >= kPrioMinRounds);
     auto prio = [&](uint32_t k) {
         if (use_prio) {
             const uint32_t left = K > k ? K - k : 0;
@@ -607,7 +486,6 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     };
     auto step = [&](Round &c0, Round &c1, Round &p0, Round &p1, uint32_t k) {
         prio(k);
-        if constexpr (Walk::kDynamic) walk.begin_step(k);
         const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
         if constexpr (!LATE) {
             load_round_buf<true>(p0, pv0.p, lane_off);
@@ -621,10 +499,8 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         }
         if constexpr (LATE) {
             __builtin_amdgcn_sched_barrier(0);
-            if (!kHeadPf || k != 0) {
-                load_round_buf<true>(p0, pv0.p, lane_off);
-                load_round_buf<true>(p1, pv1.p, lane_off);
-            }
+            load_round_buf<true>(p0, pv0.p, lane_off);
+            load_round_buf<true>(p1, pv1.p, lane_off);
             __builtin_amdgcn_sched_barrier(0);
         }
         uint32_t x0, x1;
@@ -643,15 +519,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // in it is the same code: an exit from the middle of the body, or a special last step that values
     // reach from both buffer sets, makes the register allocator copy the rounds (32 v_mov per step).
     const uint32_t nr = (K + 1) & ~1u;  // rounds rounded up to whole steps
-    if constexpr (Walk::kDynamic) {
-        // pair k + 2's views were resolved two steps back: walk.K is final for it
-        for (uint32_t k = 0;; k += 4) {
-            step(a0, a1, b0, b1, k);
-            if (k + 2 >= walk.K) break;
-            step(b0, b1, a0, a1, k + 2);
-            if (k + 4 >= walk.K) break;
-        }
-    } else if constexpr (SOLO) {
+    if constexpr (SOLO) {
         // The last step outside the loop, its two rounds as single chains one after the other: the
         // first chain overlaps the second round's arrival, and only one round's lookups remain once
         // the wave's last data has landed. Its buffers are STATIC: with F = nr / 2 - 1 full steps,
@@ -766,38 +634,8 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
         if (a.last_len % kRoundBytes)  // wave-uniform: a stream of whole rounds has no slow region
             slow_region<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
                                      a.check_short_tail, a.result);
-    } else if constexpr ((LAB & kLabXDyn) != 0 && VERIFY && BPC <= 2048) {
-#if HDFS3_LAB
-        // the launch's 8 counters; the launch 128 ahead's zeroed here (no launch runs 128 behind)
-        uint32_t *ctrs = g_lab_claim + 8 * (a.lab_seq % kLabClaimRing);
-        if (blockIdx.x == 0 && threadIdx.x < 8)
-            g_lab_claim[8 * ((a.lab_seq + kLabClaimRing / 2) % kLabClaimRing) + threadIdx.x] = 0u;
-        constexpr uint32_t D = (LAB & kLabXDyn4) ? 4u : 2u;
-        const bool dyn = a.kq >= 4 + D && gridDim.x % 8 == 0;
-        XDynWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, a.len / kRoundBytes, ctrs + blockIdx.x % 8,
-                         dyn ? a.kq - D : K, blockIdx.x % 8, uint32_t(kWpb), gridDim.x / 8, dyn ? ~0u : K, dummy, dyn};
-        wave_rounds<BPC, VERIFY, false, false, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
-        if (a.len % kRoundBytes)
-            slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
-#endif
-    } else if constexpr ((LAB & kLabDyn) != 0 && VERIFY && BPC <= 2048) {
-        const uint64_t wgbase = uint64_t(blockIdx.x) * kWpb;
-        const uint32_t extra = a.kr > wgbase ? uint32_t(a.kr - wgbase < kWpb ? a.kr - wgbase : kWpb) : 0u;
-        DynWalk<kCpu> w{a.data, words, a.chunk_base, wgbase, nwaves, lds + kLdsBytesWave / 4 - 1,
-                        uint32_t(wave - wgbase), uint32_t(kWpb), kWpb * a.kq + extra, ~0u, dummy};
-        wave_rounds<BPC, VERIFY, false, false, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
-        if (a.len % kRoundBytes)
-            slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     } else {
-        // kLabSpread: wave (b, s) starts at unit s * grid + b, so a step's 16 rounds of one workgroup lie
-        // 1 MiB apart (128 MiB launch) instead of forming one 64 KiB run
-        uint64_t first = wave;
-        uint32_t Kw = K;
-        if constexpr ((LAB & kLabSpread) != 0 && VERIFY) {
-            first = rfl64(uint64_t(threadIdx.x >> 6) * gridDim.x + blockIdx.x);
-            Kw = a.kq + (first < a.kr ? 1u : 0u);
-        }
-        BlockWalk<kCpu> w{a.data, words, a.chunk_base, first, nwaves, Kw, dummy, a.kq, a.kr};
+        BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, K, dummy, a.kq, a.kr};
         wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result, lab_mid);
         if (a.len % kRoundBytes)  // wave-uniform: a block of whole rounds has no slow region
             slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
@@ -881,7 +719,7 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     const uint64_t nwaves = uint64_t(grid) * (TPB / 64);
     if (units / nwaves >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
     ChunkLaunch b = a;
-    if constexpr ((LAB & (kLabClock | kLabXDyn)) != 0) b.lab_seq = g_lab_seq++;
+    if constexpr ((LAB & kLabClock) != 0) b.lab_seq = g_lab_seq++;
     b.kq = uint32_t(units / nwaves);
     b.kr = uint32_t(units % nwaves);
     // Verify launches below 64 MiB take smaller workgroups (round 4): a 1024-thread workgroup fills a
@@ -915,13 +753,6 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
         hipExtLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB, TPB>), dim3(grid),
                               dim3(TPB), 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, b, tab, nib);
     } else {
-        if constexpr (SOLO && (LAB & kLabSoloBar) != 0) {
-            if (units * kRoundBytes <= kSoloTailMaxBytes) {
-                hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, true, LAB, TPB>), dim3(grid), dim3(TPB), 0, s,
-                                   b, tab, nib);
-                return hipGetLastError();
-            }
-        }
         hipLaunchKernelGGL((crc32c_wave_kernel<BPC, V, PITCH, false, LAB, TPB>), dim3(grid), dim3(TPB),
                            0, s, b, tab, nib);
     }
