@@ -304,3 +304,59 @@ def test_pooled_readers_count_against_the_pinned_cap(tmp_path, cap_mib):
     assert pinned >= (windows if cap_mib == 24 else 6 * windows), (pinned, windows)
     assert pooled >= 1
     assert p2 == 0 and n2 == 0
+
+
+_KNOB_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from libhdfs3_amd.engine import LocalBlockReader
+d, m, n, bad = sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+ref = np.fromfile(d, dtype=np.uint8)
+with LocalBlockReader(d, m) as r:
+    out = np.zeros(n, dtype=np.uint8)
+    pos = 0
+    try:
+        while pos < n:
+            got = r.read_into(out, pos, min((2 << 20) + 3, n - pos))
+            if got <= 0:
+                break
+            pos += got
+    except Exception as e:
+        print("error", pos, type(e).__name__)
+    assert np.array_equal(out[:pos], ref[:pos])
+    print("read", pos)
+"""
+
+
+@pytest.mark.parametrize("knobs", [{"HDFS3_COPY_NT": "1"}, {"HDFS3_LOCAL_BLOCKING_SYNC": "1"},
+                                   {"HDFS3_COPY_NT": "1", "HDFS3_LOCAL_BLOCKING_SYNC": "1", "HDFS3_COPY_HELPERS": "8"}])
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_host_side_knobs_keep_the_bytes_and_the_checks(tmp_path, knobs, corrupt):
+    """The short-circuit reader's host-side knobs (streaming-store copies, blocking window events, the
+    copy pool's helper count; read once per process, so a child per setting): every delivered byte
+    equals the file's, reads of 2 MiB + 3 bytes split unevenly over the pool, and a corrupt chunk
+    still withholds its whole 1 MiB local buffer (LocalBlockReader.cpp:138-163)."""
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = (13 << 20) + 777
+    data = splitmix_bytes(n, 4242)
+    crc = oracle_compute(data, 512)
+    bad = (9 << 20) + 12345
+    if corrupt:
+        data = data.copy()
+        data[bad] ^= 0x40
+    d, m = write_block(tmp_path, "knob", data, crc=crc)
+    env = dict(os.environ, **knobs)
+    out = subprocess.run([sys.executable, "-c", _KNOB_CHILD, repo, d, m, str(n), str(bad)], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = out.stdout.split()
+    got = int(lines[lines.index("read") + 1])
+    if corrupt:
+        assert "error" in lines and got == (bad >> 20) << 20, out.stdout  # up to the bad chunk's 1 MiB buffer
+    else:
+        assert "error" not in lines and got == n, out.stdout
