@@ -29,6 +29,11 @@ def main():
     ap.add_argument("--kinds", default="crc,read")
     ap.add_argument("--read-grid", type=int, default=-512)
     ap.add_argument("--variant", type=int, default=125)
+    ap.add_argument("--form", default="", choices=["", "bench"],
+                    help="bench: the driver's region (2000 barriered, W overlapped, settle, K timed: the first "
+                         "barriered, the rest overlapped) against K launches after 1000 overlapped ones; "
+                         "per-launch rows instead of medians (with --mid: each launch's head)")
+    ap.add_argument("--w", type=int, default=5)
     ap.add_argument("--mid", action="store_true", help="variant 146: word 2 holds the fill-done and first-data "
                     "times of the wave (kLabMid) instead of its shader clocks")
     args = ap.parse_args()
@@ -86,6 +91,71 @@ def main():
         n = lib.hdfs3x_wave_stamps(None, 0)
         st = stamps.view(-1, 4).cpu().numpy()
         return a.elapsed_time(b) * 1e3 / k, n, st
+
+    if args.form == "bench":
+        lib.hdfs3x_set_variant(args.variant)
+        m21 = np.uint64(0x1FFFFF)
+
+        def launches(pre, stamped_pre):
+            # stamped_pre: the buffer goes in before pre() (no sync between pre() and the region; the
+            # ring keeps the last 256 launches, the region's are the last K)
+            if stamped_pre:
+                torch.cuda.synchronize()
+                stamps.zero_()
+                torch.cuda.synchronize()
+                lib.hdfs3x_wave_stamps(stamps.data_ptr(), cap)
+                pre()
+            else:
+                pre()
+                stamps.zero_()
+                torch.cuda.synchronize()
+                lib.hdfs3x_wave_stamps(stamps.data_ptr(), cap)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for i in range(args.k):
+                crc_launch(i, True)
+            b.record(stream)
+            torch.cuda.synchronize()
+            n = lib.hdfs3x_wave_stamps(None, 0)
+            st = stamps.view(-1, 4).cpu().numpy()
+            st = st[st[:, 1] != 0]
+            seq = (st[:, 3].astype(np.uint64) >> np.uint64(52)).astype(np.int64)
+            region = [(n - args.k + li) & 0xFFF for li in range(args.k)]
+            st = st[np.isin(seq, region)]
+            seq = (st[:, 3].astype(np.uint64) >> np.uint64(52)).astype(np.int64)
+            rows = []
+            t_first = st[:, 0].min() / 100.0
+            for li, sq in enumerate(region):
+                x = st[seq == sq]
+                r0, r1 = x[:, 0] / 100.0, x[:, 1] / 100.0
+                row = {"launch": li + 1, "start_us": round(r0.min() - t_first, 2), "span_us": round(r1.max() - r0.min(), 2),
+                       "wave_end_p10_p90_us": [round(float(np.percentile(r1 - r0.min(), q)), 2) for q in (10, 90)]}
+                if args.mid:
+                    w2 = x[:, 2].astype(np.uint64)
+                    row["fill_done_p50_us"] = round(float(np.median((w2 & m21).astype(np.float64))) / 100.0, 2)
+                    row["first_data_p50_us"] = round(float(np.median(((w2 >> np.uint64(21)) & m21).astype(np.float64))) / 100.0, 2)
+                rows.append(row)
+            return a.elapsed_time(b) * 1e3 / args.k, rows
+
+        def pre_bench():
+            for i in range(2000):
+                crc_launch(i, False)
+            for i in range(args.w):
+                crc_launch(i, True)
+            settle()
+
+        def pre_steady():
+            for i in range(1000):
+                crc_launch(i, True)
+
+        for name, pre, sp in (("bench", pre_bench, False), ("steady_after_1000", pre_steady, True)):
+            us, rows = launches(pre, sp)
+            print(json.dumps({"form": name, "k": args.k, "us_per_launch_events": round(us, 2), "launches": rows}),
+                  flush=True)
+        lib.hdfs3x_set_variant(0)
+        lib.hdfs3x_wave_stamps(None, 0)
+        assert not bool((res != 0).any().item()), "clean blocks reported bad"
+        return
 
     out = []
     for kind in args.kinds.split(","):
