@@ -660,7 +660,9 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
         const uint32_t m = blockIdx.x & 3;
         const bool ok = a.kr == 0 && gridDim.x % 4 == 0 && a.kq >= 2;
         const uint32_t Ks = !ok ? K : m == 0 ? a.kq + 1 : m == 2 ? a.kq - 1 : a.kq;
-        SkewWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, wave + 2 * kWpb, Ks, a.kq, dummy};
+        // without the skew, round kq (waves below kr) is the wave's own: pfirst + (kq - 1) W = wave + kq W
+        SkewWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, ok ? wave + 2 * kWpb : wave + nwaves, Ks, a.kq,
+                         dummy};
         wave_rounds<BPC, VERIFY, SOLO, false, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
         if (a.len % kRoundBytes)
             slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
