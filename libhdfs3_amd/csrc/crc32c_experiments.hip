@@ -59,9 +59,6 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabStageWin>(a, tab, fold, grid_cap, s);
         case 128:  // compute: staged words through plain global stores (production before round 4)
             return launch_wave3<BPC, V, false, true, kLabStorePlain>(a, tab, fold, grid_cap, s);
-        case 153:  // verify: uneven workgroups on overlapped launches (kLabSkew), production otherwise
-            if (V && a.overlap_previous) return launch_wave3<BPC, true, false, true, kLabSkew>(a, tab, fold, grid_cap, s);
-            return launch_wave3<BPC, V, false, true>(a, tab, fold, grid_cap, s);
         case 146:  // production with every wave's fill-done and first-data times (wave_spread.py --variant 146 --mid)
             return launch_wave3<BPC, V, false, true, kLabClock | kLabMid>(a, tab, fold, grid_cap, s);
         case 147:  // diagnostic: no table loads (wrong results), with fill-done / first-data stamps

@@ -43,7 +43,6 @@ constexpr int kLabStageWin = 2048;  // compute at bpc 512: staged words past kSt
 constexpr int kLabClock = 4096;     // clock stamps of workgroup 0 (LabClock, crc32c_device.h; lab builds only)
 constexpr int kLabStorePlain = 8192;  // compute, staged words: plain global stores (production before round 4)
 constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every launch size (production before round 4)
-constexpr int kLabSkew = 8388608;     // verify: workgroups b = 0 / 2 mod 4 take kq + 1 / kq - 1 rounds (staggered ends)
 constexpr int kLabNoTabLoad = 2097152;  // diagnostic: the table images are not loaded (made up from t: wrong results)
 constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = fill done | first data << 21 | kernel
                                      // arguments landed << 42, each - start, 21 bits of 10 ns
@@ -95,27 +94,6 @@ struct BlockWalk {
     uint32_t kq = 0, kr = 0;  // the launch's round split (ChunkLaunch::kq/kr): any wave's K
     __device__ __forceinline__ WView view(uint32_t k) const {
         const uint64_t u = first + uint64_t(k) * stride;
-        const bool in = k < K;
-        return WView{in ? data + u * kRoundBytes : dummy, in ? words + 4 * CPU * u : const_cast<uint8_t *>(dummy),
-                     key0 + CPU * u};
-    }
-};
-
-// kLabSkew (lab): BlockWalk's split with uneven workgroups, so the CUs of one launch end at different
-// times and the next overlapped launch's workgroups start staggered (the driver's region: launches 2-4
-// start almost together behind a lockstep first launch, §5.0.2). Workgroup b = 0 mod 4 also takes the
-// last row's units of workgroup b + 2, which stops one row early; launches with kr = 0 only.
-template <int CPU>
-struct SkewWalk {
-    static constexpr bool kLaneView = true;
-    static constexpr bool kContiguous = true;
-    const uint8_t *data;
-    uint8_t *words;
-    uint64_t key0, first, stride, pfirst;  // pfirst: the partner's first unit
-    uint32_t K, kq;
-    const uint8_t *dummy;
-    __device__ __forceinline__ WView view(uint32_t k) const {
-        const uint64_t u = k < kq ? first + uint64_t(k) * stride : pfirst + uint64_t(kq - 1) * stride;
         const bool in = k < K;
         return WView{in ? data + u * kRoundBytes : dummy, in ? words + 4 * CPU * u : const_cast<uint8_t *>(dummy),
                      key0 + CPU * u};
@@ -656,16 +634,6 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
         if (a.last_len % kRoundBytes)  // wave-uniform: a stream of whole rounds has no slow region
             slow_region<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
                                      a.check_short_tail, a.result);
-    } else if constexpr ((LAB & kLabSkew) != 0 && VERIFY) {
-        const uint32_t m = blockIdx.x & 3;
-        const bool ok = a.kr == 0 && gridDim.x % 4 == 0 && a.kq >= 2;
-        const uint32_t Ks = !ok ? K : m == 0 ? a.kq + 1 : m == 2 ? a.kq - 1 : a.kq;
-        // without the skew, round kq (waves below kr) is the wave's own: pfirst + (kq - 1) W = wave + kq W
-        SkewWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, ok ? wave + 2 * kWpb : wave + nwaves, Ks, a.kq,
-                         dummy};
-        wave_rounds<BPC, VERIFY, SOLO, false, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
-        if (a.len % kRoundBytes)
-            slow_region<BPC, VERIFY, TPB>(lds, a.data, words, a.len, a.chunk_base, a.check_short_tail, a.result);
     } else {
         BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, K, dummy, a.kq, a.kr};
         wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result, lab_mid);
