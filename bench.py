@@ -65,6 +65,10 @@ def parse():
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-compute", action="store_true", help="skip the compute-on-write block of the line")
     p.add_argument("--no-packets", action="store_true", help="skip the packet-stream block of the line")
+    p.add_argument("--no-configs2", action="store_true",
+                   help="skip BASELINE.json configs[2] (1 GiB compute + verify, bpc 512/2048/4096)")
+    p.add_argument("--no-config5", action="store_true",
+                   help="skip BASELINE.json configs[4] (loopback hdfsRead of 1 GiB, PCIe-inclusive, CPU reference)")
     p.add_argument("--sweep", action="store_true", help="extra diagnostics on stderr")
     p.add_argument("--graph", action="store_true",
                    help="replay the K steps from captured HIP graphs instead of launching them eagerly "
@@ -72,6 +76,7 @@ def parse():
     p.add_argument("--no-overlap", action="store_true",
                    help="barrier every timed launch (no HDFS3_LAUNCH_OVERLAP_PREVIOUS); the overlapped "
                         "run is the default and the barriered one is reported beside it")
+    p.add_argument("--out-json", default=None, help="also write the JSON line to this file (rank 0)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--plumbing-check", action="store_true",
                    help="CPU-only rehearsal of the N-rank entry (tests/test_multigpu.py): rank spawn, "
@@ -137,6 +142,22 @@ def spawn_ranks(n: int) -> int:
                     q.terminate()
         time.sleep(0.05)
     return rc
+
+
+def check_distinct_devices(rows, world, ndev):
+    """rows: gather_per_rank rows [rank, current_device, seed, elapsed, host_elapsed, rate, pci...].
+    With world > 1 and at least `world` visible GPUs, every rank must report its own device (ordinal
+    and, where torch exposes it, PCI address); otherwise SystemExit. Returns what was checked."""
+    if world <= 1:
+        return {"checked": False, "why": "one rank"}
+    if ndev < world:
+        return {"checked": False, "why": f"{ndev} visible GPU(s) for {world} ranks (a rehearsal sharing devices)"}
+    ords = [int(r[1]) for r in rows]
+    pcis = [tuple(int(x) for x in r[6:9]) for r in rows]
+    if len(set(ords)) != world or (all(p[1] >= 0 for p in pcis) and len(set(pcis)) != world):
+        raise SystemExit(f"MULTI-GPU FAILURE: {world} ranks on {ndev} visible GPUs but devices {ords} / pci {pcis} "
+                         "are not distinct")
+    return {"checked": True, "devices": ords}
 
 
 def gather_per_rank(dist, world, rank, row, device):
@@ -517,6 +538,215 @@ def paired_regions(torch, work, ctx, stream, n, overlap, dst, reps=3):
             "how": f"{reps} x (verify region, compute region), 50 warmup + settle + {n} timed launches each; medians"}
 
 
+def configs2_block(torch, work, ctx, stream, K, host_data, reps=3, warm=120, bpcs=(512, 2048, 4096)):
+    """BASELINE.json configs[2]: a 1 GiB synthetic stream per launch (the rank's 8 blocks as ONE
+    contiguous 1 GiB buffer, which they are in HBM), compute-on-write (`hdfs3_crc32c_compute_dev`,
+    OutputStreamImpl.cpp:298-359 / Packet.cpp:73-81) and verify-on-read (`hdfs3_crc32c_verify_dev_async`,
+    RemoteBlockReader.cpp:306-326) at bytes-per-checksum 512 / 2048 / 4096. Per bpc and launch form
+    (overlapped: HDFS3_LAUNCH_OVERLAP_PREVIOUS after each region's first launch; barriered: every
+    launch), `reps` x (verify region, compute region), each `warm` untimed launches (~20 ms of
+    sustained load), settle, then n = max(K, 20) timed launches between HIP events on the launch
+    stream; medians. Checked: the words the first compute wrote equal the oracle's for every chunk
+    of the GiB (before timing), a flipped bit comes back as its chunk, every verify result slot of
+    the timed regions is clean, and the timed compute launches' words equal those words (after)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from util import oracle_compute  # test infrastructure: the checker only, outside the timed regions
+
+    dev = work.data.device
+    flat = work.data.view(-1)
+    n_bytes = flat.numel()
+    dptr = flat.data_ptr()
+    n = max(K, 20)
+    res = torch.zeros(256, dtype=torch.int64, device=dev)
+    rp = res.data_ptr()
+    out = {"workload": f"{n_bytes >> 20} MiB contiguous stream per launch (the rank's {work.blocks} blocks), "
+                       "compute and verify, device-resident",
+           "bytes_per_launch": n_bytes, "timed_launches_per_region": n, "warmup_launches_per_region": warm,
+           "how": f"{reps} x (verify region, compute region) per launch form; medians",
+           "timing": "HIP events on the launch stream around each region's n launches (the clock of value)",
+           "bpc": {}}
+    for bpc in bpcs:
+        nch = (n_bytes + bpc - 1) // bpc
+        words = torch.full((4 * nch,), 0xA5, dtype=torch.uint8, device=dev)
+        dst = torch.full_like(words, 0x5A)
+        wp, op = words.data_ptr(), dst.data_ptr()
+        ctx.compute_dev(dptr, n_bytes, bpc, wp)
+        ctx.synchronize()
+        want = oracle_compute(host_data, bpc)
+        got = words.cpu().numpy()
+        if not np.array_equal(got, want):
+            bad = int(np.nonzero(got != want)[0][0]) // 4
+            raise SystemExit(f"PARITY FAILURE: configs2 bpc {bpc}: compute word {bad} differs from the oracle")
+        k = (nch * 5) // 7
+        pos = k * bpc + bpc // 3
+        orig = int(flat[pos].item())
+        flat[pos] = orig ^ 0x02
+        torch.cuda.synchronize()
+        first = ctx.verify_dev(dptr, n_bytes, bpc, wp)
+        flat[pos] = orig
+        torch.cuda.synchronize()
+        if first != k or ctx.verify_dev(dptr, n_bytes, bpc, wp) != -1:
+            raise SystemExit(f"PARITY FAILURE: configs2 bpc {bpc}: flip in chunk {k} reported as {first}")
+        alg = nch * (bpc + 4)  # verify reads C + 4 per chunk; compute reads C, writes 4
+
+        def ver(i, overlap):
+            ctx.verify_dev_async(dptr, n_bytes, bpc, wp, rp + 8 * (i % 256), overlap_previous=overlap and i > 0)
+
+        def cmp_(i, overlap):
+            ctx.compute_dev(dptr, n_bytes, bpc, op, overlap_previous=overlap and i > 0)
+
+        def region(fn, overlap):
+            for i in range(warm):
+                fn(i, overlap)
+            settle(torch, stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(n):
+                fn(i, overlap)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) * 1e-3 / n
+
+        row = {}
+        for form, overlap in (("overlapped", True), ("barriered", False)):
+            v, c = [], []
+            for _ in range(reps):
+                v.append(region(ver, overlap))
+                c.append(region(cmp_, overlap))
+            for mode, ts in (("verify", v), ("compute", c)):
+                t = sorted(ts)[reps // 2]
+                row.setdefault(mode, {})[form] = {
+                    "avg_launch_us": round(t * 1e6, 2), "value": round(n_bytes / t / 2**30, 1), "unit": "GiB/s",
+                    "achieved_GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
+                    "regions_us": [round(x * 1e6, 2) for x in ts]}
+            row.setdefault("compute_vs_verify", {})[form] = round(sorted(v)[reps // 2] / sorted(c)[reps // 2], 4)
+        if bool((res != 0).any().item()):
+            raise SystemExit(f"PARITY FAILURE: configs2 bpc {bpc}: a clean stream reported a bad chunk")
+        if not torch.equal(dst, words):
+            raise SystemExit(f"PARITY FAILURE: configs2 bpc {bpc}: the timed compute launches wrote other words")
+        row["alg_bytes_per_launch"] = alg
+        row["checked"] = (f"all {nch} words of the first compute against the oracle, a flipped bit in chunk {k}, "
+                          "every timed verify's result slot, the timed computes' words against those")
+        out["bpc"][str(bpc)] = row
+        del words, dst
+    return out
+
+
+def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4):
+    """BASELINE.json configs[4]: a 1 GiB file of 128 MiB blocks served by the loopback datanode over
+    127.0.0.1 TCP (64 KiB packets, test infrastructure), read end to end through the product's hdfsRead
+    (hdfs3_input_read, 4 MiB reads: InputStreamImpl's block walk -> the block reader's receiver ->
+    pinned arena -> H2D -> GPU verify -> caller buffer), i.e. PCIe-inclusive: verify on, verify off,
+    and block read-ahead 2 (hdfs3_input_set_readahead); the host API on the same GiB
+    (hdfs3_crc32c_verify: pinned and pageable host buffers, H2D-inclusive). Beside them, the
+    reference CPU path on the same packet stream: RemoteBlockReader's receive -> verifyChecksum ->
+    copy loop on the reading thread with the reference's own HWCrc32c (oracle/_ref; test
+    infrastructure, this baseline leg only; RemoteBlockReader.cpp:226-357), verify on and off.
+    Every line: one untimed first pass (reported as cold), then `reps` timed passes (median and all);
+    every pass's output buffer is compared with the file, byte for byte."""
+    import ctypes
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from loopback import LoopbackDatanode, reference_read_block
+    from util import ref_lib
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import CrcContext, InputStream
+
+    total = host_data.nbytes
+    nblk = total // block_bytes
+    crc_host = None
+    dn = LoopbackDatanode(packet_bytes=65536)
+    outbuf = np.empty(total, dtype=np.uint8)
+    lines = {}
+    dev = device.index or 0
+    try:
+        hctx = CrcContext(dev)  # the host API's own ctx (its pinned staging ring)
+        crc_host = hctx.compute(host_data, bpc)  # the .meta words the datanode serves (GPU compute)
+        blocks = []
+        for i in range(nblk):
+            dn.add_block(100 + i, host_data[i * block_bytes:(i + 1) * block_bytes],
+                         crc_host[4 * (i * block_bytes // bpc):4 * ((i + 1) * block_bytes // bpc)], bpc)
+            blocks.append((100 + i, block_bytes))
+        located = [(b, nb, [("127.0.0.1", dn.port)]) for b, nb in blocks]
+
+        def hdfs_read(verify, ahead):
+            with InputStream(located, device=dev, verify=verify, batch_packets=64) as s:
+                if ahead:
+                    s.set_readahead(ahead)
+                pos = 0
+                while pos < total:
+                    got = s.read_into(outbuf, pos, min(read_mib << 20, total - pos))
+                    if got <= 0:
+                        raise SystemExit(f"config5: hdfsRead returned {got} at {pos}")
+                    pos += got
+
+        def ref_read(verify):
+            for i, (b, nb) in enumerate(blocks):
+                reference_read_block(dn.port, b, nb, outbuf, i * block_bytes, verify=verify)
+
+        def host_api(buf):
+            bad = hctx.verify(buf, bpc, crc_host)
+            if bad != -1:
+                raise SystemExit(f"PARITY FAILURE: config5 host API reported chunk {bad} on a clean GiB")
+
+        def measure(fn, check_out=True):
+            rates = []
+            for rep in range(1 + reps):
+                if check_out:
+                    outbuf[::4096] = ~host_data[::4096]  # poison: every pass must rewrite the buffer
+                t0 = time.perf_counter()
+                fn()
+                dt = time.perf_counter() - t0
+                if check_out and not np.array_equal(outbuf, host_data):
+                    bad = int(np.nonzero(outbuf != host_data)[0][0])
+                    raise SystemExit(f"PARITY FAILURE: config5 delivered a wrong byte at {bad}")
+                rates.append(total / dt / 2**30)
+            timed = rates[1:]
+            return {"gib_s": round(sorted(timed)[len(timed) // 2], 2), "gib_s_all": [round(r, 2) for r in timed],
+                    "cold_gib_s": round(rates[0], 2), "unit": "GiB/s"}
+
+        lines["hdfsRead_verify"] = dict(measure(lambda: hdfs_read(True, 0)), readahead_blocks=0, verify=True)
+        lines["hdfsRead_no_verify"] = dict(measure(lambda: hdfs_read(False, 0)), readahead_blocks=0, verify=False)
+        lines["hdfsRead_verify_readahead2"] = dict(measure(lambda: hdfs_read(True, 2)), readahead_blocks=2,
+                                                   verify=True)
+        hp = ctypes.c_void_p()
+        _native.check("hdfs3_host_malloc_pinned", _native.lib().hdfs3_host_malloc_pinned(ctypes.byref(hp), total))
+        try:
+            pinned = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(hp.value))
+            pinned[:] = host_data
+            lines["host_api_pinned"] = dict(measure(lambda: host_api(pinned), check_out=False),
+                                            api="hdfs3_crc32c_verify on a pinned 1 GiB host buffer (H2D + verify)")
+            del pinned
+        finally:
+            _native.lib().hdfs3_host_free_pinned(hp)
+        lines["host_api_pageable"] = dict(measure(lambda: host_api(host_data), check_out=False),
+                                          api="hdfs3_crc32c_verify on a pageable 1 GiB host buffer "
+                                              "(staging copy + H2D + verify)")
+        if ref_lib() is not None:
+            lines["reference_cpu_verify"] = dict(measure(lambda: ref_read(True)), verify=True, cores=1,
+                                                 kind="reference")
+            lines["reference_cpu_no_verify"] = dict(measure(lambda: ref_read(False)), verify=False, cores=1,
+                                                    kind="reference")
+        hctx.close()
+    finally:
+        dn.stop()
+    out = {"workload": f"{total >> 20} MiB file = {nblk} x {block_bytes >> 20} MiB blocks, {bpc} B chunks, "
+                       f"64 KiB packets from a loopback datanode on 127.0.0.1 (test infrastructure), "
+                       f"{read_mib} MiB hdfsRead calls, one stream",
+           "lines": lines,
+           "reference_cpu": ("RemoteBlockReader's loop on the reading thread (receive a packet, verifyChecksum "
+                             "with the reference HWCrc32c built from src/common/HWCrc32c.cpp, copy to the caller; "
+                             "RemoteBlockReader.cpp:226-357) over the same loopback packet stream"),
+           "checked": "every pass's 1 GiB output buffer byte for byte against the file (poisoned before each "
+                      "pass); host API passes must report the GiB clean"}
+    if "reference_cpu_verify" in lines:
+        out["gpu_over_reference_cpu"] = round(lines["hdfsRead_verify"]["gib_s"] / lines["reference_cpu_verify"]["gib_s"], 2)
+        out["readahead2_over_reference_cpu"] = round(
+            lines["hdfsRead_verify_readahead2"]["gib_s"] / lines["reference_cpu_verify"]["gib_s"], 2)
+    return out
+
+
 def lab_context(work, stream):
     """A context of the measurement library (libhdfs3_crc_lab.so) on the bench's device and
     stream: the plain-read ceiling kernels live there, not in the product library."""
@@ -610,7 +840,7 @@ def cpu_quota_cores():
         return None
 
 
-def cpu_baseline(work, seconds, bpc):
+def cpu_baseline(work, seconds, bpc, data=None, crc=None):
     """Reference CPU path on this host, a bounded streaming sample of the same workload: the
     rank's whole block set (8 x 128 MiB = 1 GiB, host copies of the blocks and their CRC arrays),
     each thread verifying its own contiguous part, so every rep streams ~1 GiB from DRAM (more
@@ -624,8 +854,10 @@ def cpu_baseline(work, seconds, bpc):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from util import PCL, oracle, ref_lib  # test infrastructure: baseline leg only
 
-    data = np.ascontiguousarray(work.data.cpu().numpy()).reshape(-1)  # [blocks, bytes] -> one stream
-    crc = np.ascontiguousarray(work.crc.cpu().numpy()).reshape(-1)    # the blocks' CRC arrays, in order
+    if data is None:
+        data = np.ascontiguousarray(work.data.cpu().numpy()).reshape(-1)  # [blocks, bytes] -> one stream
+    if crc is None:
+        crc = np.ascontiguousarray(work.crc.cpu().numpy()).reshape(-1)    # the blocks' CRC arrays, in order
     affinity = max(1, len(os.sched_getaffinity(0)))
     quota = cpu_quota_cores()
     threads = max(1, min(affinity, int(quota))) if quota else affinity
@@ -735,6 +967,7 @@ def main():
         sys.exit(spawn_ranks(args.gpus))  # nothing in this process has touched a GPU
     if args.plumbing_check:
         return plumbing_check(args)
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -835,12 +1068,17 @@ def main():
     if args.mode == "verify" and bool((result != 0).any().item()):
         raise SystemExit("PARITY FAILURE: clean blocks reported a bad chunk in the timed region")
     my_rate = block_bytes * K / elapsed / 2**30
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    pci = [getattr(props, "pci_domain_id", -1), getattr(props, "pci_bus_id", -1), getattr(props, "pci_device_id", -1)]
     rows = gather_per_rank(dist, world, rank, [rank, torch.cuda.current_device(), rank_seed(rank), elapsed,
-                                               host_elapsed, my_rate], coll_device)
+                                               host_elapsed, my_rate] + pci, coll_device)
     dist_world = dist.get_world_size() if dist.is_initialized() else 1
     elapsed_max = max(r[3] for r in rows)
     host_max = max(r[4] for r in rows)
     value = aggregate_rate(block_bytes * K, world, elapsed_max)
+    # N > 1 on a node with >= N visible GPUs: every rank must have driven its own device (config 4 is
+    # one block set PER GPU); a launcher that mapped two ranks onto one device fails loudly here
+    distinct = check_distinct_devices(rows, world, ndev)
 
     if rank != 0:
         if world > 1:
@@ -848,6 +1086,9 @@ def main():
             dist.destroy_process_group()
         return
 
+    pre_pass = {"diagnostic_event_bracketed": D, "barriered": (max(D - K, 1000) + K) if overlap else 0,
+                "warmup": W}
+    pre_pass["total_before_timed_region"] = sum(pre_pass.values())
     launch_ms = [events[2 * s].elapsed_time(events[2 * s + 1]) for s in range(D)]
     eager_launch_s = sum(launch_ms[-K:]) / K * 1e-3  # the last K of the diagnostic pass
     avg_launch_s = elapsed / K  # rank 0's own launches, same clock as value
@@ -857,6 +1098,12 @@ def main():
                 "alg_bytes_per_launch": alg_bytes, "avg_launch_us": round(avg_launch_s * 1e6, 2),
                 "timing": "HIP events on the launch stream around the K timed steps / K (the clock of value)",
                 "eager_per_launch_us": round(eager_launch_s * 1e6, 2)}
+    if world > 1:
+        # the whole job against the whole node's HBM: N x alg bytes x K / max elapsed / (N x 8 TB/s)
+        roofline["aggregate_frac"] = round(world * alg_bytes * K / elapsed_max / 1e9 / (world * HBM_PEAK_GBPS), 4)
+        roofline["aggregate_achieved"] = round(world * alg_bytes * K / elapsed_max / 1e9, 1)
+        roofline["aggregate_peak"] = world * HBM_PEAK_GBPS
+        roofline["frac_note"] = "frac/achieved: rank 0's own launches; aggregate_*: all ranks over the slowest rank's time"
     extra = {}
     lab = None
     ceilings = None
@@ -894,6 +1141,11 @@ def main():
                 v = roofline["frac"] if m == "overlapped" else (barriered or {}).get("frac")
                 if v:
                     extra["compute"][m]["frac_vs_verify"] = round(extra["compute"][m]["frac"] / v, 4)
+        host_data = None
+        if args.mode == "verify" and (not args.no_configs2 or not args.no_config5):
+            host_data = np.ascontiguousarray(work.data.cpu().numpy()).reshape(-1)
+        if args.mode == "verify" and not args.no_configs2:
+            extra["configs2"] = configs2_block(torch, work, ctx, stream, K, host_data)
         if args.mode == "verify" and not args.no_packets:
             pk = packets_block(torch, work, ctx, K, W, stream)
             if pk:
@@ -905,9 +1157,11 @@ def main():
             raise
         except Exception as e:
             log("batched pass failed:", e)
+    if world == 1 and args.mode == "verify" and not args.no_config5 and args.bpc == 512:
+        extra["config5"] = config5_block(torch, device, host_data, args.bpc, block_bytes)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(work, args.cpu_seconds, args.bpc)
+        cpu = cpu_baseline(work, args.cpu_seconds, args.bpc, data=host_data)
     if args.sweep and world == 1 and lab is not None:
         log(json.dumps({"lane_read_GBps": round(lane_read_rate(torch, work, lab), 1)}))
     if world == 1 and not args.no_pmc:
@@ -917,7 +1171,8 @@ def main():
 
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": K,
-        "warmup": W, "ms_per_step": round(elapsed_max / K * 1e3, 4), "higher_is_better": True,
+        "warmup": W, "pre_pass_launches": pre_pass, "ms_per_step": round(elapsed_max / K * 1e3, 4),
+        "higher_is_better": True,
         "host_ms_per_step": round(host_max / K * 1e3, 4),
         "clock": "value, ms_per_step and roofline: HIP events on each rank's launch stream around its K timed "
                  "steps (max over ranks); host_ms_per_step: host wall clock of the same barrier+synchronize bracket",
@@ -933,9 +1188,10 @@ def main():
                    "parallelism": f"{world} GPU(s), independent blocks one set per GPU, no collectives"},
         "world_size": dist_world, "backend": backend if world > 1 else None,
         "roofline": roofline, "cpu_baseline": cpu,
-        "per_rank": [{"rank": int(r[0]), "current_device": int(r[1]), "seed": int(r[2]),
-                      "ms_per_step": round(r[3] / K * 1e3, 4),
-                      "value": round(r[5], 2)} for r in rows],
+        "per_rank": [{"rank": int(r[0]), "current_device": int(r[1]), "pci": [int(x) for x in r[6:9]],
+                      "seed": int(r[2]), "ms_per_step": round(r[3] / K * 1e3, 4), "value": round(r[5], 2),
+                      "frac": round(alg_bytes * K / r[3] / 1e9 / HBM_PEAK_GBPS, 4)} for r in rows],
+        "distinct_devices": distinct,
     }
     if "barriered" in extra:
         line["barriered"] = extra["barriered"]
@@ -945,6 +1201,10 @@ def main():
         line["packets"] = extra["packets"]
     if "compute" in extra:
         line["compute"] = extra["compute"]
+    if "configs2" in extra:
+        line["configs2"] = extra["configs2"]
+    if "config5" in extra:
+        line["config5"] = extra["config5"]
     if cpu:
         line["gpu_over_cpu"] = round(value / cpu["value"], 1)
         line["gpu_over_cpu_note"] = (f"against the reference engine on {cpu['cores']} threads = the effective cores "
@@ -953,6 +1213,9 @@ def main():
         if "pcl_port" in cpu and "all_cores" in cpu["pcl_port"]:
             line["gpu_over_cpu_pcl"] = round(value / cpu["pcl_port"]["all_cores"]["value"], 1)
     print(json.dumps(line), flush=True)
+    if args.out_json:
+        with open(args.out_json, "w") as f:
+            f.write(json.dumps(line) + "\n")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -123,14 +123,24 @@ LocalPoolStats entry_bytes(const LocalResources &r) {
     return st;
 }
 
+// a pooled entry dropped to keep the cap: destroyed outright, as local_pool_trim does. Releasing its
+// ctx into the ctx pool would only move the bytes the cap just refused into the other pool.
+void destroy_resources(LocalResources &r) {
+    for (PacketArena &a : r.a) a.release();
+    hdfs3_crc_ctx_destroy(r.ctx);
+    r.ctx = nullptr;
+}
+
 // Pooled unless that would take the retained pinned bytes of both pools past the cap
-// (HDFS3_POOL_PINNED_MAX): the oldest pooled entries are freed first, then this one.
+// (HDFS3_POOL_PINNED_MAX): the oldest pooled entries are evicted first, then this one is not
+// admitted. The decision is made under pool_admission_mu (ctx.h), so a ctx_release or another
+// give_back on another thread cannot admit bytes into the same headroom meanwhile.
 void give_back(LocalResources r) {
     std::vector<LocalResources> evict;
     bool keep = false;
-    // the ctx pool's bytes first, outside g_pool_mu: ctx_release takes the two locks the other way round
-    const uint64_t cap = pool_pinned_cap_bytes(), ctxs = ctx_pool_pinned_bytes(), mine = entry_bytes(r).pinned;
     {
+        std::lock_guard<std::mutex> adm(pool_admission_mu());
+        const uint64_t cap = pool_pinned_cap_bytes(), ctxs = ctx_pool_pinned_bytes(), mine = entry_bytes(r).pinned;
         std::lock_guard<std::mutex> lk(g_pool_mu);
         if (g_pool.size() < kPoolMax) {
             uint64_t local = 0;
@@ -146,7 +156,9 @@ void give_back(LocalResources r) {
             }
         }
     }
-    for (LocalResources &e : evict) free_resources(e);
+    for (LocalResources &e : evict) destroy_resources(e);
+    // not admitted: the windows go, and the ctx takes its own admission into the ctx pool
+    // (ctx_release takes pool_admission_mu itself, so this runs after the scope above)
     if (!keep) free_resources(r);
 }
 

@@ -87,6 +87,12 @@ uint64_t pool_pinned_cap_bytes();
 // bytes the ctx pool retains now
 void ctx_footprint(hdfs3_crc_ctx *ctx, uint64_t *pinned, uint64_t *device);
 uint64_t ctx_pool_pinned_bytes();
+// Serialises every ADMISSION into either pool (ctx_release, the local readers' give_back): the only
+// operations that add retained pinned bytes. Each admission reads the other pool's bytes and decides
+// under this lock, so two releases at once cannot both fit the same headroom. Taking a
+// ctx or an entry out of a pool, shedding and trimming only lower the total and do not take it.
+// Order: this lock first, then a pool's own mutex (never the reverse).
+std::mutex &pool_admission_mu();
 // The short-circuit readers' own pool (local_reader.cpp: a ctx and its windows per entry) counts
 // against the same cap: its retained bytes, pooled entries, and a trim that frees them all
 struct LocalPoolStats {

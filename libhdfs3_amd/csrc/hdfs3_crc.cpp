@@ -619,6 +619,11 @@ void shed(hdfs3_crc_ctx *ctx, size_t keep_arenas, bool slots) {
 
 uint64_t pool_pinned_cap_bytes() { return pool_pinned_cap(); }
 
+std::mutex &pool_admission_mu() {
+    static std::mutex mu;
+    return mu;
+}
+
 void ctx_footprint(hdfs3_crc_ctx *ctx, uint64_t *pinned, uint64_t *device) {
     const Footprint f = footprint(ctx);
     if (pinned) *pinned = f.pinned;
@@ -668,10 +673,11 @@ void ctx_release(hdfs3_crc_ctx *ctx) {
         ok = hipStreamSynchronize(ctx->stream) == hipSuccess;
     }
     for (Slot &s : ctx->slot) s.pending_out = nullptr;
-    // the short-circuit readers' pool counts against the same cap (taken before g_ctx_pool_mu: the
-    // local pool locks its own mutex first and then this one)
-    const uint64_t local = ok ? local_pool_stats().pinned : 0;
     if (ok) {
+        // one admission at a time across both pools (pool_admission_mu): the short-circuit readers'
+        // pool counts against the same cap, and its bytes cannot grow while this decision is made
+        std::lock_guard<std::mutex> adm(pool_admission_mu());
+        const uint64_t local = local_pool_stats().pinned;
         std::lock_guard<std::mutex> lk(g_ctx_pool_mu);
         if (g_ctx_pool.size() < kCtxPoolMax) {
             // a read-ahead reader's deep ring leaves up to a block's worth of pinned arenas in

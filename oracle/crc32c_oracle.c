@@ -291,3 +291,17 @@ void oracle_compute_chunks_crc32(const void *data, size_t len, uint32_t bpc, voi
         wr_be32(o + 4 * i, ~oracle_crc32_update(0xFFFFFFFFu, d + off, sz));
     }
 }
+
+/* ---- the reference's remote read loop (config-5 CPU baseline, oracle/remote_loop.h) ---- */
+
+#include "remote_loop.h"
+
+static int64_t loop_verify(void *user, const void *data, int64_t len, int bpc, const void *crc_be) {
+    return oracle_verify_chunks(*(int *)user, data, (size_t)len, (uint32_t)bpc, crc_be, 0);
+}
+
+int64_t oracle_remote_read_block(int fd, int engine, void *out, int64_t cap, int bpc, int verify,
+                                 int64_t *bad_packet) {
+    ensure_init();
+    return remote_loop_read_block(fd, out, cap, bpc, verify, bad_packet, loop_verify, &engine);
+}

@@ -72,6 +72,13 @@ void oracle_fill_splitmix(void *dst, size_t len, uint64_t seed);
 uint32_t oracle_crc32_update(uint32_t state, const void *p, size_t len);
 void oracle_compute_chunks_crc32(const void *data, size_t len, uint32_t bpc, void *crc_be_out);
 
+/* One block of an OP_READ_BLOCK connection (request and response already exchanged) through
+ * RemoteBlockReader's receive -> verifyChecksum -> copy loop on the calling thread
+ * (src/client/RemoteBlockReader.cpp:226-357; oracle/remote_loop.h), with a restated engine.
+ * Returns bytes copied to out, -1 on error; *bad_packet = first packet that failed verify. */
+int64_t oracle_remote_read_block(int fd, int engine, void *out, int64_t cap, int bpc, int verify,
+                                 int64_t *bad_packet);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,6 +19,8 @@
 #include <time.h>
 #include <arpa/inet.h>
 
+#include "remote_loop.h"
+
 using Hdfs::Internal::HWCrc32c;
 
 extern "C" {
@@ -112,6 +114,16 @@ double ref_hw_bench_verify(const void *data, int64_t len, int bpc, const void *c
     clock_gettime(CLOCK_MONOTONIC, &t1);
     if (bad_out) *bad_out = bad;
     return double(t1.tv_sec - t0.tv_sec) + 1e-9 * double(t1.tv_nsec - t0.tv_nsec);
+}
+
+static int64_t ref_loop_verify(void *, const void *data, int64_t len, int bpc, const void *crc_be) {
+    return ref_hw_verify(data, len, bpc, crc_be, 0);
+}
+
+/* One block through RemoteBlockReader's receive -> verify -> copy loop (oracle/remote_loop.h)
+ * with the reference's HWCrc32c: the config-5 CPU baseline (bench.py). */
+int64_t ref_remote_read_block(int fd, void *out, int64_t cap, int bpc, int verify, int64_t *bad_packet) {
+    return remote_loop_read_block(fd, out, cap, bpc, verify, bad_packet, ref_loop_verify, nullptr);
 }
 
 }  // extern "C"

@@ -97,3 +97,46 @@ class LoopbackDatanode:
         if self.port:
             self.lb.hdfs3_loopback_stop(self.port)
             self.port = 0
+
+
+def reference_read_block(port: int, block_id: int, nbytes: int, out: np.ndarray, offset: int = 0, *,
+                         verify: bool = True, engine: str = "reference") -> int:
+    """Test/bench infrastructure (bench.py's config-5 CPU baseline): one block read the way the
+    reference's RemoteBlockReader reads it — OP_READ_BLOCK, the BlockOpResponseProto check, then
+    every packet received, verified by the CPU engine on this thread and copied to `out`
+    (RemoteBlockReader.cpp:112-357, oracle/remote_loop.h), then the ClientReadStatusProto.
+    engine: "reference" = oracle/_ref's HWCrc32c (the reference source), "hw" / "pcl" = the
+    oracle's restatements. Returns the bytes delivered; raises on a checksum mismatch."""
+    import dtp
+    from util import HW, PCL, oracle, ref_lib
+
+    conn = dtp.Conn(port)
+    try:
+        conn.s.settimeout(None)
+        conn.s.sendall(dtp.read_block_request(block_id, 0, nbytes, pool=b"BP-loopback"))
+        resp = dtp.parse(conn.recv_delimited())
+        if resp[1][0] != 0:
+            raise OSError(f"datanode refused block {block_id}: status {resp[1][0]}")
+        bpc = dtp.parse(dtp.parse(resp[4][0])[1][0])[2][0]
+        bad = ctypes.c_int64(-1)
+        view = out[offset:offset + nbytes]
+        if engine == "reference":
+            lib = ref_lib()
+            fn = lib.ref_remote_read_block
+            fn.restype, fn.argtypes = ctypes.c_int64, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                                       ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+            got = fn(conn.s.fileno(), view.ctypes.data, nbytes, bpc, int(verify), ctypes.byref(bad))
+        else:
+            fn = oracle().oracle_remote_read_block
+            fn.restype, fn.argtypes = ctypes.c_int64, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                                       ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+            got = fn(conn.s.fileno(), {"hw": HW, "pcl": PCL}[engine], view.ctypes.data, nbytes, bpc, int(verify),
+                     ctypes.byref(bad))
+        if got < 0:
+            raise OSError(f"block {block_id}: the reference read loop failed")
+        if bad.value >= 0:
+            raise OSError(f"ChecksumException: block {block_id} packet {bad.value}")
+        conn.send_status(6 if verify else 0)  # CHECKSUM_OK / SUCCESS (RemoteBlockReader.cpp:289-304)
+        return got
+    finally:
+        conn.close()

@@ -13,11 +13,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(320)  # the verify line carries configs[2] and configs[4] too (~1 min on the box)
 @pytest.mark.parametrize("mode", ["verify", "compute"])
 def test_bench_json_line(mode):
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "50", "--warmup", "10", "--no-pmc",
            "--no-cpu-baseline", "--mode", mode]
-    out = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=110)
+    out = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, out.stdout
@@ -34,3 +35,25 @@ def test_bench_json_line(mode):
     assert 0 < r["frac"] <= 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     # verify reads data + words; compute reads data and writes words: same algorithmic bytes
     assert r["alg_bytes_per_launch"] == 262144 * (512 + 4)
+    # the untimed launches before the timed region are disclosed beside `warmup`
+    pp = j["pre_pass_launches"]
+    assert pp["warmup"] == 10 and pp["total_before_timed_region"] == sum(v for k, v in pp.items()
+                                                                         if k != "total_before_timed_region")
+    if mode != "verify":
+        return
+    # BASELINE.json configs[2]: 1 GiB per launch, compute + verify at bpc 512 / 2048 / 4096, both forms
+    c2 = j["configs2"]
+    assert c2["bytes_per_launch"] == 1 << 30 and sorted(c2["bpc"]) == ["2048", "4096", "512"]
+    for bpc, row in c2["bpc"].items():
+        assert row["alg_bytes_per_launch"] == (1 << 30) // int(bpc) * (int(bpc) + 4)
+        for m in ("verify", "compute"):
+            for form in ("overlapped", "barriered"):
+                assert 0 < row[m][form]["frac"] <= 1, (bpc, m, form)
+        assert 0.5 < row["compute_vs_verify"]["overlapped"] < 1.5 and "checked" in row
+    # BASELINE.json configs[4]: loopback hdfsRead of 1 GiB, PCIe-inclusive, the reference CPU path beside it
+    c5 = j["config5"]["lines"]
+    for k in ("hdfsRead_verify", "hdfsRead_no_verify", "hdfsRead_verify_readahead2", "host_api_pinned",
+              "host_api_pageable"):
+        assert c5[k]["gib_s"] > 0 and len(c5[k]["gib_s_all"]) == 3, k
+    if "reference_cpu_verify" in c5:  # oracle/_ref travels with the tree when it was built
+        assert c5["reference_cpu_verify"]["kind"] == "reference" and c5["reference_cpu_verify"]["gib_s"] > 0

@@ -175,6 +175,61 @@ def test_overlapped_stream_chain_and_large_stream(gpu_ctx):
             assert w == 0, i
 
 
+@pytest.mark.parametrize("bpc", [8192, 65536])
+def test_overlapped_chain_chunks_above_4k_pieces(gpu_ctx, bpc):
+    """an overlapped verify at bpc = R x 4096 runs the piece compute of the pitch walk
+    (crc32c_wave_kernel<4096, compute, PITCH, SOLO>) without the AQL barrier, then the combine. 30
+    chained launches over 5 resident arenas of 64 KiB packets (one arena corrupted, one with a short
+    last packet), each into its own result word, alternating the two piece buffers: every word
+    reports exactly its arena's first bad (packet, chunk), and a compute -> verify round trip in
+    the same overlapped form writes the oracle's words."""
+    from libhdfs3_amd.engine import CrcContext, DeviceBuffer
+
+    n, plen = 96, 65536
+    arenas, streams, hosts = [], [], []
+    for a in range(5):
+        last = plen if a != 3 else bpc * 2 + 300
+        host, pitch, crc_off, data_off, datas = build_arena(n, plen, last, bpc, 7000 + 131 * a + bpc % 1013)
+        hosts.append((host, pitch, crc_off, data_off, datas))
+        arenas.append(gpu_ctx.upload(host))
+        streams.append(CrcContext.packet_stream(crc_off, data_off, pitch, n, plen, last))
+    p_bad, q_bad = 61, 40000
+    host, pitch, crc_off, data_off, datas = hosts[2]
+    bad = host.copy()
+    bad[p_bad * pitch + data_off + q_bad] ^= 0x20
+    gpu_ctx.upload(bad, arenas[2])
+    want2 = oracle_key([np.frombuffer(bad[i * pitch + data_off:i * pitch + data_off + datas[i].size], np.uint8)
+                        for i in range(n)], bad, pitch, crc_off, bpc, False)
+    assert want2 == (p_bad, q_bad // bpc)
+    res = DeviceBuffer(30 * 8)
+    gpu_ctx.memset(res, 0, 30 * 8)
+    for i in range(30):
+        a = i % 5
+        gpu_ctx.verify_packet_stream_async(arenas[a].ptr, hosts[a][0].nbytes, streams[a], bpc, res.ptr + 8 * i,
+                                           overlap_previous=i > 0)
+    gpu_ctx.synchronize()
+    words = gpu_ctx.download(res, 30 * 8).view(np.uint64).tolist()
+    for i, w in enumerate(words):
+        if i % 5 == 2:
+            key = gpu_ctx.decode_result(int(w))
+            assert (key >> 32, key & 0xFFFFFFFF) == want2, i
+        else:
+            assert w == 0, i
+    # compute (barriered, its scratch alternating with the verifies') then overlapped verifies of it
+    host, pitch, crc_off, data_off, datas = hosts[3]
+    blank = host.copy()
+    for i in range(n):
+        blank[i * pitch + crc_off:i * pitch + data_off] = 0
+    gpu_ctx.upload(blank, arenas[3])
+    gpu_ctx.compute_packet_stream_async(arenas[3].ptr, host.nbytes, streams[3], bpc)
+    gpu_ctx.memset(res, 0, 30 * 8)
+    for i in range(6):
+        gpu_ctx.verify_packet_stream_async(arenas[3].ptr, host.nbytes, streams[3], bpc, res.ptr + 8 * i,
+                                           overlap_previous=i > 0)
+    assert np.array_equal(gpu_ctx.download(arenas[3], host.nbytes), host)
+    assert not gpu_ctx.download(res, 6 * 8).view(np.uint64).any()
+
+
 def test_compute_word_scratch_grows_across_calls(gpu_ctx):
     """Compute over in-packet words goes through the ctx's dense word scratch and a scatter
     kernel. Streams of growing length on one ctx (the scratch is reallocated between them, after

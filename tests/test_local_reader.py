@@ -306,6 +306,90 @@ def test_pooled_readers_count_against_the_pinned_cap(tmp_path, cap_mib):
     assert p2 == 0 and n2 == 0
 
 
+_CONCURRENT_POOL_CHILD = r"""
+import ctypes, sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from libhdfs3_amd import _native
+from libhdfs3_amd.engine import CrcContext, LocalBlockReader
+lib = _native.lib()
+files = sys.argv[2:]
+pairs = [(files[i], files[i + 1]) for i in range(0, len(files), 2)]
+over, errors = [], []
+mu = threading.Lock()
+
+def sample(where):
+    st = _native.PoolStats()
+    assert lib.hdfs3_crc_pool_stats_get(ctypes.byref(st)) == 0
+    if st.pinned_bytes > st.pinned_cap_bytes:
+        with mu:
+            over.append((where, st.pinned_bytes, st.pinned_cap_bytes))
+
+def local_worker(t):
+    try:
+        for k in range(2):  # 8 threads x 2 readers = the 16 block files, closed concurrently
+            d, m = pairs[2 * t + k]
+            r = LocalBlockReader(d, m)
+            out = r.read_all(1 << 30)
+            assert out.nbytes == np.fromfile(d, dtype=np.uint8).nbytes
+            r.close()
+            sample(f"local {t}.{k}")
+    except Exception as e:
+        errors.append(repr(e))
+
+def ctx_worker(t):
+    # contexts released into the ctx pool at the same time, each holding host-API staging
+    try:
+        data = np.random.default_rng(t).integers(0, 256, (3 << 20) + 512 * t, dtype=np.uint8)
+        for k in range(3):
+            p = ctypes.c_void_p()
+            assert lib.hdfs3_crc_ctx_acquire(0, ctypes.byref(p)) == 0
+            words = np.zeros(4 * ((data.nbytes + 511) // 512), np.uint8)
+            assert lib.hdfs3_crc32c_compute(p, data.ctypes.data, data.nbytes, 512, words.ctypes.data) == 0
+            lib.hdfs3_crc_ctx_release(p)
+            sample(f"ctx {t}.{k}")
+    except Exception as e:
+        errors.append(repr(e))
+
+th = [threading.Thread(target=local_worker, args=(t,)) for t in range(8)]
+th += [threading.Thread(target=ctx_worker, args=(t,)) for t in range(4)]
+for x in th:
+    x.start()
+for x in th:
+    x.join()
+sample("end")
+st = _native.PoolStats()
+assert lib.hdfs3_crc_pool_stats_get(ctypes.byref(st)) == 0
+print("over", len(over), over[:3])
+print("errors", len(errors), errors[:3])
+print("final", st.pinned_bytes, st.pinned_cap_bytes, st.pooled_contexts)
+"""
+
+
+def test_concurrent_closes_keep_the_pinned_cap(tmp_path):
+    """ADVICE/VERDICT r4: admissions into the two pools used to be check-then-act across two mutexes, so
+    readers closing at once could each take the same headroom. 16 short-circuit readers closed from 8
+    threads while 4 more threads release host-API contexts into the ctx pool, at a 24 MiB cap: after
+    every close and release, hdfs3_crc_pool_stats_get reports pinned_bytes <= cap."""
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = []
+    for i in range(16):
+        args += write_block(tmp_path, f"cblk{i}", splitmix_bytes((5 << 20) + 4096 * i + 77, 1300 + i))
+    env = dict(os.environ, HDFS3_POOL_PINNED_MAX="24M")
+    out = subprocess.run([sys.executable, "-c", _CONCURRENT_POOL_CHILD, repo] + args, env=env, capture_output=True,
+                         text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = {ln.split()[0]: ln for ln in out.stdout.splitlines() if ln.strip()}
+    assert lines["errors"].startswith("errors 0"), lines["errors"]
+    assert lines["over"].startswith("over 0 "), lines["over"]
+    pinned, cap, pooled = (int(x) for x in lines["final"].split()[1:])
+    assert cap == 24 << 20 and pinned <= cap and pooled >= 1
+
+
 _KNOB_CHILD = r"""
 import sys
 import numpy as np

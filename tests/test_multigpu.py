@@ -64,6 +64,23 @@ def test_bench_gpus_2_real_run_on_one_gpu():
     # aggregate = both ranks' bytes / the slower rank's time = 2 x the slower rank's own rate
     # (per-rank rates carry 0.01 GiB/s rounding; ms_per_step only 4 decimals, too coarse here)
     assert j["value"] == pytest.approx(2 * min(a["value"], b["value"]), rel=1e-3)
+    _check_scaling_fields(j, 2)
+
+
+def _check_scaling_fields(j, n):
+    """The N > 1 line reads as a scaling point: the whole job against N x 8 TB/s, every rank's own
+    fraction, and the device-distinctness check (skipped, and saying why, when ranks share a GPU)."""
+    r = j["roofline"]
+    assert r["aggregate_peak"] == n * 8000.0
+    alg = r["alg_bytes_per_launch"]
+    # ms_per_step carries 4 decimals (0.0041 ms at 16 MiB blocks): checks through it allow that rounding
+    tol = max(2e-3, 0.6e-4 / j["ms_per_step"])
+    assert r["aggregate_frac"] == pytest.approx(n * alg / (j["ms_per_step"] * 1e-3) / 1e9 / (n * 8000.0), rel=tol)
+    for p in j["per_rank"]:
+        assert p["frac"] == pytest.approx(alg / (p["ms_per_step"] * 1e-3) / 1e9 / 8000.0, rel=tol)
+    # the whole job's fraction is the slowest rank's (weak scaling, max-over-ranks time)
+    assert min(p["frac"] for p in j["per_rank"]) == pytest.approx(r["aggregate_frac"], abs=1.5e-4)
+    assert j["distinct_devices"]["checked"] is False and "visible GPU" in j["distinct_devices"]["why"]
 
 
 def _multi(devices):
@@ -189,6 +206,26 @@ def test_bench_gpus_8_driver_command_rehearsed_on_one_gpu():
     slowest = max(r["ms_per_step"] for r in ranks)
     assert j["ms_per_step"] == pytest.approx(slowest, rel=1e-3)
     assert j["value"] == pytest.approx(8 * min(r["value"] for r in ranks), rel=1e-3)
+    _check_scaling_fields(j, 8)
+
+
+def test_distinct_devices_check_cpu():
+    """bench.py's N > 1 guard: with >= N visible GPUs every rank must report its own device."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    row = lambda r, d, pci: [r, d, 0, 1.0, 1.0, 1.0, 0, pci, 0]
+    assert bench.check_distinct_devices([row(0, 0, 3)], 1, 8)["checked"] is False
+    ok = bench.check_distinct_devices([row(r, r, 10 + r) for r in range(8)], 8, 8)
+    assert ok == {"checked": True, "devices": list(range(8))}
+    shared = bench.check_distinct_devices([row(r, 0, 10) for r in range(8)], 8, 1)  # the 1-GPU rehearsal
+    assert shared["checked"] is False and "1 visible GPU" in shared["why"]
+    with pytest.raises(SystemExit, match="not distinct"):
+        bench.check_distinct_devices([row(r, r % 4, 10 + r % 4) for r in range(8)], 8, 8)
+    with pytest.raises(SystemExit, match="not distinct"):  # distinct ordinals, one PCI device
+        bench.check_distinct_devices([row(r, r, 10) for r in range(8)], 8, 8)
+    # torch without PCI fields (-1): the ordinals alone decide
+    assert bench.check_distinct_devices([row(r, r, -1) for r in range(2)], 2, 2)["checked"] is True
 
 
 @pytest.mark.gpu
