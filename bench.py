@@ -499,7 +499,70 @@ def packets_block(torch, work, ctx, K, W, stream, reps=3):
         raise SystemExit("PARITY FAILURE: clean packets reported a bad chunk in the packet-stream regions")
     out["checked"] = "every launch's result slot after the timed regions; a flipped bit located before them"
     del arena
+    out["reader_batch"] = reader_batch_layouts(torch, work, ctx, stream)
     return out
+
+
+def reader_batch_layouts(torch, work, ctx, stream, npk=64, nbat=16, reps=5, n=200):
+    """The block reader's own GPU unit: one batch of 64 datanode packets (64 KiB data, 512 B chunks),
+    verified by one barriered launch, in the two device layouts the reader can land a batch in
+    (block_reader.cpp): `wire` = [128 BE32 words][64 KiB data] per packet at a 66,048-byte pitch (the
+    pitch walk; rounds 1-4), `dense` = the 64 packets' words back to back, then their data back to back
+    from a 4 KiB boundary (one contiguous 4 MiB block and its word array: the block walk; round 5
+    default). `nbat` batches rotate (64 MiB, as the reader's just-copied arenas, cache-resident); per
+    layout `reps` regions of `n` barriered launches (HIP events), median. Results checked."""
+    plen, bpc = 65536, 512
+    dev = work.data.device
+    src = work.data[0, :nbat * npk * plen].view(nbat, npk, plen)
+    words = work.crc[0, :nbat * npk * 512].view(nbat, npk, 512)
+    pitch = 512 + plen
+    wire = torch.empty((nbat, npk, pitch), dtype=torch.uint8, device=dev)
+    wire[:, :, :512] = words
+    wire[:, :, 512:] = src
+    d0 = npk * 512  # 32 KiB of words, already 4 KiB aligned
+    dense = torch.empty((nbat, d0 + npk * plen), dtype=torch.uint8, device=dev)
+    dense[:, :d0] = words.reshape(nbat, -1)
+    dense[:, d0:] = src.reshape(nbat, -1)
+    torch.cuda.synchronize()
+    res = torch.zeros(256, dtype=torch.int64, device=dev)
+    rp = res.data_ptr()
+    ps = ctx.packet_stream(0, 512, pitch, npk, plen)
+    wb, db, wspan, dspan = wire.data_ptr(), dense.data_ptr(), npk * pitch, d0 + npk * plen
+
+    def w_launch(i):
+        ctx.verify_packet_stream_async(wb + (i % nbat) * wspan, wspan, ps, bpc, rp + 8 * (i % 256))
+
+    def d_launch(i):
+        b = db + (i % nbat) * dspan
+        ctx.verify_dev_async(b + d0, npk * plen, bpc, b, rp + 8 * (i % 256))
+
+    def region(fn):
+        for i in range(50):
+            fn(i)
+        settle(torch, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(n):
+            fn(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / n
+
+    w, d = [], []
+    for _ in range(reps):
+        w.append(region(w_launch))
+        d.append(region(d_launch))
+    if bool((res != 0).any().item()):
+        raise SystemExit("PARITY FAILURE: clean reader batches reported a bad chunk")
+    wm, dm = sorted(w)[reps // 2], sorted(d)[reps // 2]
+    alg = npk * (plen // bpc) * (bpc + 4)
+    del wire, dense
+    return {"packets_per_batch": npk, "batch_payload_bytes": npk * plen, "launch": "barriered, one per batch",
+            "wire_us": round(wm, 2), "dense_us": round(dm, 2), "dense_speedup": round(wm / dm, 4),
+            "wire_frac": round(alg / (wm * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+            "dense_frac": round(alg / (dm * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+            "how": f"{nbat} resident batches rotating, {reps} x (wire region, dense region) of 50 warmup + {n} "
+                   "timed barriered launches; medians; every result slot checked"}
 
 
 def paired_regions(torch, work, ctx, stream, n, overlap, dst, reps=3):

@@ -79,6 +79,10 @@ int hdfs3_block_reader_close(hdfs3_block_reader *r);
  * ---------------------------------------------------------------------------------- */
 typedef struct hdfs3_input_stream hdfs3_input_stream;
 
+/* A datanode as the namenode's LocatedBlock names it, reduced to its transfer address: write
+ * targets (OP_WRITE_BLOCK, DataTransferProtocolSender.cpp:80-90) go out with this host and port and
+ * an empty uuid, zero info/ipc ports and an EMPTY location (rack) — the reference sends the
+ * namenode's rack there (e.g. "/default-rack"); datanodes use it for nothing on this path. */
 typedef struct hdfs3_datanode {  /* DatanodeInfo transfer address */
     const char *host;
     int port;

@@ -95,6 +95,11 @@ int hdfs3_fs_set_sink(hdfsFS fs, const char *path, hdfs3_packet_sink sink, void 
  * hdfsOpenFile(O_RDONLY)/hdfsRead read back what was written. Takes precedence over a sink.
  * 0, or -1 with errno (EINVAL). */
 int hdfs3_fs_set_pipeline(hdfsFS fs, const char *path, const hdfs3_located_block *blocks, int n_blocks);
+/* the file's block size as FileStatus::getBlockSize reports it (what O_APPEND continues with,
+ * OutputStreamImpl.cpp:196-230); a clean close of a write through hdfs3_fs_set_pipeline records the
+ * size it wrote with. Unset for a file of one block: the caller's or the session's size is used.
+ * 0, or -1 with errno (EINVAL). */
+int hdfs3_fs_set_block_size(hdfsFS fs, const char *path, int64_t block_size);
 /* the generation stamp updateBlockForPipeline would give `path`'s last block when it is next
  * opened O_APPEND (Pipeline.cpp:274-276); unset: that block's stamp + 1. 0, or -1 with errno. */
 int hdfs3_fs_set_append_stamp(hdfsFS fs, const char *path, uint64_t new_generation_stamp);

@@ -272,6 +272,7 @@ HDFS_API = {
     "hdfs3_fs_set_pipeline": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_int]),
     "hdfs3_fs_set_readahead": (c_int, [c_void_p, c_int, c_int64]),
     "hdfs3_fs_set_append_stamp": (c_int, [c_void_p, ctypes.c_char_p, c_uint64]),
+    "hdfs3_fs_set_block_size": (c_int, [c_void_p, ctypes.c_char_p, ctypes.c_int64]),
 }
 
 # measurement hooks (libhdfs3_crc_lab.so only; not in any public header)

@@ -21,6 +21,7 @@
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -67,6 +68,11 @@ struct Batch {
     bool verified = false;
     int64_t bad_pkt = -1;
     size_t dpkt = 0, doff = 0;  // delivery cursor
+    // dense layout (round 5, see receive()): words of every packet back to back from offset 0, the
+    // packets' data back to back from d0; chunk0[i] = packet i's first chunk in the batch
+    bool dense = false, sealed = false;
+    uint64_t d0 = 0, words_used = 0, data_used = 0;
+    std::vector<uint64_t> chunk0;
 
     void reset() {
         used = 0;
@@ -74,8 +80,26 @@ struct Batch {
         verified = false;
         bad_pkt = -1;
         dpkt = doff = 0;
+        dense = sealed = false;
+        d0 = words_used = data_used = 0;
+        chunk0.clear();
     }
 };
+
+// Chunk sizes the contiguous round kernels take (launch_chunks): 512 ... 4096, and R x 4096 (the
+// multi-round kernel / pieces + combine). Others keep the wire layout and the chunk-per-lane kernel.
+bool dense_bpc(uint32_t bpc) {
+    return bpc == 512 || bpc == 1024 || bpc == 2048 || bpc == 4096 || (bpc > 4096 && bpc % 4096 == 0);
+}
+
+// HDFS3_READER_LAYOUT=wire keeps every batch in the wire layout (A/B measurement knob)
+bool wire_layout_forced() {
+    static const bool f = [] {
+        const char *e = getenv("HDFS3_READER_LAYOUT");
+        return e && std::strcmp(e, "wire") == 0;
+    }();
+    return f;
+}
 
 uint64_t now_ns() {
     return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -262,6 +286,51 @@ struct hdfs3_block_reader {
             if (int64_t(h.packet_len) != 4 + int64_t(h.data_len) + int64_t(crc_len))
                 return rx_fail(-EIO, "Invalid Packet, packetLen does not match dataLen and checksums");
             const uint64_t size = crc_len + uint64_t(h.data_len);
+            if (b.pk.empty())
+                b.dense = verify && checksum_size == 4 && dense_bpc(chunk_size) && !wire_layout_forced();
+            if (b.dense) {
+                // Dense layout (round 5): the socket's [words][data] of each packet land in two places,
+                // the words after the batch's earlier words, the data after its earlier data. While every
+                // packet but the last holds whole chunks, the batch is then ONE contiguous block with its
+                // own .meta-style word array, and the GPU verifies it with the contiguous round kernel
+                // (launch()): no packet pitch, no 4 KiB rounds straddling packets. Same bytes on the
+                // wire, same delivery (PacketRef), same ChecksumException semantics.
+                if (b.pk.empty()) {  // geometry from the batch's first packet
+                    b.d0 = (uint64_t(batch_packets) * crc_len + 4095) & ~uint64_t(4095);
+                    const uint64_t need = b.d0 + uint64_t(batch_packets) * uint64_t(h.data_len);
+                    if (need > b.a.cap)
+                        if (int rc = grow(b.a, need, size_t(batch_packets))) return rx_fail(rc, "arena growth failed");
+                } else if (b.sealed || b.words_used + crc_len > b.d0 ||
+                           b.d0 + b.data_used + uint64_t(h.data_len) > b.a.cap) {
+                    pending_hdr = h;  // close this batch; the header opens the next
+                    have_pending_hdr = true;
+                    break;
+                }
+                if (int rc = net::read_fully(fd, b.a.h + b.words_used, crc_len, timeout_ms))
+                    return rx_fail(rc, "RemoteBlockReader: failed to read packet checksums");
+                if (int rc = net::read_fully(fd, b.a.h + b.d0 + b.data_used, h.data_len, timeout_ms))
+                    return rx_fail(rc, "RemoteBlockReader: failed to read packet payload");
+                last_seqno = h.seqno;
+                packets.fetch_add(1, std::memory_order_relaxed);
+                int64_t ahead = recv_cursor - h.offset_in_block;
+                ahead = ahead > 0 ? ahead : 0;
+                const int64_t useful =
+                    std::max<int64_t>(0, std::min<int64_t>(h.data_len - ahead, end_offset - recv_cursor));
+                b.pk.push_back(PacketRef{b.d0 + b.data_used, b.words_used, uint32_t(h.data_len), uint32_t(ahead),
+                                         uint32_t(useful)});
+                b.chunk0.push_back(b.words_used / 4);
+                b.words_used += crc_len;
+                b.data_used += uint64_t(h.data_len);
+                b.used = b.d0 + b.data_used;
+                if (h.data_len % chunk_size) b.sealed = true;  // a short chunk ends the contiguous chunk run
+                const int64_t reached = recv_cursor + h.data_len - ahead;
+                recv_cursor = reached;
+                if (reached >= end_offset) {
+                    if (int rc = read_trailer()) return rc;
+                    range_done = true;
+                }
+                continue;
+            }
             uint64_t off = ((b.used + crc_len + 15) & ~uint64_t(15)) - crc_len;
             if (off + size > b.a.cap) {
                 if (!b.pk.empty()) {  // close this batch; the header opens the next
@@ -284,15 +353,20 @@ struct hdfs3_block_reader {
             const int64_t reached = recv_cursor + h.data_len - ahead;
             recv_cursor = reached;
             if (reached >= end_offset) {
-                // readTrailingEmptyPacket (:279-287): the datanode follows with an empty last packet
-                wire::PacketHeader t;
-                if (int rc = read_header(t)) return rc;
-                if (t.last_packet_in_block && t.data_len == 0) {
-                    last_seqno = t.seqno;
-                    trailer_ok = true;
-                }
+                if (int rc = read_trailer()) return rc;
                 range_done = true;
             }
+        }
+        return 0;
+    }
+
+    // readTrailingEmptyPacket (:279-287): the datanode follows the range with an empty last packet
+    int read_trailer() {
+        wire::PacketHeader t;
+        if (int rc = read_header(t)) return rc;
+        if (t.last_packet_in_block && t.data_len == 0) {
+            last_seqno = t.seqno;
+            trailer_ok = true;
         }
         return 0;
     }
@@ -304,13 +378,29 @@ struct hdfs3_block_reader {
             b.verified = true;
             return 0;
         }
-        std::vector<DevPacket> hp(b.pk.size());
-        for (size_t i = 0; i < b.pk.size(); ++i) hp[i] = DevPacket{b.pk[i].data_off, b.pk[i].crc_off, b.pk[i].data_len, 0};
+        const uint32_t *fold = ctx->d_fold_by[tables == ctx->d_tables_by[1]];
         HIP_OK(hipMemcpyAsync(b.a.d, b.a.h, b.used, hipMemcpyHostToDevice, ctx->stream));
         HIP_OK(hipMemsetAsync(b.a.d_res, 0, sizeof(unsigned long long), ctx->stream));
-        HIP_OK(launch_packet_batch(b.a.d, hp.data(), hp.size(), chunk_size, true, /*check_short_tail=*/0, b.a.d_res,
-                                   b.a.h_desc, b.a.d_desc, tables, ctx->d_fold_by[tables == ctx->d_tables_by[1]],
-                                   ctx->grid_cap, ctx->stream));
+        if (b.dense) {
+            // one contiguous block of b.data_used bytes and its word array: the contiguous round kernel
+            // (bpc <= 4096), the multi-round kernel or pieces + combine (R x 4096, on the batch's own
+            // piece scratch); keys are the batch's chunk indices (wait() maps them to packets)
+            ChunkLaunch a{};
+            a.data = b.a.d + b.d0;
+            a.len = b.data_used;
+            a.bpc = chunk_size;
+            a.crc_be = b.a.d;
+            a.result = b.a.d_res;
+            a.check_short_tail = 0;  // verifyChecksum ignores a short chunk's mismatch (:319)
+            HIP_OK(launch_chunks(a, true, tables, fold, ctx->grid_cap, ctx->stream, &b.a.pieces));
+        } else {
+            std::vector<DevPacket> hp(b.pk.size());
+            for (size_t i = 0; i < b.pk.size(); ++i)
+                hp[i] = DevPacket{b.pk[i].data_off, b.pk[i].crc_off, b.pk[i].data_len, 0};
+            HIP_OK(launch_packet_batch(b.a.d, hp.data(), hp.size(), chunk_size, true, /*check_short_tail=*/0, b.a.d_res,
+                                       b.a.h_desc, b.a.d_desc, tables, fold, ctx->grid_cap, ctx->stream, 0, nullptr,
+                                       false, nullptr, &b.a.pieces));
+        }
         ++ctx->launches;
         HIP_OK(hipMemcpyAsync(b.a.h_res, b.a.d_res, sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
         HIP_OK(hipEventRecord(b.a.done, ctx->stream));
@@ -385,7 +475,12 @@ struct hdfs3_block_reader {
         Timer tm(t_ns[3]);
         HIP_OK(hipEventSynchronize(b.a.done));
         const unsigned long long r = *b.a.h_res;
-        if (r) b.bad_pkt = int64_t((~r) >> 32);
+        if (r && b.dense) {  // the first bad chunk of the batch -> its packet
+            const uint64_t chunk = ~r;
+            b.bad_pkt = int64_t(std::upper_bound(b.chunk0.begin(), b.chunk0.end(), chunk) - b.chunk0.begin()) - 1;
+        } else if (r) {
+            b.bad_pkt = int64_t((~r) >> 32);
+        }
         b.verified = true;
         return 0;
     }

@@ -86,6 +86,9 @@ struct FileEntry {
     BlockTable pipeline_blocks;  // hdfs3_fs_set_pipeline: the blocks addBlock would allocate
     bool pipeline = false;
     uint64_t append_gs = 0;      // hdfs3_fs_set_append_stamp (0: the last block's stamp + 1)
+    // FileStatus::getBlockSize (hdfs3_fs_set_block_size, or the size a write through this table used;
+    // 0: unknown, then a file of two or more blocks states it by its first block)
+    int64_t block_size = 0;
 };
 
 }  // namespace
@@ -108,6 +111,7 @@ struct HdfsFileInternalWrapper {
     BlockTable written;              // the pipeline's blocks, for completeFile
     BlockTable prefix;               // append: the file's blocks before the pipeline's first one
     std::string path;
+    int64_t block_size = 0;          // the write's block size (the file's, for FileStatus)
 };
 
 extern "C" {
@@ -159,6 +163,13 @@ int hdfs3_fs_set_pipeline(hdfsFS fs, const char *path, const hdfs3_located_block
     FileEntry &slot = fs->files[path];
     slot.pipeline_blocks = t;
     slot.pipeline = true;
+    return 0;
+}
+
+int hdfs3_fs_set_block_size(hdfsFS fs, const char *path, int64_t block_size) {
+    PARAMETER_ASSERT(fs && path && std::strlen(path) > 0 && block_size > 0, -1, EINVAL);
+    std::lock_guard<std::mutex> lk(fs->mu);
+    fs->files[path].block_size = block_size;
     return 0;
 }
 
@@ -231,12 +242,14 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
             if (blocksize > 0) o.block_size = blocksize;
             if (append) {
                 // the reference appends with the file's own block size (FileStatus::getBlockSize,
-                // OutputStreamImpl.cpp:196-230): every block but the last is full, so a file of two
-                // or more blocks states it; a caller's size that disagrees is refused, and no
-                // registered block may hold more than the size the stream will use
+                // OutputStreamImpl.cpp:196-230): the size registered for the path (hdfs3_fs_set_block_size,
+                // or recorded by the write that created it), else a file of two or more blocks states
+                // it by its first (every block but the last is full); a caller's size that disagrees is
+                // refused, and no registered block may hold more than the size the stream will use.
+                // A one-block file of unknown block size appends with the caller's (or the session's).
                 const auto &lbs = e.located_blocks.blocks;
-                if (lbs.size() >= 2) {
-                    const int64_t fbs = int64_t(lbs[0].block.num_bytes);
+                if (e.block_size > 0 || lbs.size() >= 2) {
+                    const int64_t fbs = e.block_size > 0 ? e.block_size : int64_t(lbs[0].block.num_bytes);
                     if (blocksize > 0 && blocksize != fbs) {
                         delete file;
                         set_msg("append: block size differs from the file's block size");
@@ -289,6 +302,7 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
             }
             if (e.pipeline || (last && !e.sink)) {  // datanodes: PipelineImpl behind the stream
                 file->path = path;
+                file->block_size = o.block_size;
                 BlockTable t;
                 std::vector<hdfs3_located_block> pb;
                 if (last) pb.push_back(*last);  // its replicas are the append pipeline's nodes
@@ -360,6 +374,7 @@ void complete_written_file(hdfsFS fs, hdfsFile file) {
     FileEntry &slot = fs->files[file->path];
     slot.located_blocks.assign(all.data(), int(all.size()));
     slot.located = true;
+    slot.block_size = file->block_size;  // what FileStatus reports for the file from now on
 }
 }  // namespace
 

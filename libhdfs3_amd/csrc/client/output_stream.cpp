@@ -165,8 +165,10 @@ struct hdfs3_output_stream {
         b.chunks = chunks;
         if (n) {
             HIP_OK(hipMemcpyAsync(b.a.d + lo, b.a.h + lo, hi - lo, hipMemcpyHostToDevice, ctx->stream));
+            // the batch's own piece scratch (bpc = R x 4096 batches of whole-round packets: pieces + combine)
             HIP_OK(launch_packet_batch(b.a.d, hp, n, bpc, false, 0, nullptr, b.a.h_desc, b.a.d_desc, ctx->d_tables,
-                                       ctx->d_fold, ctx->grid_cap, ctx->stream));
+                                       ctx->d_fold, ctx->grid_cap, ctx->stream, 0, nullptr, false, nullptr,
+                                       &b.a.pieces));
             ++ctx->launches;
             HIP_OK(hipMemcpyAsync(b.a.h + crc_region, b.a.d + crc_region, 4 * chunks, hipMemcpyDeviceToHost,
                                   ctx->stream));

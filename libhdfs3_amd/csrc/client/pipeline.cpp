@@ -115,6 +115,10 @@ struct hdfs3_pipeline {
         req.block.num_bytes = t.append ? uint64_t(t.base) : 0;  // lastBlock->getNumBytes()
         req.client_name = client_name;
         for (size_t i = 1; i < t.nodes.size(); ++i) {
+            // BuildNodeInfo (DataTransferProtocolSender.cpp:80-90) from the namenode's DatanodeInfo; an
+            // hdfs3_datanode carries the transfer address only, so the uuid, info/ipc ports and the rack
+            // (location, field 8) go out empty/zero: the bytes equal the reference's for a node whose
+            // namenode record has no rack (the codec itself is pinned with racks, tests/test_wire_protobuf.py)
             wire::DatanodeAddr d;
             d.ip_addr = d.host_name = t.nodes[i].first;
             d.xfer_port = uint32_t(t.nodes[i].second);

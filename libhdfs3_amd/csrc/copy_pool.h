@@ -24,13 +24,20 @@
 #include <mutex>
 #include <thread>
 
+#if defined(__x86_64__) || defined(__i386__)
 #include <immintrin.h>
+#define HDFS3_COPY_NT_AVAILABLE 1
+#else
+#define HDFS3_COPY_NT_AVAILABLE 0
+#endif
 
 namespace hdfs3crc {
 
 // Copies with streaming (non-temporal) stores: the destination lines are written without being read
 // first, so a DRAM-bound copy moves 2 bytes per byte instead of 3 (round 4 measurement knob,
-// HDFS3_COPY_NT=1; the default is memcpy). Destination aligned to 32 B, 128 B per iteration.
+// HDFS3_COPY_NT=1; the default is memcpy). Destination aligned to 32 B, 128 B per iteration. x86 only:
+// elsewhere the knob is ignored and every copy is memcpy.
+#if HDFS3_COPY_NT_AVAILABLE
 __attribute__((target("avx2"))) inline void memcpy_stream(uint8_t *dst, const uint8_t *src, size_t n) {
     size_t head = (32 - (reinterpret_cast<uintptr_t>(dst) & 31)) & 31;
     if (head > n) head = n;
@@ -52,6 +59,9 @@ __attribute__((target("avx2"))) inline void memcpy_stream(uint8_t *dst, const ui
     std::memcpy(dst + i, src + i, n - i);
     _mm_sfence();  // the streaming stores are weakly ordered: visible before the piece is reported done
 }
+#else
+inline void memcpy_stream(uint8_t *dst, const uint8_t *src, size_t n) { std::memcpy(dst, src, n); }
+#endif
 
 inline int pread_fully(int fd, void *buf, size_t n, int64_t off) {
     uint8_t *p = static_cast<uint8_t *>(buf);
@@ -154,7 +164,9 @@ class CopyPool {
     }
     CopyPool() {
         if (const char *e = getenv("HDFS3_COPY_HELPERS")) helpers_ = size_t(std::min(std::max(atoi(e), 0), 15));
+#if HDFS3_COPY_NT_AVAILABLE
         if (const char *e = getenv("HDFS3_COPY_NT")) nt_ = e[0] == '1' && __builtin_cpu_supports("avx2");
+#endif
         for (size_t i = 0; i < helpers_; ++i)
             std::thread([this] {
                 for (;;) {

@@ -527,6 +527,13 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
     // (the last may be shorter) -> the kernel derives every descriptor (SegLaunch::stride)
     const uint64_t pitch = n > 1 ? h_pk[1].data_off - h_pk[0].data_off : 0;
     bool strided = n > 1 && g_variant != 52 && pitch > 0 && pitch == h_pk[1].crc_off - h_pk[0].crc_off;
+    // the same with the words at a pitch of their own (round 5: the output stream's batches, whose
+    // words are dense at 4 x chunks per packet while the data sits in packet slots): the pitch walk
+    // with ChunkLaunch::crc_pitch, so writer packets of whole rounds (bpc 1024 ... 65536: 64 KiB of
+    // data) take the round kernel, and at bpc = R x 4096 its pieces + combine, instead of the
+    // descriptor-array segmented kernel or (above 4 KiB) the chunk-per-lane packet kernel
+    const uint64_t cpitch = n > 1 ? h_pk[1].crc_off - h_pk[0].crc_off : 0;
+    bool dstrided = n > 1 && g_variant != 52 && pitch > 0 && h_pk[1].crc_off > h_pk[0].crc_off && (cpitch & 3) == 0;
     for (size_t i = 0; i < n; ++i) {
         if (bad_index) {  // bounds, fused into this pass (the API's only pass over pk[])
             const hdfs3crc::DevPacket &d = h_pk[i];
@@ -547,10 +554,13 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         strided = strided && h_pk[i].data_off == h_pk[0].data_off + i * pitch &&
                   h_pk[i].crc_off == h_pk[0].crc_off + i * pitch &&
                   (i + 1 == n || h_pk[i].data_len == h_pk[0].data_len);
+        dstrided = dstrided && h_pk[i].data_off == h_pk[0].data_off + i * pitch &&
+                   h_pk[i].crc_off == h_pk[0].crc_off + i * cpitch &&
+                   (i + 1 == n || h_pk[i].data_len == h_pk[0].data_len);
         units += u;
     }
     uint32_t upp_log2 = 0;
-    if (aligned && strided && n > 1 &&
+    if (aligned && (strided || dstrided) && n > 1 &&
         packet_stream_ok(h_pk[0].data_len, h_pk[n - 1].data_len, n, bpc, d_arena + h_pk[0].data_off,
                          d_arena + h_pk[0].crc_off, pitch, &upp_log2)) {
         ChunkLaunch a{};
@@ -561,6 +571,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         a.result = result;
         a.check_short_tail = check_short_tail;
         a.pitch = pitch;
+        a.crc_pitch = strided ? 0 : cpitch;
         a.npk = n;
         a.upp_log2 = upp_log2;
         a.last_len = h_pk[n - 1].data_len;

@@ -55,8 +55,13 @@ struct PacketArena {
     size_t desc_cap = 0;
     unsigned long long *d_res = nullptr, *h_res = nullptr;
     hipEvent_t done = nullptr;
+    // 4096-byte piece CRCs of a batch at bpc = R x 4096 (launch_chunks' pieces + combine): the
+    // batch's own, so two readers verifying on one ctx (a stream's sequential reader and a pread's)
+    // never share it (round 5; the ctx's scratch is for the calls of the ctx's own thread)
+    PieceScratch pieces;
 
     void release() {
+        pieces.release();
         if (h) (void)hipHostFree(h);
         if (d) (void)hipFree(d);
         if (h_desc) (void)hipHostFree(h_desc);

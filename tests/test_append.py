@@ -368,3 +368,44 @@ def test_gpu_hdfs_second_append_without_new_stamp_or_pipeline(nodes):
         assert not f and ctypes.get_errno() == errno.EINVAL
     finally:
         h.close()
+
+
+@pytest.mark.gpu
+def test_gpu_hdfs_append_one_block_file_uses_its_own_block_size(nodes):
+    """ADVICE r4 (low): FileStatus::getBlockSize decides where an append continues
+    (OutputStreamImpl.cpp:196-230). A one-block file written with a 512 KiB block size (the session's
+    is 1 MiB) that filled its block: a clean close records its block size, so the append opens a new
+    block (the registered pipeline's) instead of continuing the full block past 512 KiB; a caller
+    size that disagrees is refused; hdfs3_fs_set_block_size states it for a registered file."""
+    import errno
+
+    h = Hdfs()
+    try:
+        chain = [(HOST, d.port) for d in nodes]
+        path = b"/append/one-block"
+        half = BS // 2
+        first = splitmix_bytes(half, 61)
+        h.set_pipeline(path, [(870, chain)])
+        f = h.lib.hdfsOpenFile(h.fs, path, os.O_WRONLY | os.O_CREAT, 0, 0, half)
+        assert f, h.lib.hdfsGetLastError()
+        assert h.lib.hdfsWrite(h.fs, f, first.ctypes.data, first.nbytes) == first.nbytes
+        assert h.lib.hdfsCloseFile(h.fs, f) == 0, h.lib.hdfsGetLastError()
+        # the caller's 1 MiB disagrees with the file's 512 KiB
+        h.set_pipeline(path, [(871, chain)])
+        f = h.lib.hdfsOpenFile(h.fs, path, os.O_WRONLY | os.O_APPEND, 0, 0, BS)
+        assert not f and ctypes.get_errno() == errno.EINVAL
+        more = splitmix_bytes(1000, 62)
+        assert h.write_file(path, os.O_WRONLY | os.O_APPEND, [more]) == first.size
+        assert all(d.get_block(870)[0].size == half for d in nodes)  # the full block stays full
+        got = nodes[-1].get_block(871)
+        assert got is not None and np.array_equal(got[0], more)
+        assert np.array_equal(h.read_file(path, half + more.size), np.concatenate([first, more]))
+        # a registered (not written) one-block file: its block size comes from hdfs3_fs_set_block_size
+        path2 = b"/append/registered"
+        assert h.lib.hdfs3_fs_set_block_size(h.fs, path2, 0) == -1 and ctypes.get_errno() == errno.EINVAL
+        h.add_file(path2, [(870, half, chain)])
+        assert h.lib.hdfs3_fs_set_block_size(h.fs, path2, half) == 0
+        f = h.lib.hdfsOpenFile(h.fs, path2, os.O_WRONLY | os.O_APPEND, 0, 0, BS)
+        assert not f and ctypes.get_errno() == errno.EINVAL
+    finally:
+        h.close()

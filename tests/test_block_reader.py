@@ -174,3 +174,93 @@ def test_datanode_drop_mid_block_is_an_io_error(dn):
             assert pos <= 1 << 20 and np.array_equal(out[:pos], data[:pos])
     finally:
         node.stop()
+
+
+@pytest.mark.parametrize("bpc", [512, 4096, 8192, 12288, 16384, 65536])
+def test_dense_batches_every_chunk_size(dn, bpc):
+    """Round 5: batches land densely (the packets' words back to back, their data back to back from a
+    4 KiB boundary) and verify as ONE contiguous block: the round kernel at 512 / 4096, the
+    multi-round kernel at 8192 / 16384 / 65536, pieces + combine at 12288 (on the batch's own piece
+    scratch). A whole block and a ranged read deliver the block's bytes; a flipped bit in the first,
+    a middle and the last packet raises ChecksumException after EXACTLY the packets before it were
+    delivered (RemoteBlockReader.cpp:306-326); a short tail's mismatch is ignored (:319)."""
+    from libhdfs3_amd.engine import BlockReader
+    from libhdfs3_amd._native import Hdfs3CrcError
+
+    lb, port, add = dn
+    per = max(bpc, 65536 // bpc * bpc)  # the loopback datanode's data bytes per packet
+    n = 40 * per + bpc // 2 + 100  # 41 packets, the last one short with a short tail chunk
+    data = splitmix_bytes(n, 5100 + bpc)
+    bid = 50_000 + bpc
+    crc = add(bid, data, bpc)
+    out, st = _read(port, bid, 0, n, batch_packets=16)
+    assert np.array_equal(out, data) and st["bytes_per_checksum"] == bpc and st["gpu_batches"] == 3
+    start = 3 * per + 17
+    out, _ = _read(port, bid, start, 20 * per, batch_packets=7)
+    assert np.array_equal(out, data[start:start + 20 * per])
+    tail = crc.copy()
+    tail[-4] ^= 0x5A  # the short tail chunk's word: ignored by remote semantics
+    add(bid + 1, data, bpc, crc=tail)
+    out, _ = _read(port, bid + 1, 0, n, batch_packets=16)
+    assert np.array_equal(out, data)
+    for k, p in enumerate((0, 21, 39)):
+        bad = data.copy()
+        q = p * per + (per * 2) // 3
+        bad[q] ^= 0x40
+        add(bid + 2 + k, bad, bpc, crc=crc)
+        with BlockReader("127.0.0.1", port, bid + 2 + k, 0, n, batch_packets=16) as r:
+            got = np.zeros(n, np.uint8)
+            pos = 0
+            with pytest.raises(Hdfs3CrcError) as ei:
+                while True:
+                    g = r.read_into(got, pos, min(1 << 20, n - pos))
+                    assert g > 0
+                    pos += g
+            assert ei.value.rc == -errno.EIO and "ChecksumException" in str(ei.value)
+        assert pos == p * per, (p, pos)
+        assert np.array_equal(got[:pos], data[:pos])
+
+
+_WIRE_CHILD = r"""
+import sys
+import numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/tests"]
+from loopback import LoopbackDatanode
+from util import oracle_compute, splitmix_bytes
+from libhdfs3_amd.engine import BlockReader
+dn = LoopbackDatanode()
+try:
+    for bpc in (512, 4096, 8192):
+        data = splitmix_bytes((6 << 20) + 333, bpc)
+        crc = oracle_compute(data, bpc)
+        dn.add_block(bpc, data, crc, bpc)
+        with BlockReader("127.0.0.1", dn.port, bpc, 0, data.nbytes, batch_packets=16) as r:
+            assert np.array_equal(r.read_all(data.nbytes), data)
+        bad = data.copy()
+        bad[(5 << 20) + 9] ^= 1
+        dn.add_block(bpc + 1, bad, crc, bpc)
+        try:
+            with BlockReader("127.0.0.1", dn.port, bpc + 1, 0, data.nbytes, batch_packets=16) as r:
+                r.read_all(data.nbytes)
+            print("NO EXCEPTION", bpc)
+        except Exception as e:
+            assert "ChecksumException" in str(e), e
+        print("ok", bpc)
+finally:
+    dn.stop()
+"""
+
+
+def test_wire_layout_knob_keeps_the_packet_kernels():
+    """HDFS3_READER_LAYOUT=wire (read once per process: a child) keeps the round-4 wire layout and
+    its packet kernels (pitch walk / segmented / chunk-per-lane): same bytes and the same exception."""
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HDFS3_READER_LAYOUT="wire")
+    out = subprocess.run([sys.executable, "-c", _WIRE_CHILD, repo], env=env, capture_output=True, text=True,
+                         timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split() == ["ok", "512", "ok", "4096", "ok", "8192"], out.stdout

@@ -188,7 +188,7 @@ def test_overlapped_chain_chunks_above_4k_pieces(gpu_ctx, bpc):
     n, plen = 96, 65536
     arenas, streams, hosts = [], [], []
     for a in range(5):
-        last = plen if a != 3 else bpc * 2 + 300
+        last = plen if a != 3 else (bpc * 2 + 300 if bpc * 2 + 300 < plen else plen - 300)
         host, pitch, crc_off, data_off, datas = build_arena(n, plen, last, bpc, 7000 + 131 * a + bpc % 1013)
         hosts.append((host, pitch, crc_off, data_off, datas))
         arenas.append(gpu_ctx.upload(host))

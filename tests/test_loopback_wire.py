@@ -92,3 +92,40 @@ def test_status_reaches_datanode(datanode):
     c.send_status(6)
     c.close()
     assert lb.last_status(wait_for=6) == 6  # DT_PROTO_CHECKSUM_OK
+
+
+@pytest.mark.parametrize("engine", ["reference", "hw", "pcl"])
+@pytest.mark.parametrize("bpc", [512, 4096, 513])
+def test_reference_read_loop_baseline(datanode, engine, bpc):
+    """bench.py's config-5 CPU baseline (tests/loopback.reference_read_block over oracle/remote_loop.h):
+    RemoteBlockReader's receive -> verifyChecksum -> copy loop on one thread, with the reference's own
+    HWCrc32c (oracle/_ref) or the restated engines. Clean blocks arrive byte for byte with CHECKSUM_OK
+    sent; a flipped bit stops it at its packet (ChecksumException); verify off delivers the bytes as
+    they came; a short tail's mismatch is ignored (RemoteBlockReader.cpp:319)."""
+    from loopback import reference_read_block
+    from util import ref_lib
+
+    if engine == "reference" and ref_lib() is None:
+        pytest.skip("oracle/_ref was not built (no /root/reference here)")
+    dn, port, add = datanode
+    n = (3 << 20) + 777
+    data = splitmix_bytes(n, 900 + bpc)
+    bid = 80_000 + bpc * 10 + ["reference", "hw", "pcl"].index(engine)
+    crc = add(bid, data, bpc)
+    out = np.zeros(n, np.uint8)
+    assert reference_read_block(port, bid, n, out, engine=engine) == n
+    assert np.array_equal(out, data)
+    assert dn.last_status(wait_for=6) == 6
+    per = max(bpc, 65536 // bpc * bpc)
+    bad = data.copy()
+    bad[20 * per + 5] ^= 0x08
+    add(bid + 100_000, bad, bpc, crc=crc)
+    with pytest.raises(OSError, match=r"ChecksumException: block \d+ packet 20"):
+        reference_read_block(port, bid + 100_000, n, out, engine=engine)
+    out[:] = 0
+    assert reference_read_block(port, bid + 100_000, n, out, verify=False, engine=engine) == n
+    assert np.array_equal(out, bad)
+    tail = crc.copy()
+    tail[-4] ^= 0xFF
+    add(bid + 200_000, data, bpc, crc=tail)
+    assert reference_read_block(port, bid + 200_000, n, out, engine=engine) == n

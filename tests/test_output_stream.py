@@ -67,6 +67,11 @@ def random_ops(rng, total, flush_p=0.1):
     (4096, 65536, 2 << 20, 64),
     (2048, 4096, 256 << 10, 1),      # one chunk-ish per packet, one packet per GPU batch
     (100, 1000, 100 * 37, 5),        # odd chunk size, ragged everything
+    (1024, 65536, 4 << 20, 64),      # round 5: whole-round writer packets, words at their own pitch
+    (8192, 65536, 4 << 20, 64),      # ... and chunks above 4 KiB: pieces + combine
+    (16384, 65536, 8 << 20, 16),
+    (65536, 65536, 4 << 20, 64),
+    (12288, 65536, 3 << 20, 8),      # 6 chunks = 18 rounds per packet: not a pitch stream
 ])
 def test_packets_identical_to_reference_model(bpc, packet_size, block_size, batch):
     rng = random.Random(bpc * 7 + batch)
@@ -218,3 +223,20 @@ def test_append_to_full_last_block_is_eio():
     with pytest.raises(Hdfs3CrcError) as ei:
         OutputStream(append=(2 * BS, BS), block_size=BS)
     assert ei.value.rc == -errno.EIO
+
+
+@pytest.mark.parametrize("bpc", [1024, 4096, 8192, 16384, 65536])
+def test_long_writes_whole_batches_above_512(bpc):
+    """Round 5: long writes with rare flushes, so that most GPU batches are full batches of 64 KiB
+    writer packets at one data pitch with their words dense (the pitch walk with its own word pitch;
+    at bpc = R x 4096 the 4096-byte piece CRCs and the packet-mode combine): every packet identical to
+    the reference model, the empty last packet of each block and the flushes in the middle included."""
+    rng = random.Random(bpc)
+    data = splitmix_bytes(24 << 20, 77 + bpc)
+    ops = random_ops(rng, data.nbytes, flush_p=0.004)
+    want, got = run_both(ops, data, bytes_per_checksum=bpc, packet_size=65536, block_size=8 << 20,
+                         batch_packets=32)
+    assert len(got) == len(want)
+    for i, ((gp, gi), (wp, wi)) in enumerate(zip(got, want)):
+        assert gi == wi, (i, gi, wi)
+        assert gp == wp, i

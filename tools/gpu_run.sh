@@ -13,7 +13,7 @@
 #   bench            python bench.py (the default line: K = 2000)
 #   bench_k20        the driver's command: python3 bench.py --gpus 1 --steps 20 --warmup 5
 #   prof             rocprofv3 --kernel-trace --stats of the driver's command (PMC and CPU legs off)
-#   tool:<script>    python tools/<script> (extra args after a comma: tool:e2e_read.py,--reps,5)
+#   tool:<script>    python tools/<script> (extra args after '@': tool:ab.py@--variants@0,154@--overlap)
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -34,7 +34,9 @@ run() {  # run <seconds> <outfile> <cmd...>
     fi
 }
 
+i=0
 for step in "$@"; do
+    i=$((i + 1))
     echo "== $step ($(date +%T))"
     case "$step" in
     tests) run 900 gpurun_out/${TAG}_gpu_tests.txt $PYT tests; tail -3 gpurun_out/${TAG}_gpu_tests.txt ;;
@@ -52,7 +54,7 @@ for step in "$@"; do
               -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-pmc --no-cpu-baseline \
               --out-json gpurun_out/${TAG}_prof_bench.json
           cat gpurun_out/${TAG}_prof_bench.json ;;
-    tool:*) t=${step#tool:}; IFS=, read -r -a parts <<< "$t"; n=$(basename "${parts[0]}" .py)
+    tool:*) t=${step#tool:}; IFS=@ read -r -a parts <<< "$t"; n=$(basename "${parts[0]}" .py)_$i
             run 600 gpurun_out/${TAG}_${n}.jsonl python -u tools/"${parts[0]}" "${parts[@]:1}"; tail -30 gpurun_out/${TAG}_${n}.jsonl ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
