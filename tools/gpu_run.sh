@@ -14,6 +14,7 @@
 #   bench_k20        the driver's command: python3 bench.py --gpus 1 --steps 20 --warmup 5
 #   prof             rocprofv3 --kernel-trace --stats of the driver's command (PMC and CPU legs off)
 #   tool:<script>    python tools/<script> (extra args after '@': tool:ab.py@--variants@0,154@--overlap)
+#   rprof:<script>   the same under rocprofv3 --kernel-trace --stats (csv in gpurun_out/<tag>_<script>_<i>/)
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -56,6 +57,10 @@ for step in "$@"; do
           cat gpurun_out/${TAG}_prof_bench.json ;;
     tool:*) t=${step#tool:}; IFS=@ read -r -a parts <<< "$t"; n=$(basename "${parts[0]}" .py)_$i
             run 600 gpurun_out/${TAG}_${n}.jsonl python -u tools/"${parts[0]}" "${parts[@]:1}"; tail -30 gpurun_out/${TAG}_${n}.jsonl ;;
+    rprof:*) t=${step#rprof:}; IFS=@ read -r -a parts <<< "$t"; n=$(basename "${parts[0]}" .py)_$i
+              run 600 gpurun_out/${TAG}_${n}.txt rocprofv3 --kernel-trace --stats --output-format csv \
+                  -d gpurun_out/${TAG}_${n} -o run -- python3 -u tools/"${parts[0]}" "${parts[@]:1}"
+              tail -5 gpurun_out/${TAG}_${n}.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
