@@ -44,8 +44,6 @@ constexpr int kLabClock = 4096;     // clock stamps of workgroup 0 (LabClock, cr
 constexpr int kLabStorePlain = 8192;  // compute, staged words: plain global stores (production before round 4)
 constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every launch size (production before round 4)
 constexpr int kLabNoTabLoad = 2097152;  // diagnostic: the table images are not loaded (made up from t: wrong results)
-constexpr int kLabStageQ = 4194304;  // compute at bpc 512, one staging window: each wave quartile's lines written by
-                                      // its last wave (an LDS counter per quartile), no end-of-workgroup barrier
 constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = fill done | first data << 21 | kernel
                                      // arguments landed << 42, each - start, 21 bits of 10 ns
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
@@ -266,13 +264,6 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             dst[0] = n0[f];
             dst[1] = n1[f];
         }
-    }
-    // kLabStageQ: the 4 quartile counters live in the staging area's last 4 words (round kSR - 1 of
-    // slot 15), which a launch whose waves have fewer than kSR rounds never stages
-    constexpr bool kStageQ = !VERIFY && (LAB & kStageWords) != 0 && (LAB & kLabStageQ) != 0 && BPC == 512 &&
-                             Walk::kContiguous && TPB == 1024;
-    if constexpr (kStageQ) {
-        if (threadIdx.x < 4) lds[kLdsBytesWave / 4 - 4 + threadIdx.x] = 0;
     }
     lds_barrier();
     if constexpr ((LAB & kLabMid) != 0) lab_mid[0] = __builtin_amdgcn_s_memrealtime();
@@ -566,41 +557,6 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             step(a0, a1, b0, b1, k);
             if (k + 2 >= nr) break;
             step(b0, b1, a0, a1, k + 2);
-        }
-    }
-    if constexpr (kStageQ) {
-        // lab (kLabStageQ): with one window (every wave < kSR rounds), slots 4q .. 4q + 3 hold round k's words
-        // of 4 consecutive units = one 128-byte line per k. Each wave counts itself out of its quartile; the
-        // quartile's last wave writes the quartile's lines (16 B per lane, 8 lines per store), and no wave
-        // waits for the workgroup: the quartiles that finish first (the SIMD arbiter's oldest waves) write
-        // while the others still read, and the workgroup's end carries one quartile's lines, not four.
-        const uint32_t ks_max = walk.kq + (walk.kr ? 1u : 0u);
-        if (ks_max < kSR) {
-            uint32_t *ctr = lds + kLdsBytesWave / 4 - 4;
-            const uint32_t q = slot >> 2;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's staged words, before its count
-            uint32_t old = 0;
-            if (lane == 0) old = __hip_atomic_fetch_add(ctr + q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            old = __builtin_amdgcn_readfirstlane(old);
-            if (old == 3) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                const uint64_t wg_first = walk.first - slot;
-                const uint32_t o = lane & 7, s = 4 * q + (o >> 1);
-                const uint32_t ks = walk.kq + (wg_first + s < walk.kr ? 1u : 0u);
-                const uint64_t wb = rfl64(reinterpret_cast<uint64_t>(walk.words));
-                const __amdgpu_buffer_rsrc_t rs =
-                    __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(wb), 0, 0x7FFFFFFF, 0x00020000);
-                for (uint32_t k0 = 0; k0 < ks_max; k0 += 8) {
-                    const uint32_t k = k0 + (lane >> 3);
-                    if (k < ks) {
-                        const uint32_t *src = stage + (k * 16 + 4 * q) * kCpw + 4 * o;
-                        const u32x4 v = {src[0], src[1], src[2], src[3]};
-                        const uint64_t off = 4 * kCpw * (wg_first + 4 * q + uint64_t(k) * walk.stride) + 16 * o;
-                        __builtin_amdgcn_raw_buffer_store_b128(v, rs, uint32_t(off), 0, 1 | 2 | 16);
-                    }
-                }
-            }
-            return;
         }
     }
     if constexpr (kStage) {

@@ -255,6 +255,10 @@ int packets_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len, 
     HIP_TRY(e);
     ++ctx->launches;
     HIP_TRY(hipEventRecord(st->done, ctx->stream));
+    // the launch may have copied its descriptors out of st->h asynchronously (the segmented kernel's
+    // array, the chunk-per-lane kernel's DevPackets): the slot is reused only after that copy ran
+    // (round 5: unarmed, a fifth async batch could overwrite a queued copy's source)
+    st->armed = true;
     return 0;
 }
 

@@ -175,21 +175,27 @@ def test_overlapped_stream_chain_and_large_stream(gpu_ctx):
             assert w == 0, i
 
 
+@pytest.mark.parametrize("aligned", [True, False])
 @pytest.mark.parametrize("bpc", [8192, 65536])
-def test_overlapped_chain_chunks_above_4k_pieces(gpu_ctx, bpc):
+def test_overlapped_chain_chunks_above_4k_pieces(gpu_ctx, bpc, aligned):
     """an overlapped verify at bpc = R x 4096 runs the piece compute of the pitch walk
     (crc32c_wave_kernel<4096, compute, PITCH, SOLO>) without the AQL barrier, then the combine. 30
     chained launches over 5 resident arenas of 64 KiB packets (one arena corrupted, one with a short
     last packet), each into its own result word, alternating the two piece buffers: every word
     reports exactly its arena's first bad (packet, chunk), and a compute -> verify round trip in
-    the same overlapped form writes the oracle's words."""
+    the same overlapped form writes the oracle's words. aligned=False puts the data 4 bytes off a
+    16-byte boundary at bpc 65536 (4-byte word regions): the stream falls back to descriptors and the
+    chunk-per-lane kernel, queued 30 deep without a sync — the case that found the descriptor staging
+    ring being rewritten under a queued copy (round 5, packets_async)."""
     from libhdfs3_amd.engine import CrcContext, DeviceBuffer
 
     n, plen = 96, 65536
     arenas, streams, hosts = [], [], []
     for a in range(5):
         last = plen if a != 3 else (bpc * 2 + 300 if bpc * 2 + 300 < plen else plen - 300)
-        host, pitch, crc_off, data_off, datas = build_arena(n, plen, last, bpc, 7000 + 131 * a + bpc % 1013)
+        words = 4 * (-(-plen // bpc))
+        gap = 32 + ((-(32 + words)) % 16 if aligned else 0)
+        host, pitch, crc_off, data_off, datas = build_arena(n, plen, last, bpc, 7000 + 131 * a + bpc % 1013, gap)
         hosts.append((host, pitch, crc_off, data_off, datas))
         arenas.append(gpu_ctx.upload(host))
         streams.append(CrcContext.packet_stream(crc_off, data_off, pitch, n, plen, last))

@@ -7,7 +7,7 @@
 #
 # steps:
 #   tests            the whole -m gpu suite
-#   tests:<expr>     the -m gpu tests selected by -k <expr> (use _ for spaces: tests:bench_json_or_scaling)
+#   tests:<expr>     the -m gpu tests selected by -k <expr> (+ for spaces: tests:bench_json+or+scaling)
 #   file:<path>      the -m gpu tests of one test file
 #   smoke            __graft_entry__.smoke()
 #   bench            python bench.py (the default line: K = 2000)
@@ -41,7 +41,7 @@ for step in "$@"; do
     echo "== $step ($(date +%T))"
     case "$step" in
     tests) run 900 gpurun_out/${TAG}_gpu_tests.txt $PYT tests; tail -3 gpurun_out/${TAG}_gpu_tests.txt ;;
-    tests:*) k=${step#tests:}; k=${k//_/ }
+    tests:*) k=${step#tests:}; k=${k//+/ }
              run 900 gpurun_out/${TAG}_gpu_tests_k.txt $PYT tests -k "$k"; tail -3 gpurun_out/${TAG}_gpu_tests_k.txt ;;
     file:*) f=${step#file:}; n=$(basename "$f" .py)
             run 900 gpurun_out/${TAG}_${n}.txt $PYT "$f"; tail -3 gpurun_out/${TAG}_${n}.txt ;;
