@@ -297,7 +297,10 @@ struct hdfs3_block_reader {
                 // wire, same delivery (PacketRef), same ChecksumException semantics.
                 if (b.pk.empty()) {  // geometry from the batch's first packet
                     b.d0 = (uint64_t(batch_packets) * crc_len + 4095) & ~uint64_t(4095);
-                    const uint64_t need = b.d0 + uint64_t(batch_packets) * uint64_t(h.data_len);
+                    // the arena as acquired holds the batch (64 KiB packets: 32 KiB of words + 4 MiB of
+                    // data in the 64 x 66,064 B the ring is sized for); larger packets close the batch
+                    // early, as in the wire layout, and only a single packet that does not fit grows it
+                    const uint64_t need = b.d0 + uint64_t(h.data_len);
                     if (need > b.a.cap)
                         if (int rc = grow(b.a, need, size_t(batch_packets))) return rx_fail(rc, "arena growth failed");
                 } else if (b.sealed || b.words_used + crc_len > b.d0 ||

@@ -347,6 +347,11 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // -0.16 / -0.44 and -0.26, nt alone -0.22 / -0.21 and -0.14. The buffer offset is 31-bit:
     // launch_wave3 stages only launches whose words stay below 2 GiB (data below 256 GiB at bpc 512).
     auto stage_store = [&](gu8 *p, uint32_t v) {
+        // kLabNoStore (diagnostic 118): the staged words are kept live (a store that practically never
+        // happens) but not written: what the flush's global stores cost a launch (wrong results)
+        if constexpr ((LAB & kLabNoStore) != 0) {
+            if (v != 0x9E3779B9u) return;
+        }
         if constexpr (kStage && (LAB & kLabStorePlain) == 0) {
             const uint64_t wb = rfl64(reinterpret_cast<uint64_t>(walk.words));
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(

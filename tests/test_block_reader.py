@@ -264,3 +264,22 @@ def test_wire_layout_knob_keeps_the_packet_kernels():
                          timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.split() == ["ok", "512", "ok", "4096", "ok", "8192"], out.stdout
+
+
+def test_dense_batches_of_large_packets_keep_the_arena_size():
+    """256 KiB datanode packets (64-packet batches would need 16 MiB): a dense batch closes when the
+    arena the ring was sized for is full, as the wire layout does, instead of growing it (the pinned
+    pool's budget assumes 64 KiB packets): 15 packets per batch, every byte delivered."""
+    from loopback import LoopbackDatanode
+
+    node = LoopbackDatanode(packet_bytes=256 << 10)
+    try:
+        data = splitmix_bytes(16 << 20, 4321)
+        node.add_block(1, data, oracle_compute(data, 512), 512)
+        out, st = _read(node.port, 1, 0, data.nbytes, batch_packets=64)
+        assert np.array_equal(out, data)
+        # 15 packets per batch in a 64 x 66,064-byte arena (fewer batches if the pooled ctx hands back a
+        # larger cached arena; a batch grown to take all 64 packets would be one)
+        assert st["packets"] == 64 and st["gpu_batches"] >= 2, st
+    finally:
+        node.stop()
