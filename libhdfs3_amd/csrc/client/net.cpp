@@ -9,6 +9,7 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 namespace hdfs3crc {
@@ -87,24 +88,41 @@ int listen_tcp(int port, int *bound_port) {
     return fd;
 }
 
+// Reads of at least this many bytes that find nothing buffered wait for their whole remainder in one
+// blocking recv (MSG_WAITALL under SO_RCVTIMEO): a 64 KiB packet payload arriving as many TCP segments
+// then costs one wake-up of the reading thread instead of a poll + recv per segment (round 5)
+constexpr size_t kWaitAllMin = 4096;
+
 int read_fully(int fd, void *buf, size_t n, int timeout_ms) {
     char *p = static_cast<char *>(buf);
     while (n) {
-        // poll first: a blocking recv would ignore the timeout
-        if (const int rc = wait_fd(fd, POLLIN, timeout_ms)) return rc;
+        // what is already buffered first: no poll when the data is there
         const ssize_t r = ::recv(fd, p, n, MSG_DONTWAIT);
         if (r > 0) {
             p += r;
             n -= size_t(r);
-        } else if (r == 0) {
-            return -ECONNRESET;  // peer closed before the message was complete
-        } else if (errno == EINTR) {
             continue;
-        } else if (errno == EAGAIN || errno == EWOULDBLOCK) {
-            continue;
-        } else {
-            return -errno;
         }
+        if (r == 0) return -ECONNRESET;  // peer closed before the message was complete
+        if (errno == EINTR) continue;
+        if (errno != EAGAIN && errno != EWOULDBLOCK) return -errno;
+        if (n >= kWaitAllMin && timeout_ms > 0) {
+            timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
+            if (setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv)) == 0) {
+                const ssize_t w = ::recv(fd, p, n, MSG_WAITALL);
+                if (w > 0) {  // all of it, or what arrived before the timeout / a signal
+                    p += w;
+                    n -= size_t(w);
+                    continue;
+                }
+                if (w == 0) return -ECONNRESET;
+                if (errno == EINTR) continue;
+                if (errno == EAGAIN || errno == EWOULDBLOCK) return -ETIMEDOUT;
+                return -errno;
+            }
+        }
+        // poll: a blocking recv without SO_RCVTIMEO would ignore the timeout
+        if (const int rc = wait_fd(fd, POLLIN, timeout_ms)) return rc;
     }
     return 0;
 }
@@ -112,7 +130,7 @@ int read_fully(int fd, void *buf, size_t n, int timeout_ms) {
 int write_fully(int fd, const void *buf, size_t n, int timeout_ms) {
     const char *p = static_cast<const char *>(buf);
     while (n) {
-        if (const int rc = wait_fd(fd, POLLOUT, timeout_ms)) return rc;
+        // send first: poll only when the socket's buffer is full (round 5; a poll per send before)
         const ssize_t r = ::send(fd, p, n, MSG_NOSIGNAL | MSG_DONTWAIT);
         if (r > 0) {
             p += r;
@@ -120,7 +138,7 @@ int write_fully(int fd, const void *buf, size_t n, int timeout_ms) {
         } else if (r < 0 && errno == EINTR) {
             continue;
         } else if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-            continue;
+            if (const int rc = wait_fd(fd, POLLOUT, timeout_ms)) return rc;
         } else {
             return r < 0 ? -errno : -EIO;
         }
