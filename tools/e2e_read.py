@@ -189,10 +189,17 @@ def main():
     ap.add_argument("--read-mib", type=int, default=4, help="hdfsRead request size")
     ap.add_argument("--diag", action="store_true", help="per-phase timing of the block reader only")
     ap.add_argument("--local-only", action="store_true", help="only the short-circuit reader lines")
+    ap.add_argument("--torch", action="store_true",
+                    help="initialise torch's own HIP runtime on cuda:0 first (as bench.py's process has it)")
+    ap.add_argument("--only-hdfsread", action="store_true", help="the single-stream hdfsRead lines only")
     ap.add_argument("--readahead", default="1,2,3,7",
                     help="block read-ahead depths of the extra single-stream hdfsRead lines ('' = none)")
     args = ap.parse_args()
 
+    if args.torch:
+        import torch
+        _keep = torch.empty(1 << 30, dtype=torch.uint8, device="cuda:0")  # noqa: F841 (held for the run)
+        torch.cuda.synchronize()
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import CrcContext
 
@@ -241,7 +248,7 @@ def main():
         return
     try:
         for verify in (True, False):
-            for mode in ("hdfsRead", "parallel_pread"):
+            for mode in (("hdfsRead",) if args.only_hdfsread else ("hdfsRead", "parallel_pread")):
                 best = 0.0
                 for _ in range(args.reps):
                     errors: list[str] = []
@@ -277,7 +284,7 @@ def main():
             _native.check("pool_stats", _native.lib().hdfs3_crc_pool_stats_get(ctypes.byref(st)))
             return round(st.pinned_bytes / 2**20, 1), round(st.pinned_cap_bytes / 2**20, 1)
 
-        for ahead in [int(x) for x in args.readahead.split(",") if x]:
+        for ahead in ([] if args.only_hdfsread else [int(x) for x in args.readahead.split(",") if x]):
             best = 0.0
             rates = []
             cold = []
@@ -307,7 +314,8 @@ def main():
                               "pool_retained_pinned_mib": retained, "pool_cap_mib": cap}), flush=True)
     finally:
         dn.stop()
-    local_reads(data, crc, args, line)
+    if not args.only_hdfsread:
+        local_reads(data, crc, args, line)
     ctx.close()
 
 
