@@ -48,7 +48,12 @@ typedef struct hdfs3_reader_opts {
 } hdfs3_reader_opts;
 
 /* Connect, send OP_READ_BLOCK for [start, start+len) and check the response
- * (RemoteBlockReader ctor, :46-75). 0 or -errno. */
+ * (RemoteBlockReader ctor, :46-75). 0 or -errno.
+ * Packets are read ahead into pinned batch arenas and verified on the GPU a batch at a time. A
+ * batch lands densely (every packet's checksums back to back, their data back to back) and is
+ * verified as one contiguous block while its packets hold whole chunks; HDFS3_READER_LAYOUT=wire
+ * keeps each packet's [checksums][data] together instead (read once per process). Delivery and
+ * errors are the same either way. */
 int hdfs3_block_reader_open(const char *host, int port, const hdfs3_block_id *block, int64_t start,
                             int64_t len, const char *client_name, const hdfs3_reader_opts *opts,
                             hdfs3_block_reader **out);

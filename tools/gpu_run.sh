@@ -15,6 +15,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of the driver's command (PMC and CPU legs off)
 #   tool:<script>    python tools/<script> (extra args after '@': tool:ab.py@--variants@0,154@--overlap)
 #   rprof:<script>   the same under rocprofv3 --kernel-trace --stats (csv in gpurun_out/<tag>_<script>_<i>/)
+#   pmc[:args]       tools/pmc.sh counter passes over tools/pmc_driver.py (args after '@', e.g. pmc:--overlap)
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -61,6 +62,9 @@ for step in "$@"; do
               run 600 gpurun_out/${TAG}_${n}.txt rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/${TAG}_${n} -o run -- python3 -u tools/"${parts[0]}" "${parts[@]:1}"
               tail -5 gpurun_out/${TAG}_${n}.txt ;;
+    pmc|pmc:*) t=${step#pmc}; t=${t#:}; IFS=@ read -r -a parts <<< "$t"
+               run 900 gpurun_out/${TAG}_pmc_$i.txt bash tools/pmc.sh gpurun_out/${TAG}_pmc_$i "${parts[@]}"
+               python3 tools/pmc_summary.py gpurun_out/${TAG}_pmc_$i | tail -40 ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
