@@ -117,8 +117,9 @@ int read_fully(int fd, void *buf, size_t n, int timeout_ms) {
                 }
                 if (w == 0) return -ECONNRESET;
                 if (errno == EINTR) continue;
-                if (errno == EAGAIN || errno == EWOULDBLOCK) return -ETIMEDOUT;
-                return -errno;
+                // EAGAIN: SO_RCVTIMEO expired with nothing, or the socket is non-blocking after all:
+                // the poll below decides (ready: read on; its own timeout: -ETIMEDOUT)
+                if (errno != EAGAIN && errno != EWOULDBLOCK) return -errno;
             }
         }
         // poll: a blocking recv without SO_RCVTIMEO would ignore the timeout
