@@ -339,3 +339,50 @@ def test_packet_stream_chunks_above_4k_pieces(gpu_ctx, bpc, last):
     gpu_ctx.upload(blank, d)
     gpu_ctx.compute_packet_stream_async(d.ptr, arena.nbytes, ps, bpc)
     assert np.array_equal(gpu_ctx.download(d, arena.nbytes), arena)
+
+
+@pytest.mark.parametrize("bpc", [1024, 4096, 8192, 65536])
+@pytest.mark.parametrize("last", [65536, 65536 - 4096 * 3, 4096 * 2 + 77])
+def test_descriptors_with_words_at_their_own_pitch(gpu_ctx, bpc, last):
+    """Round 5: a descriptor list whose packets sit at one data pitch and whose words are dense (the
+    output stream's batches) takes the pitch walk with its own word pitch (and at R x 4096 its pieces +
+    the packet-mode combine). Verify keys and computed words against the oracle, with a flip in the
+    first and the last packet; remote and local tail semantics."""
+    n, plen, pitch = 20, 65536, 65536 + 4096
+    wpp = 4 * (plen // bpc)
+    arena = np.zeros(n * pitch + n * wpp + 4096, np.uint8)
+    wbase = n * pitch
+    datas, pk = [], []
+    for i in range(n):
+        dl = plen if i + 1 < n else last
+        d = splitmix_bytes(dl, 600 + i + bpc)
+        arena[i * pitch:i * pitch + dl] = d
+        w = oracle_compute(d, bpc)
+        arena[wbase + i * wpp:wbase + i * wpp + w.nbytes] = w
+        datas.append(d)
+        pk.append((i * pitch, wbase + i * wpp, dl))
+    dev = gpu_ctx.upload(arena)
+    for local in (False, True):
+        assert gpu_ctx.verify_packets_dev(dev.ptr, arena.nbytes, pk, bpc, local) == (-1, -1)
+    for p, q in [(0, 7), (n - 1, last - 1)]:
+        bad = arena.copy()
+        bad[p * pitch + q] ^= 0x01
+        gpu_ctx.upload(bad, dev)
+        for local in (False, True):
+            want = (-1, -1)
+            for i in range(n):
+                c = oracle_verify(bad[i * pitch:i * pitch + datas[i].size], bpc,
+                                  bad[wbase + i * wpp:wbase + i * wpp + 4 * (-(-datas[i].size // bpc))], local)
+                if c >= 0:
+                    want = (i, c)
+                    break
+            assert gpu_ctx.verify_packets_dev(dev.ptr, arena.nbytes, pk, bpc, local) == want, (p, q, local)
+    blank = arena.copy()
+    blank[wbase:] = 0xA5
+    gpu_ctx.upload(blank, dev)
+    gpu_ctx.compute_packets_dev(dev.ptr, arena.nbytes, pk, bpc)
+    got = gpu_ctx.download(dev, arena.nbytes)
+    for i in range(n):
+        nw = 4 * (-(-datas[i].size // bpc))
+        assert np.array_equal(got[wbase + i * wpp:wbase + i * wpp + nw], oracle_compute(datas[i], bpc)), i
+    assert np.array_equal(got[:wbase], arena[:wbase])
