@@ -705,7 +705,9 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
     (hdfs3_crc32c_verify: pinned and pageable host buffers, H2D-inclusive). Beside them, the
     reference CPU path on the same packet stream: RemoteBlockReader's receive -> verifyChecksum ->
     copy loop on the reading thread with the reference's own HWCrc32c (oracle/_ref; test
-    infrastructure, this baseline leg only; RemoteBlockReader.cpp:226-357), verify on and off.
+    infrastructure, this baseline leg only; RemoteBlockReader.cpp:226-357), verify on and off. The write
+    direction (compute-on-write: H2D of the data, D2H of the words): hdfsWrite of the GiB into a sink, beside
+    the reference's write loop (OutputStreamImpl::appendInternal + Packet, its HWCrc32c) into the same sink.
     Every line: one untimed first pass (reported as cold), then `reps` timed passes (median and all);
     every pass's output buffer is compared with the file, byte for byte."""
     import ctypes
@@ -791,6 +793,11 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
                                                  kind="reference")
             lines["reference_cpu_no_verify"] = dict(measure(lambda: ref_read(False)), verify=False, cores=1,
                                                     kind="reference")
+        # the write direction (compute-on-write, H2D of the data + D2H of the words): hdfsWrite of the same
+        # GiB in 1 MiB writes into a sink that reads the packets (tools/loopback's count sink), beside the
+        # reference's write loop with its HWCrc32c on the writing thread (oracle/ref_driver.cpp
+        # ref_write_packets); both sinks must see the same packets and wire bytes
+        lines.update(write_lines(host_data, bpc, block_bytes, dev, reps))
         hctx.close()
     finally:
         dn.stop()
@@ -807,6 +814,64 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
         out["gpu_over_reference_cpu"] = round(lines["hdfsRead_verify"]["gib_s"] / lines["reference_cpu_verify"]["gib_s"], 2)
         out["readahead2_over_reference_cpu"] = round(
             lines["hdfsRead_verify_readahead2"]["gib_s"] / lines["reference_cpu_verify"]["gib_s"], 2)
+    return out
+
+
+def write_lines(host_data, bpc, block_bytes, dev, reps):
+    """config5's write lines (see config5_block): GPU compute-on-write through hdfs3_output_* into a C sink,
+    and the reference's loop. Rates are GiB/s of user data; 1 untimed + `reps` timed passes each."""
+    import ctypes
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from util import ref_lib
+    from libhdfs3_amd import _native
+    from libhdfs3_amd.engine import OutputStream
+
+    total = host_data.nbytes
+    sink = ctypes.cast(_native.loopback().hdfs3_loopback_count_sink, ctypes.c_void_p).value
+    seen = {}
+
+    def gpu_write():
+        counts = (ctypes.c_uint64 * 3)()
+        with OutputStream(device=dev, bytes_per_checksum=bpc, block_size=block_bytes, batch_packets=64,
+                          raw_sink=sink, raw_user=ctypes.addressof(counts)) as s:
+            for off in range(0, total, 1 << 20):
+                s.write(host_data[off:off + (1 << 20)])
+            s.close()
+        seen["gpu"] = (int(counts[0]), int(counts[1]))
+
+    def rates(fn):
+        r = []
+        for _ in range(1 + reps):
+            t0 = time.perf_counter()
+            fn()
+            r.append(total / (time.perf_counter() - t0) / 2**30)
+        t = r[1:]
+        return {"gib_s": round(sorted(t)[len(t) // 2], 2), "gib_s_all": [round(x, 2) for x in t],
+                "cold_gib_s": round(r[0], 2), "unit": "GiB/s"}
+
+    out = {"hdfsWrite_sink": dict(rates(gpu_write), api="hdfs3_output_write, 1 MiB writes, 64-packet GPU batches "
+                                                       "(H2D data, compute, D2H words) into a C sink")}
+    ref = ref_lib()
+    if ref is not None:
+        f = ref.ref_write_packets
+        f.restype = ctypes.c_double
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        pk, wb = ctypes.c_uint64(), ctypes.c_uint64()
+
+        def ref_write():
+            if f(host_data.ctypes.data, total, bpc, 65536, block_bytes, ctypes.byref(pk), ctypes.byref(wb)) < 0:
+                raise SystemExit("config5: the reference write loop failed")
+            seen["ref"] = (pk.value, wb.value)
+
+        out["reference_cpu_write_sink"] = dict(rates(ref_write), cores=1, kind="reference",
+                                               api="OutputStreamImpl::appendInternal + Packet::addChecksum/addData "
+                                                   "with the reference HWCrc32c, the same sink")
+        if seen["gpu"] != seen["ref"]:
+            raise SystemExit(f"PARITY FAILURE: config5 write: GPU path sent {seen['gpu']} (packets, bytes), "
+                             f"the reference loop {seen['ref']}")
+        out["hdfsWrite_sink"]["checked"] = (f"{seen['gpu'][0]} packets / {seen['gpu'][1]} wire bytes, equal to the "
+                                            "reference loop's (every packet's bytes: tests/test_output_stream.py)")
     return out
 
 

@@ -126,4 +126,74 @@ int64_t ref_remote_read_block(int fd, void *out, int64_t cap, int bpc, int verif
     return remote_loop_read_block(fd, out, cap, bpc, verify, bad_packet, ref_loop_verify, nullptr);
 }
 
+/* The reference's write loop on one thread, for bench.py's config-5 write line: OutputStreamImpl::
+ * appendInternal's whole-chunk path (OutputStreamImpl.cpp:298-359: checksum->update over the chunk,
+ * appendChunkToPacket = Packet::addChecksum + addData, Packet.cpp:73-100) with the reference HWCrc32c,
+ * packets of computePacketChunkSize chunks (:161-170), sendPacket when a packet is full or the block ends,
+ * and each block's empty last packet (Packet::getBuffer framing: 31-byte header, then the BE words, then
+ * the data). Every packet goes to a sink that touches one byte per 64 B (tools/loopback's count sink).
+ * len a multiple of bpc. Returns seconds; *packets / *wire_bytes: what reached the sink. */
+double ref_write_packets(const void *data, int64_t len, int bpc, int packet_size, int64_t block_size,
+                         uint64_t *packets, uint64_t *wire_bytes) {
+    const int hdr = 31, with_sum = bpc + 4;
+    int cpp = (packet_size - hdr + with_sum - 1) / with_sum;
+    if (cpp < 1) cpp = 1;
+    char *pkt = static_cast<char *>(malloc(size_t(hdr) + size_t(cpp) * size_t(with_sum)));
+    if (!pkt) return -1.0;
+    HWCrc32c cs;
+    const char *d = static_cast<const char *>(data);
+    uint64_t np = 0, nb = 0, touch = 0;
+    int64_t seq = 0;
+    auto sink = [&](const char *p, size_t n) {
+        for (size_t i = 0; i < n; i += 64) touch += uint8_t(p[i]);
+        ++np;
+        nb += n;
+    };
+    auto header = [&](int64_t off, int32_t dlen, bool last) {  // PacketHeader::writeInBuffer, 31 bytes
+        const int32_t plen = dlen + 4 * ((dlen + bpc - 1) / bpc) + 4;
+        const uint32_t be = htonl(uint32_t(plen));
+        memcpy(pkt, &be, 4);
+        pkt[4] = 0;
+        pkt[5] = 25;
+        pkt[6] = 0x09;
+        memcpy(pkt + 7, &off, 8);
+        pkt[15] = 0x11;
+        memcpy(pkt + 16, &seq, 8);
+        pkt[24] = 0x18;
+        pkt[25] = last ? 1 : 0;
+        pkt[26] = 0x25;
+        memcpy(pkt + 27, &dlen, 4);
+        ++seq;
+    };
+    timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int64_t b0 = 0; b0 < len; b0 += block_size) {
+        const int64_t bend = b0 + block_size < len ? b0 + block_size : len;
+        for (int64_t p0 = b0; p0 < bend;) {
+            int n = 0;
+            char *sums = pkt + hdr;
+            char *pdata = sums + 4 * cpp;  // Packet's layout: checksums before data (getBuffer moves them)
+            for (; n < cpp && p0 + int64_t(n) * bpc < bend; ++n) {
+                const char *c = d + p0 + int64_t(n) * bpc;
+                cs.reset();
+                cs.update(c, bpc);
+                const uint32_t w = htonl(cs.getValue());
+                memcpy(sums + 4 * n, &w, 4);
+                memcpy(pdata + int64_t(n) * bpc, c, size_t(bpc));
+            }
+            header(p0 - b0, n * bpc, false);
+            if (n < cpp) memmove(sums + 4 * n, pdata, size_t(n) * size_t(bpc));  // getBuffer: words next to data
+            sink(pkt, size_t(hdr) + size_t(n) * size_t(with_sum));
+            p0 += int64_t(n) * bpc;
+        }
+        header(bend - b0, 0, true);  // the block's empty last packet
+        sink(pkt, size_t(hdr));
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(pkt);
+    if (packets) *packets = np + (touch & 0);
+    if (wire_bytes) *wire_bytes = nb;
+    return double(t1.tv_sec - t0.tv_sec) + 1e-9 * double(t1.tv_nsec - t0.tv_nsec);
+}
+
 }  // extern "C"

@@ -53,7 +53,8 @@ def test_bench_json_line(mode):
     # BASELINE.json configs[4]: loopback hdfsRead of 1 GiB, PCIe-inclusive, the reference CPU path beside it
     c5 = j["config5"]["lines"]
     for k in ("hdfsRead_verify", "hdfsRead_no_verify", "hdfsRead_verify_readahead2", "host_api_pinned",
-              "host_api_pageable"):
+              "host_api_pageable", "hdfsWrite_sink"):
         assert c5[k]["gib_s"] > 0 and len(c5[k]["gib_s_all"]) == 3, k
     if "reference_cpu_verify" in c5:  # oracle/_ref travels with the tree when it was built
         assert c5["reference_cpu_verify"]["kind"] == "reference" and c5["reference_cpu_verify"]["gib_s"] > 0
+        assert c5["reference_cpu_write_sink"]["gib_s"] > 0 and "checked" in c5["hdfsWrite_sink"]
