@@ -192,6 +192,7 @@ def main():
     ap.add_argument("--torch", action="store_true",
                     help="initialise torch's own HIP runtime on cuda:0 first (as bench.py's process has it)")
     ap.add_argument("--only-hdfsread", action="store_true", help="the single-stream hdfsRead lines only")
+    ap.add_argument("--no-local", action="store_true", help="skip the short-circuit reader lines")
     ap.add_argument("--readahead", default="1,2,3,7",
                     help="block read-ahead depths of the extra single-stream hdfsRead lines ('' = none)")
     args = ap.parse_args()
@@ -314,7 +315,7 @@ def main():
                               "pool_retained_pinned_mib": retained, "pool_cap_mib": cap}), flush=True)
     finally:
         dn.stop()
-    if not args.only_hdfsread:
+    if not args.only_hdfsread and not args.no_local:
         local_reads(data, crc, args, line)
     ctx.close()
 
