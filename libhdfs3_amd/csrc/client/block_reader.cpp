@@ -309,9 +309,9 @@ struct hdfs3_block_reader {
                     have_pending_hdr = true;
                     break;
                 }
-                if (int rc = net::read_fully(fd, b.a.h + b.words_used, crc_len, timeout_ms))
-                    return rx_fail(rc, "RemoteBlockReader: failed to read packet checksums");
-                if (int rc = net::read_fully(fd, b.a.h + b.d0 + b.data_used, h.data_len, timeout_ms))
+                // the packet's checksums and data in one scatter read (:244-245 reads them as one buffer)
+                if (int rc = net::read_fully2(fd, b.a.h + b.words_used, crc_len, b.a.h + b.d0 + b.data_used,
+                                              size_t(h.data_len), timeout_ms))
                     return rx_fail(rc, "RemoteBlockReader: failed to read packet payload");
                 last_seqno = h.seqno;
                 packets.fetch_add(1, std::memory_order_relaxed);

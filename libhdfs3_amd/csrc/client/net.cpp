@@ -9,6 +9,7 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <sys/time.h>
 #include <unistd.h>
 
@@ -124,6 +125,51 @@ int read_fully(int fd, void *buf, size_t n, int timeout_ms) {
         }
         // poll: a blocking recv without SO_RCVTIMEO would ignore the timeout
         if (const int rc = wait_fd(fd, POLLIN, timeout_ms)) return rc;
+    }
+    return 0;
+}
+
+int read_fully2(int fd, void *a, size_t na, void *b, size_t nb, int timeout_ms) {
+    iovec v[2] = {{a, na}, {b, nb}};
+    int first = na ? 0 : 1;
+    while (first < 2) {
+        msghdr m{};
+        m.msg_iov = v + first;
+        m.msg_iovlen = size_t(2 - first);
+        const size_t want = v[first].iov_len + (first == 0 ? v[1].iov_len : 0);
+        ssize_t r = ::recvmsg(fd, &m, MSG_DONTWAIT);
+        if (r < 0 && errno == EINTR) continue;
+        if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+            r = 0;
+            if (want >= kWaitAllMin && timeout_ms > 0) {
+                timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
+                if (setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv)) == 0) {
+                    r = ::recvmsg(fd, &m, MSG_WAITALL);
+                    if (r < 0 && errno == EINTR) continue;
+                    if (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK) return -errno;
+                    if (r == 0) return -ECONNRESET;
+                    if (r < 0) r = 0;
+                }
+            }
+            if (r == 0) {
+                if (const int rc = wait_fd(fd, POLLIN, timeout_ms)) return rc;
+                continue;
+            }
+        } else if (r < 0) {
+            return -errno;
+        } else if (r == 0) {
+            return -ECONNRESET;
+        }
+        // advance over what arrived
+        size_t got = size_t(r);
+        while (got && first < 2) {
+            const size_t take = got < v[first].iov_len ? got : v[first].iov_len;
+            v[first].iov_base = static_cast<char *>(v[first].iov_base) + take;
+            v[first].iov_len -= take;
+            got -= take;
+            if (v[first].iov_len == 0) ++first;
+        }
+        while (first < 2 && v[first].iov_len == 0) ++first;
     }
     return 0;
 }

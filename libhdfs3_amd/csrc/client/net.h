@@ -16,6 +16,9 @@ int connect_tcp(const char *host, int port, int timeout_ms);
 int listen_tcp(int port, int *bound_port);
 // 0 on success, -errno on failure (-ETIMEDOUT, -ECONNRESET on EOF)
 int read_fully(int fd, void *buf, size_t n, int timeout_ms);
+// na bytes into a, then nb bytes into b, in as few recvmsg calls as the data allows (one when it is
+// buffered or arrives within the timeout): a packet's checksums and data into two places
+int read_fully2(int fd, void *a, size_t na, void *b, size_t nb, int timeout_ms);
 int write_fully(int fd, const void *buf, size_t n, int timeout_ms);
 // protobuf varint32 length prefix, as BufferedSocketReader::readVarint32
 int read_varint32(int fd, uint32_t *out, int timeout_ms);

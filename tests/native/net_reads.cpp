@@ -1,0 +1,75 @@
+// CPU test of csrc/client/net.cpp's reads (tests/test_wire_sanitized.py builds it under ASan/UBSan):
+// a writer thread sends a byte stream in random-sized pieces with random pauses over a socketpair;
+// the reader takes it apart with read_fully and read_fully2 (scatter into two buffers, the block
+// reader's [checksums][data] read) in random-sized requests, and every byte must land where expected.
+// Also: EOF mid-message is -ECONNRESET, and a silent peer times out as -ETIMEDOUT.
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "client/net.h"
+
+using namespace hdfs3crc;
+
+static int fail(const char *what) {
+    std::printf("FAIL %s\n", what);
+    return 1;
+}
+
+int main() {
+    std::mt19937_64 rng(12345);
+    const size_t total = 24u << 20;
+    std::vector<unsigned char> src(total);
+    for (auto &c : src) c = static_cast<unsigned char>(rng());
+    int sv[2];
+    if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv)) return fail("socketpair");
+    std::thread writer([&] {
+        std::mt19937_64 r(777);
+        size_t off = 0;
+        while (off < total) {
+            size_t n = 1 + r() % 200000;
+            if (n > total - off) n = total - off;
+            if (net::write_fully(sv[1], src.data() + off, n, 10000)) break;
+            off += n;
+            if (r() % 8 == 0) std::this_thread::sleep_for(std::chrono::microseconds(r() % 300));
+        }
+    });
+    std::vector<unsigned char> a(70000), b(300000);
+    size_t off = 0;
+    while (off < total) {
+        const size_t left = total - off;
+        if (rng() % 2) {
+            size_t n = 1 + rng() % 250000;
+            if (n > left) n = left;
+            if (net::read_fully(sv[0], b.data(), n, 10000)) return fail("read_fully");
+            if (std::memcmp(b.data(), src.data() + off, n)) return fail("read_fully bytes");
+            off += n;
+        } else {
+            size_t na = rng() % 70000, nb = rng() % 250000;
+            if (na > left) na = left;
+            if (nb > left - na) nb = left - na;
+            if (net::read_fully2(sv[0], a.data(), na, b.data(), nb, 10000)) return fail("read_fully2");
+            if (std::memcmp(a.data(), src.data() + off, na) || std::memcmp(b.data(), src.data() + off + na, nb))
+                return fail("read_fully2 bytes");
+            off += na + nb;
+        }
+    }
+    writer.join();
+    // a silent peer: both reads time out
+    if (net::read_fully(sv[0], b.data(), 10, 200) != -ETIMEDOUT) return fail("read_fully timeout");
+    if (net::read_fully2(sv[0], a.data(), 100, b.data(), 100000, 200) != -ETIMEDOUT) return fail("read_fully2 timeout");
+    // EOF in the middle of a message
+    if (net::write_fully(sv[1], src.data(), 5000, 1000)) return fail("write");
+    shutdown(sv[1], SHUT_WR);
+    if (net::read_fully2(sv[0], a.data(), 1000, b.data(), 10000, 1000) != -ECONNRESET) return fail("read_fully2 eof");
+    close(sv[0]);
+    close(sv[1]);
+    std::printf("net reads ok\n");
+    return 0;
+}
