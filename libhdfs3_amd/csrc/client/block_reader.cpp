@@ -257,7 +257,7 @@ struct hdfs3_block_reader {
             return 0;
         }
         uint8_t buf[wire::kPacketHeaderSize];
-        if (int rc = net::read_fully(fd, buf, sizeof(buf), timeout_ms))
+        if (int rc = net::recv_fully(fd, buf, sizeof(buf)))
             return rx_fail(rc, "RemoteBlockReader: failed to read block header");
         if (!h.decode(buf, sizeof(buf))) return rx_fail(-EPROTO, "Invalid PacketHeader");
         return 0;
@@ -310,8 +310,8 @@ struct hdfs3_block_reader {
                     break;
                 }
                 // the packet's checksums and data in one scatter read (:244-245 reads them as one buffer)
-                if (int rc = net::read_fully2(fd, b.a.h + b.words_used, crc_len, b.a.h + b.d0 + b.data_used,
-                                              size_t(h.data_len), timeout_ms))
+                if (int rc = net::recv_fully2(fd, b.a.h + b.words_used, crc_len, b.a.h + b.d0 + b.data_used,
+                                              size_t(h.data_len)))
                     return rx_fail(rc, "RemoteBlockReader: failed to read packet payload");
                 last_seqno = h.seqno;
                 packets.fetch_add(1, std::memory_order_relaxed);
@@ -344,7 +344,7 @@ struct hdfs3_block_reader {
                 if (int rc = grow(b.a, size + 64, size_t(batch_packets))) return rx_fail(rc, "arena growth failed");
                 off = ((crc_len + 15) & ~uint64_t(15)) - crc_len;
             }
-            if (int rc = net::read_fully(fd, b.a.h + off, size, timeout_ms))
+            if (int rc = net::recv_fully(fd, b.a.h + off, size))
                 return rx_fail(rc, "RemoteBlockReader: failed to read packet payload");
             last_seqno = h.seqno;
             packets.fetch_add(1, std::memory_order_relaxed);
@@ -674,6 +674,11 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
     if (int rc = r->check_response()) {
         delete r;
         return rc;
+    }
+    // the receiver's blocking reads (net::recv_fully) time out through SO_RCVTIMEO, set once here
+    if (int rc = net::set_recv_timeout(r->fd, r->timeout_ms)) {
+        delete r;
+        return fail(rc, "RemoteBlockReader: cannot set the socket's read timeout");
     }
     r->start_receiver();  // read-ahead starts now, as RemoteBlockReader's first read would
     *out = r;

@@ -19,6 +19,13 @@ int read_fully(int fd, void *buf, size_t n, int timeout_ms);
 // na bytes into a, then nb bytes into b, in as few recvmsg calls as the data allows (one when it is
 // buffered or arrives within the timeout): a packet's checksums and data into two places
 int read_fully2(int fd, void *a, size_t na, void *b, size_t nb, int timeout_ms);
+// Blocking reads for a socket whose SO_RCVTIMEO was set once (set_recv_timeout): one recv/recvmsg with
+// MSG_WAITALL per message when it arrives within the timeout, the way RemoteBlockReader's reading thread
+// does it — no poll or setsockopt per call (round 5: the block reader's receiver spent ~4 syscalls per
+// packet on them). -ETIMEDOUT when the timeout passes with the message incomplete, -ECONNRESET at EOF.
+int set_recv_timeout(int fd, int timeout_ms);
+int recv_fully(int fd, void *buf, size_t n);
+int recv_fully2(int fd, void *a, size_t na, void *b, size_t nb);
 int write_fully(int fd, const void *buf, size_t n, int timeout_ms);
 // protobuf varint32 length prefix, as BufferedSocketReader::readVarint32
 int read_varint32(int fd, uint32_t *out, int timeout_ms);

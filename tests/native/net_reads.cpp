@@ -40,11 +40,21 @@ int main() {
             if (r() % 8 == 0) std::this_thread::sleep_for(std::chrono::microseconds(r() % 300));
         }
     });
+    if (net::set_recv_timeout(sv[0], 10000)) return fail("set_recv_timeout");
     std::vector<unsigned char> a(70000), b(300000);
     size_t off = 0;
     while (off < total) {
         const size_t left = total - off;
-        if (rng() % 2) {
+        const unsigned pick = unsigned(rng() % 4);
+        if (pick == 3) {  // the block reader's receive: blocking WAITALL under SO_RCVTIMEO
+            size_t na = rng() % 600, nb = rng() % 250000;
+            if (na > left) na = left;
+            if (nb > left - na) nb = left - na;
+            if (net::recv_fully2(sv[0], a.data(), na, b.data(), nb)) return fail("recv_fully2");
+            if (std::memcmp(a.data(), src.data() + off, na) || std::memcmp(b.data(), src.data() + off + na, nb))
+                return fail("recv_fully2 bytes");
+            off += na + nb;
+        } else if (pick < 2) {
             size_t n = 1 + rng() % 250000;
             if (n > left) n = left;
             if (net::read_fully(sv[0], b.data(), n, 10000)) return fail("read_fully");
@@ -64,6 +74,9 @@ int main() {
     // a silent peer: both reads time out
     if (net::read_fully(sv[0], b.data(), 10, 200) != -ETIMEDOUT) return fail("read_fully timeout");
     if (net::read_fully2(sv[0], a.data(), 100, b.data(), 100000, 200) != -ETIMEDOUT) return fail("read_fully2 timeout");
+    if (net::set_recv_timeout(sv[0], 200)) return fail("set_recv_timeout 200");
+    if (net::recv_fully(sv[0], b.data(), 10) != -ETIMEDOUT) return fail("recv_fully timeout");
+    if (net::recv_fully2(sv[0], a.data(), 31, b.data(), 65536) != -ETIMEDOUT) return fail("recv_fully2 timeout");
     // EOF in the middle of a message
     if (net::write_fully(sv[1], src.data(), 5000, 1000)) return fail("write");
     shutdown(sv[1], SHUT_WR);
