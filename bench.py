@@ -1271,10 +1271,10 @@ def main():
                     extra["compute"][m]["frac_vs_verify"] = round(extra["compute"][m]["frac"] / v, 4)
         host_data = None
         if args.mode == "verify" and (not args.no_configs2 or not args.no_config5):
-            # a numpy-owned copy: numpy backs large arrays with transparent huge pages, torch's CPU tensors
-            # sit on 4 KiB pages. config5's loopback datanode serves the file from this buffer, and from 4 KiB
-            # pages its sending thread held one hdfsRead stream to 5.8-5.9 GiB/s against 7.8-7.9 from a numpy
-            # buffer on the same box, for the GPU path and the reference loop alike (profiles/r05/r5n)
+            # a numpy-owned copy (numpy asks for transparent huge pages on large arrays; torch's CPU tensors,
+            # by default, do not): config5's loopback datanode serves the file from this buffer, and served
+            # from the torch tensor one hdfsRead stream ran at 5.8-5.9 GiB/s against 7.8-7.9 in
+            # tools/e2e_read.py's numpy buffer on the same box (profiles/r05/r5n, r5o)
             host_data = np.empty(work.data.numel(), dtype=np.uint8)
             host_data[:] = work.data.view(-1).cpu().numpy()
         if args.mode == "verify" and not args.no_configs2:
