@@ -193,6 +193,8 @@ def main():
                     help="initialise torch's own HIP runtime on cuda:0 first (as bench.py's process has it)")
     ap.add_argument("--only-hdfsread", action="store_true", help="the single-stream hdfsRead lines only")
     ap.add_argument("--no-local", action="store_true", help="skip the short-circuit reader lines")
+    ap.add_argument("--reference", action="store_true",
+                    help="also the reference's read loop (oracle/_ref HWCrc32c) on the same stream: 1 and 8 threads")
     ap.add_argument("--readahead", default="1,2,3,7",
                     help="block read-ahead depths of the extra single-stream hdfsRead lines ('' = none)")
     args = ap.parse_args()
@@ -278,6 +280,39 @@ def main():
                 print(json.dumps({**line, "mode": mode, "verify": verify, "streams": 1 if mode == "hdfsRead"
                                   else args.blocks, "batch_packets": args.batch, "packet_kib": args.packet_kib,
                                   "gib_s": round(best, 2)}), flush=True)
+        if args.reference:
+            from loopback import reference_read_block
+
+            for streams in (1, args.blocks):
+                for verify in (True, False):
+                    best = 0.0
+                    for _ in range(args.reps):
+                        errors: list[str] = []
+
+                        def one(i):
+                            try:
+                                reference_read_block(dn.port, blocks[i][0], bsz, out, i * bsz, verify=verify)
+                            except Exception as e:  # noqa: BLE001 - reported
+                                errors.append(f"block {i}: {e}")
+
+                        t0 = time.perf_counter()
+                        if streams == 1:
+                            for i in range(args.blocks):
+                                one(i)
+                        else:
+                            th = [threading.Thread(target=one, args=(i,)) for i in range(args.blocks)]
+                            for t in th:
+                                t.start()
+                            for t in th:
+                                t.join()
+                        dt = time.perf_counter() - t0
+                        assert not errors, errors
+                        best = max(best, total / dt / GIB)
+                    assert np.array_equal(out, data)
+                    out[:] = 0
+                    print(json.dumps({**line, "mode": "reference_read_loop", "verify": verify, "streams": streams,
+                                      "engine": "oracle/_ref HWCrc32c (RemoteBlockReader loop)",
+                                      "gib_s": round(best, 2)}), flush=True)
         # single-stream hdfsRead with block read-ahead (hdfs3_input_set_readahead): blocks
         # i+1 .. i+D read and verified by background threads while block i is consumed
         def pool_mib():
