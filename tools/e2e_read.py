@@ -62,25 +62,39 @@ def diag(dn, blocks, out, data, args):
     from libhdfs3_amd.engine import BlockReader
 
     lib = _native.lab()
+    offs = np.cumsum([0] + [n for _, n in blocks])
     for verify in (True, False, True, False):
         acc = np.zeros(5, np.uint64)
-        t0 = time.perf_counter()
-        off = 0
-        for bid, n in blocks:
+        lock = threading.Lock()
+
+        def one(i):
+            bid, n = blocks[i]
             with BlockReader("127.0.0.1", dn.port, bid, 0, n, verify=verify, batch_packets=args.batch) as r:
                 pos = 0
                 while pos < n:
-                    got = r.read_into(out, off + pos, min(args.read_mib << 20, n - pos))
+                    got = r.read_into(out, int(offs[i]) + pos, min(args.read_mib << 20, n - pos))
                     assert got > 0
                     pos += got
                 t = (ctypes.c_uint64 * 5)()
                 _native.check("timing", lib.hdfs3x_block_reader_timing(r.r, t))
-                acc += np.array(list(t), np.uint64)
-            off += n
+                with lock:
+                    acc[:] += np.array(list(t), np.uint64)
+
+        t0 = time.perf_counter()
+        if args.diag_streams <= 1:  # one block after another on this thread
+            for i in range(len(blocks)):
+                one(i)
+        else:  # every block on its own thread (the parallel_pread shape)
+            th = [threading.Thread(target=one, args=(i,)) for i in range(len(blocks))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        off = int(offs[-1])
         dt = time.perf_counter() - t0
         assert np.array_equal(out[:off], data[:off])
-        print(json.dumps({"bench": "e2e_diag", "verify": verify, "gib_s": round(off / dt / GIB, 2),
-                          "wall_ms": round(dt * 1e3, 1),
+        print(json.dumps({"bench": "e2e_diag", "verify": verify, "streams": max(1, args.diag_streams),
+                          "gib_s": round(off / dt / GIB, 2), "wall_ms": round(dt * 1e3, 1),
                           **{k: round(float(v) / 1e6, 1) for k, v in
                              zip(["recv_ms", "alloc_ms", "launch_ms", "wait_ms", "deliver_ms"], acc)}}),
               flush=True)
@@ -188,6 +202,8 @@ def main():
                     help="short-circuit and read-ahead lines: untimed passes first (reported as cold_gib_s)")
     ap.add_argument("--read-mib", type=int, default=4, help="hdfsRead request size")
     ap.add_argument("--diag", action="store_true", help="per-phase timing of the block reader only")
+    ap.add_argument("--diag-streams", type=int, default=1,
+                    help="--diag: 1 = blocks one after another, >1 = every block on its own thread")
     ap.add_argument("--local-only", action="store_true", help="only the short-circuit reader lines")
     ap.add_argument("--torch", action="store_true",
                     help="initialise torch's own HIP runtime on cuda:0 first (as bench.py's process has it)")
