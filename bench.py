@@ -771,8 +771,40 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
             return {"gib_s": round(sorted(timed)[len(timed) // 2], 2), "gib_s_all": [round(r, 2) for r in timed],
                     "cold_gib_s": round(rates[0], 2), "unit": "GiB/s"}
 
-        lines["hdfsRead_verify"] = dict(measure(lambda: hdfs_read(True, 0)), readahead_blocks=0, verify=True)
-        lines["hdfsRead_no_verify"] = dict(measure(lambda: hdfs_read(False, 0)), readahead_blocks=0, verify=False)
+        def measure_paired(fa, fb):
+            # the GPU path and the reference loop pass by pass (A B A B ...), so that drift of the box
+            # (page cache, clocks, other tenants' load) falls on both alike; each with its untimed first pass
+            ra, rb = [], []
+            for rep in range(1 + reps):
+                for fn, rates in ((fa, ra), (fb, rb)):
+                    outbuf[::4096] = ~host_data[::4096]
+                    t0 = time.perf_counter()
+                    fn()
+                    dt = time.perf_counter() - t0
+                    if not np.array_equal(outbuf, host_data):
+                        bad = int(np.nonzero(outbuf != host_data)[0][0])
+                        raise SystemExit(f"PARITY FAILURE: config5 delivered a wrong byte at {bad}")
+                    rates.append(total / dt / 2**30)
+            out = []
+            for rates in (ra, rb):
+                timed = rates[1:]
+                out.append({"gib_s": round(sorted(timed)[len(timed) // 2], 2),
+                            "gib_s_all": [round(r, 2) for r in timed], "cold_gib_s": round(rates[0], 2),
+                            "unit": "GiB/s"})
+            ratios = sorted(a / b for a, b in zip(ra[1:], rb[1:]))
+            return out[0], out[1], round(ratios[len(ratios) // 2], 3)
+
+        paired = {}
+        if ref_lib() is not None:
+            for verify, gk, rk in ((True, "hdfsRead_verify", "reference_cpu_verify"),
+                                   (False, "hdfsRead_no_verify", "reference_cpu_no_verify")):
+                g, r, paired[verify] = measure_paired(lambda v=verify: hdfs_read(v, 0), lambda v=verify: ref_read(v))
+                lines[gk] = dict(g, readahead_blocks=0, verify=verify)
+                lines[rk] = dict(r, verify=verify, cores=1, kind="reference")
+        else:
+            lines["hdfsRead_verify"] = dict(measure(lambda: hdfs_read(True, 0)), readahead_blocks=0, verify=True)
+            lines["hdfsRead_no_verify"] = dict(measure(lambda: hdfs_read(False, 0)), readahead_blocks=0,
+                                               verify=False)
         lines["hdfsRead_verify_readahead2"] = dict(measure(lambda: hdfs_read(True, 2)), readahead_blocks=2,
                                                    verify=True)
         hp = ctypes.c_void_p()
@@ -788,11 +820,6 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
         lines["host_api_pageable"] = dict(measure(lambda: host_api(host_data), check_out=False),
                                           api="hdfs3_crc32c_verify on a pageable 1 GiB host buffer "
                                               "(staging copy + H2D + verify)")
-        if ref_lib() is not None:
-            lines["reference_cpu_verify"] = dict(measure(lambda: ref_read(True)), verify=True, cores=1,
-                                                 kind="reference")
-            lines["reference_cpu_no_verify"] = dict(measure(lambda: ref_read(False)), verify=False, cores=1,
-                                                    kind="reference")
         # the write direction (compute-on-write, H2D of the data + D2H of the words): hdfsWrite of the same
         # GiB in 1 MiB writes into a sink that reads the packets (tools/loopback's count sink), beside the
         # reference's write loop with its HWCrc32c on the writing thread (oracle/ref_driver.cpp
@@ -812,6 +839,10 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
                       "pass); host API passes must report the GiB clean"}
     if "reference_cpu_verify" in lines:
         out["gpu_over_reference_cpu"] = round(lines["hdfsRead_verify"]["gib_s"] / lines["reference_cpu_verify"]["gib_s"], 2)
+        # median over the timed passes of (GPU pass rate / the reference pass run right after it)
+        out["paired_gpu_over_reference_cpu"] = {"verify": paired[True], "no_verify": paired[False],
+                                                "how": "GPU and reference passes alternated; median of the "
+                                                       "per-pair rate ratios"}
         out["readahead2_over_reference_cpu"] = round(
             lines["hdfsRead_verify_readahead2"]["gib_s"] / lines["reference_cpu_verify"]["gib_s"], 2)
     return out
@@ -1291,7 +1322,7 @@ def main():
         except Exception as e:
             log("batched pass failed:", e)
     if world == 1 and args.mode == "verify" and not args.no_config5 and args.bpc == 512:
-        extra["config5"] = config5_block(torch, device, host_data, args.bpc, block_bytes)
+        extra["config5"] = config5_block(torch, device, host_data, args.bpc, block_bytes, reps=5)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(work, args.cpu_seconds, args.bpc, data=host_data)

@@ -54,7 +54,9 @@ def test_bench_json_line(mode):
     c5 = j["config5"]["lines"]
     for k in ("hdfsRead_verify", "hdfsRead_no_verify", "hdfsRead_verify_readahead2", "host_api_pinned",
               "host_api_pageable", "hdfsWrite_sink"):
-        assert c5[k]["gib_s"] > 0 and len(c5[k]["gib_s_all"]) == 3, k
+        assert c5[k]["gib_s"] > 0 and len(c5[k]["gib_s_all"]) == 5, k
     if "reference_cpu_verify" in c5:  # oracle/_ref travels with the tree when it was built
         assert c5["reference_cpu_verify"]["kind"] == "reference" and c5["reference_cpu_verify"]["gib_s"] > 0
         assert c5["reference_cpu_write_sink"]["gib_s"] > 0 and "checked" in c5["hdfsWrite_sink"]
+        pr = j["config5"]["paired_gpu_over_reference_cpu"]
+        assert pr["verify"] > 0 and pr["no_verify"] > 0
