@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--block-mib", type=int, default=128)
     ap.add_argument("--verify", type=int, default=1)
+    ap.add_argument("--modes", default="hdfsRead,parallel_pread")
     args = ap.parse_args()
 
     from e2e_read import pread_block
@@ -69,6 +70,8 @@ def main():
 
     try:
         for name, fn in (("hdfsRead", one_stream), ("parallel_pread", eight_streams)):
+            if name not in args.modes.split(","):
+                continue
             rates = {"0": [], "1": []}
             for rep in range(1 + args.reps):
                 for val in ("0", "1"):
