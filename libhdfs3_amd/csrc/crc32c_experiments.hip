@@ -57,6 +57,8 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabNoStage>(a, tab, fold, grid_cap, s);
         case 130:  // compute: staged words at every size, written out window by window (kLabStageWin)
             return launch_wave3<BPC, V, false, true, kLabStageWin>(a, tab, fold, grid_cap, s);
+        case 157:  // the round-4 chains (16 table steps, the fold on the finished state; kLabFull16)
+            return launch_wave3<BPC, V, false, true, kLabFull16>(a, tab, fold, grid_cap, s);
         case 128:  // compute: staged words through plain global stores (production before round 4)
             return launch_wave3<BPC, V, false, true, kLabStorePlain>(a, tab, fold, grid_cap, s);
         case 146:  // production with every wave's fill-done and first-data times (wave_spread.py --variant 146 --mid)

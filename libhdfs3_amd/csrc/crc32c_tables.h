@@ -90,6 +90,21 @@ inline void build_fold_nibbles(const uint32_t fold[kFoldWords], int set, uint32_
     }
 }
 
+// The round kernel's sets take a chain's state BEFORE its last word's table step (round 5): lane j's
+// 16-word chain ends in x = s ^ w15, whose finished state is T(x) (T = the 4-byte slice-by-4 step,
+// linear), so the entry M_j(T(e << 4k)) folds T into the lane fold and the kernel skips the last
+// word's 4 lookups (64 -> 60 slice lookups per lane and round).
+inline void build_fold_nibbles_pre(const uint32_t t0[kTableEntries], const uint32_t fold[kFoldWords], int set,
+                                   uint32_t out[kFoldNibbleWords]) {
+    const int g = kFoldGs[set];
+    for (int lane = 0; lane < 64; ++lane) {
+        const uint32_t *cols = fold + (kFoldOffset[set] + lane % g) * 32;
+        for (int k = 0; k < 8; ++k)
+            for (uint32_t e = 0; e < 16; ++e)
+                out[(k * 16 + e) * 64 + lane] = apply_cols(cols, advance_bytes(t0, e << (4 * k), 4));
+    }
+}
+
 // Affine lane-fold nibble sets (the production round kernel, crc32c_wave.h): the sets above with
 // the chunk's init and final xor folded in. By linearity the CRC of a chunk of C = 64 G bytes is
 //   ~state(init ~0) = crc0 ^ A^C(~0) ^ ~0,   crc0 = XOR_j M_j(x_j) over chains started from 0,
@@ -100,8 +115,10 @@ inline void build_fold_nibbles(const uint32_t fold[kFoldWords], int set, uint32_
 // round to compare or store them).
 // The device fold image is the kFoldWords matrix columns followed by the 4 affine sets.
 constexpr int kFoldAffineOff = kFoldWords;
-constexpr int kFoldImageWords = kFoldAffineOff + 4 * kFoldNibbleWords;
-// `out` holds set `set` built by build_fold_nibbles; adds K_C in place
+// (lab A/B, round 5: the round-4 sets on the chain's finished state follow at kFoldAffineOldOff)
+constexpr int kFoldAffineOldOff = kFoldAffineOff + 4 * kFoldNibbleWords;
+constexpr int kFoldImageWords = kFoldAffineOldOff + 4 * kFoldNibbleWords;
+// `out` holds set `set` built by build_fold_nibbles_pre; adds K_C in place
 inline void build_fold_affine(const uint32_t t0[kTableEntries], int set, uint32_t out[kFoldNibbleWords]) {
     const int g = kFoldGs[set];
     const uint32_t kc = advance_bytes(t0, 0xFFFFFFFFu, uint64_t(64) * g) ^ 0xFFFFFFFFu;

@@ -44,6 +44,7 @@ constexpr int kLabClock = 4096;     // clock stamps of workgroup 0 (LabClock, cr
 constexpr int kLabStorePlain = 8192;  // compute, staged words: plain global stores (production before round 4)
 constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every launch size (production before round 4)
 constexpr int kLabNoTabLoad = 2097152;  // diagnostic: the table images are not loaded (made up from t: wrong results)
+constexpr int kLabFull16 = 8388608;  // the round-4 chains: 16 table steps per chain, the fold on the finished state
 constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = fill done | first data << 21 | kernel
                                      // arguments landed << 42, each - start, 21 bits of 10 ns
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
@@ -443,21 +444,37 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         if constexpr (NOMATH) return Look{{x, 0u, 0u, 0u}};
         return lookups(t, x);
     };
-    // two interleaved chains over c0, c1 (chain 1's 4 reads fly while chain 0 folds)
+    // two interleaved chains over c0, c1 (chain 1's 4 reads fly while chain 0 folds). A chain ends in
+    // x = state ^ w15, before the last word's table step: the lane fold's image carries that step
+    // (build_fold_nibbles_pre), 60 lookups per lane and round instead of 64
     auto chains = [&](Round &c0, Round &c1, uint32_t &x0, uint32_t &x1) {
         x0 = word(c0, 0);
         x1 = word(c1, 0);
         Look l0 = look(x0), l1;
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr ((LAB & kLabFull16) != 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < 16; ++i) {
+                l1 = look(x1);
+                __builtin_amdgcn_sched_barrier(0);
+                x0 = combine(l0, i < 15 ? word(c0, i < 15 ? i + 1 : 15) : 0u);
+                __builtin_amdgcn_sched_barrier(0);
+                if (i < 15) l0 = look(x0);
+                __builtin_amdgcn_sched_barrier(0);
+                x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < 15; ++i) {
             l1 = look(x1);
             __builtin_amdgcn_sched_barrier(0);
-            x0 = combine(l0, i < 15 ? word(c0, i < 15 ? i + 1 : 15) : 0u);
+            x0 = combine(l0, word(c0, i + 1));
             __builtin_amdgcn_sched_barrier(0);
-            if (i < 15) l0 = look(x0);
+            if (i < 14) l0 = look(x0);
             __builtin_amdgcn_sched_barrier(0);
-            x1 = combine(l1, i < 15 ? word(c1, i < 15 ? i + 1 : 15) : 0u);
+            x1 = combine(l1, word(c1, i + 1));
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -465,8 +482,13 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // identical code otherwise gets tail-merged into one copy that both run (register copies in).
     auto solo = [&](Round &c, const WView &v, uint32_t k, uint32_t w, auto id) {
         uint32_t x = word(c, 0);
+        if constexpr ((LAB & kLabFull16) != 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) x = combine(look(x), i < 15 ? word(c, i < 15 ? i + 1 : 15) : 0u);
+            for (int i = 0; i < 16; ++i) x = combine(look(x), i < 15 ? word(c, i < 15 ? i + 1 : 15) : 0u);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 15; ++i) x = combine(look(x), word(c, i + 1));
+        }
         finish(k, v, group_xor<G>(fold(x)), w);
         if constexpr (decltype(id)::value == 0) asm volatile("; solo round 0" ::: "memory");
         else asm volatile("; solo round 1" ::: "memory");
@@ -714,7 +736,7 @@ template <int BPC, bool V, bool PITCH, bool SOLO, int LAB = 0, int TPB = kBlockT
 hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *fold, int grid_cap, hipStream_t s) {
     constexpr int G = BPC / 64;
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
-    const uint32_t *nib = fold + kFoldAffineOff + set * kFoldNibbleWords;
+    const uint32_t *nib = fold + ((LAB & kLabFull16) ? kFoldAffineOldOff : kFoldAffineOff) + set * kFoldNibbleWords;
     const uint64_t units = PITCH ? ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes : a.len / kRoundBytes;
     const uint64_t need = (units + 2 * (TPB / 64) - 1) / (2 * (TPB / 64));
     int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
@@ -768,7 +790,7 @@ template <int BPC, bool V, int LAB = 0>
 hipError_t launch_segments3(const SegLaunch &L, const uint32_t *tab, const uint32_t *fold, int grid, hipStream_t s) {
     constexpr int G = BPC / 64;
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
-    const uint32_t *nib = fold + kFoldAffineOff + set * kFoldNibbleWords;
+    const uint32_t *nib = fold + ((LAB & kLabFull16) ? kFoldAffineOldOff : kFoldAffineOff) + set * kFoldNibbleWords;
     if (L.uniform)
         hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, true, LAB>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab,
                            nib);

@@ -66,8 +66,11 @@ const HostImage *host_images() {
             build_fold_matrices(img[p].t[0], img[p].fold);
             for (int set = 0; set < 4; ++set) {
                 uint32_t *nib = img[p].fold + kFoldAffineOff + set * kFoldNibbleWords;
-                build_fold_nibbles(img[p].fold, set, nib);
+                build_fold_nibbles_pre(img[p].t[0], img[p].fold, set, nib);
                 build_fold_affine(img[p].t[0], set, nib);
+                uint32_t *old = img[p].fold + kFoldAffineOldOff + set * kFoldNibbleWords;
+                build_fold_nibbles(img[p].fold, set, old);
+                build_fold_affine(img[p].t[0], set, old);
             }
         }
     });

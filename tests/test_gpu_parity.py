@@ -357,7 +357,8 @@ def test_compute_staged_windows_lab(lab_ctx, bpc, n):
 # variants exist for the round kernel's chunk sizes only
 @pytest.mark.parametrize("variant,bpc", [(0, b) for b in (512, 1024, 2048, 4096, 8192)] +
                          [(v, b) for v in (92, 93, 94, 95, 115, 117) for b in (512, 1024, 2048, 4096)] +
-                         [(115, 8192), (122, 512), (122, 2048)])
+                         [(115, 8192), (122, 512), (122, 2048)] +
+                         [(157, b) for b in (512, 1024, 2048, 4096)])
 def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
     """All kernel designs kept for A/B (hdfs3x_set_variant) are parity-checked too:
     whole rounds, the slow region (len not a multiple of the 4 KiB round) and the tail."""
@@ -385,7 +386,7 @@ def test_every_kernel_variant_matches_oracle(lab_ctx, variant, bpc):
         lib.hdfs3x_set_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93, 94, 115, 117, 125, 132, 134, 137, 146])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 115, 117, 125, 132, 134, 137, 146, 157])
 @pytest.mark.parametrize("bpc", [512, 2048, 4096])
 def test_round_kernel_variants_overlapped_match_oracle(lab_ctx, variant, bpc):
     """The round kernel's prefetch/last-step variants as they run in the bench: overlapped
@@ -593,7 +594,7 @@ def test_host_api_random_sizes_and_offsets(gpu_ctx):
         assert gpu_ctx.verify(bad, bpc, want, True) == pos // bpc, (n, off, bpc, pos)
 
 
-@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95, 122, 128])
+@pytest.mark.parametrize("variant", [0, 92, 93, 94, 95, 122, 128, 157])
 @pytest.mark.parametrize("bpc", [512, 4096])
 def test_round_kernel_variants_overlapped_compute_match_oracle(lab_ctx, variant, bpc):
     """Compute-mode variants of the round kernel (held stores or not, solo last step or not) as
