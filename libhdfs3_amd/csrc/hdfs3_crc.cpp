@@ -51,6 +51,13 @@ namespace hdfs3crc {
 // Per polynomial ([0] CRC32C, [1] CRC32): slice tables, then the fold image (kFoldWords
 // matrix columns, then the 4 affine nibble-table sets for G = 8, 16, 32, 64 of the round
 // kernel), built once per process.
+// the device copy: the product stops before the lab-only sets
+#if HDFS3_LAB
+constexpr size_t kFoldUploadBytes = sizeof(uint32_t) * kFoldImageWords;
+#else
+constexpr size_t kFoldUploadBytes = sizeof(uint32_t) * kFoldAffineOldOff;
+#endif
+
 struct HostImage {
     uint32_t t[kSlices][kTableEntries];
     uint32_t fold[kFoldImageWords];
@@ -68,9 +75,11 @@ const HostImage *host_images() {
                 uint32_t *nib = img[p].fold + kFoldAffineOff + set * kFoldNibbleWords;
                 build_fold_nibbles_pre(img[p].t[0], img[p].fold, set, nib);
                 build_fold_affine(img[p].t[0], set, nib);
+#if HDFS3_LAB  // the round-4 sets of lab variant 157; the product never reads them (nor uploads them)
                 uint32_t *old = img[p].fold + kFoldAffineOldOff + set * kFoldNibbleWords;
                 build_fold_nibbles(img[p].fold, set, old);
                 build_fold_affine(img[p].t[0], set, old);
+#endif
             }
         }
     });
@@ -491,10 +500,10 @@ int hdfs3_crc_ctx_create(int device, hdfs3_crc_ctx **out) {
     const HostImage *img = host_images();
     for (int p = 0; p < 2; ++p) {
         if (hipMalloc(reinterpret_cast<void **>(&ctx->d_tables_by[p]), sizeof(img[p].t)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&ctx->d_fold_by[p]), sizeof(img[p].fold)) != hipSuccess)
+            hipMalloc(reinterpret_cast<void **>(&ctx->d_fold_by[p]), kFoldUploadBytes) != hipSuccess)
             return bail(fail(-ENOMEM, "device allocation for ctx failed"));
         if (hipMemcpy(ctx->d_tables_by[p], img[p].t, sizeof(img[p].t), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(ctx->d_fold_by[p], img[p].fold, sizeof(img[p].fold), hipMemcpyHostToDevice) != hipSuccess)
+            hipMemcpy(ctx->d_fold_by[p], img[p].fold, kFoldUploadBytes, hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(-EIO, "table upload failed"));
     }
     ctx->d_tables = ctx->d_tables_by[0];
@@ -597,7 +606,7 @@ Footprint footprint(hdfs3_crc_ctx *ctx) {
     }
     f.pinned += sizeof(unsigned long long);
     f.device += ctx->words.cap + sizeof(unsigned long long);
-    for (int p = 0; p < 2; ++p) f.device += sizeof(host_images()[p].t) + sizeof(host_images()[p].fold);
+    for (int p = 0; p < 2; ++p) f.device += sizeof(host_images()[p].t) + kFoldUploadBytes;
     return f;
 }
 
