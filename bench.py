@@ -500,6 +500,7 @@ def packets_block(torch, work, ctx, K, W, stream, reps=3):
     out["checked"] = "every launch's result slot after the timed regions; a flipped bit located before them"
     del arena
     out["reader_batch"] = reader_batch_layouts(torch, work, ctx, stream)
+    out["writer_batch"] = writer_batch_layout(torch, work, ctx, stream)
     return out
 
 
@@ -563,6 +564,113 @@ def reader_batch_layouts(torch, work, ctx, stream, npk=64, nbat=16, reps=5, n=20
             "dense_frac": round(alg / (dm * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
             "how": f"{nbat} resident batches rotating, {reps} x (wire region, dense region) of 50 warmup + {n} "
                    "timed barriered launches; medians; every result slot checked"}
+
+
+WRITER_HEADER = 31  # PacketHeader::GetPkHeaderLen (PacketHeader.cpp:38)
+
+
+def writer_batch_layout(torch, work, ctx, stream, npk=64, nbat=16, reps=5, n=200):
+    """The output stream's own GPU unit (output_stream.cpp dispatch): one batch of 64 packets of 127
+    chunks at bpc 512 (computePacketChunkSize at the default 64 KiB packet, OutputStreamImpl.cpp:161-170;
+    65,024 B = 15 whole rounds + 3,584 B), compute-on-write by one barriered launch of
+    hdfs3_crc32c_compute_packets_dev_async over the batch's descriptors, in the writer's device layout:
+    packet slots [lead: header + words room][data] at one stride, the batch's words compact after the
+    slots. `nbat` batches rotate (device-resident). Paired, region by region, with the reader's dense
+    4 MiB batch verify (`reps` x (writer region, reader region) of `n` barriered launches; medians), and
+    the same batches verified (verify_packets_dev_async) for the symmetric read-side number. The words
+    are checked against block 0's (the packets are its consecutive chunk-aligned slices)."""
+    bpc, plen0 = 512, 65536
+    with_sum = bpc + 4
+    cpp = max(1, (plen0 - WRITER_HEADER + with_sum - 1) // with_sum)
+    plen = cpp * bpc
+    lead = (WRITER_HEADER + 4 * cpp + 15) // 16 * 16
+    stride = lead + (plen + 15) // 16 * 16
+    crc_region = stride * npk
+    span = crc_region + 4 * cpp * npk
+    span += (-span) % 4096
+    dev = work.data.device
+    if nbat * npk * plen > work.block_bytes:
+        return None
+    src = work.data[0, :nbat * npk * plen].view(nbat, npk, plen)
+    want = work.crc[0, :nbat * npk * cpp * 4].view(nbat, npk * cpp * 4)
+    arena = torch.zeros((nbat, span), dtype=torch.uint8, device=dev)
+    arena[:, :crc_region].view(nbat, npk, stride)[:, :, lead:lead + plen] = src
+    arena[:, crc_region:crc_region + 4 * cpp * npk] = want  # stored words for the verify leg
+    # the reader's dense batch (64 x 64 KiB + its words), as reader_batch_layouts lays it
+    rsrc = work.data[0, :nbat * 64 * plen0].view(nbat, -1)
+    rwords = work.crc[0, :nbat * 64 * 512].view(nbat, -1)
+    d0 = 64 * 512
+    dense = torch.empty((nbat, d0 + 64 * plen0), dtype=torch.uint8, device=dev)
+    dense[:, :d0] = rwords
+    dense[:, d0:] = rsrc
+    torch.cuda.synchronize()
+    from libhdfs3_amd.engine import CrcContext
+    descs = CrcContext._descs([(lead + stride * p, crc_region + 4 * cpp * p, plen) for p in range(npk)])
+    res = torch.zeros(256, dtype=torch.int64, device=dev)
+    rp, ab, db, dspan = res.data_ptr(), arena.data_ptr(), dense.data_ptr(), d0 + 64 * plen0
+
+    def w_compute(i):
+        ctx.compute_packets_dev_async(ab + (i % nbat) * span, span, descs, bpc)
+
+    def w_verify(i):
+        ctx.verify_packets_dev_async(ab + (i % nbat) * span, span, descs, bpc, rp + 8 * (i % 256))
+
+    def r_launch(i):
+        b = db + (i % nbat) * dspan
+        ctx.verify_dev_async(b + d0, 64 * plen0, bpc, b, rp + 8 * (i % 256))
+
+    def region(fn):
+        for i in range(50):
+            fn(i)
+        settle(torch, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(n):
+            fn(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / n
+
+    # the gate: a flipped bit in the partial round of packet 9 of batch 3 comes back as its key
+    q = 61440 + 3 * bpc + 17
+    pos = (3, lead + stride * 9 + q)
+    orig = int(arena[pos].item())
+    arena[pos] = orig ^ 0x08
+    torch.cuda.synchronize()
+    w_verify(3)
+    torch.cuda.synchronize()
+    got = int(res[3].item())
+    arena[pos] = orig
+    res.zero_()
+    torch.cuda.synchronize()
+    if got == 0 or ((~got) & (2**64 - 1)) != (9 << 32) | (q // bpc):
+        raise SystemExit(f"PARITY FAILURE: writer batch reported {got:#x} for a flip in packet 9 chunk {q // bpc}")
+    arena[:, crc_region:crc_region + 4 * cpp * npk] = 0
+    c, rv, wv = [], [], []
+    for _ in range(reps):
+        c.append(region(w_compute))
+        rv.append(region(r_launch))
+        wv.append(region(w_verify))
+    if not bool(torch.equal(arena[:, crc_region:crc_region + 4 * cpp * npk], want)):
+        raise SystemExit("PARITY FAILURE: the writer batches' computed words differ from the block's")
+    if bool((res != 0).any().item()):
+        raise SystemExit("PARITY FAILURE: clean writer / reader batches reported a bad chunk")
+    cm, rm, vm = (sorted(x)[reps // 2] for x in (c, rv, wv))
+    alg = npk * cpp * (bpc + 4)
+    ralg = 64 * (plen0 // bpc) * (bpc + 4)
+    del arena, dense
+    return {"packets_per_batch": npk, "chunks_per_packet": cpp, "packet_data_bytes": plen,
+            "slot_stride": stride, "batch_payload_bytes": npk * plen, "alg_bytes": alg,
+            "api": "hdfs3_crc32c_compute_packets_dev_async (descriptors; the output stream's launch_packet_batch)",
+            "launch": "barriered, one per batch",
+            "compute_us": round(cm, 2), "verify_us": round(vm, 2), "reader_dense_us": round(rm, 2),
+            "compute_frac": round(alg / (cm * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+            "verify_frac": round(alg / (vm * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+            "compute_vs_reader_dense": round(cm / rm, 4),
+            "compute_vs_reader_dense_per_byte": round((cm / alg) / (rm / ralg), 4),
+            "how": f"{nbat} resident batches rotating, {reps} x (writer compute, reader dense verify, writer "
+                   f"verify) regions of 50 warmup + {n} timed barriered launches; medians; words and result "
+                   "slots checked"}
 
 
 def paired_regions(torch, work, ctx, stream, n, overlap, dst, reps=3):
@@ -696,21 +804,28 @@ def configs2_block(torch, work, ctx, stream, K, host_data, reps=3, warm=120, bpc
     return out
 
 
-def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4):
+def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4, dn=None, reads_only=False):
     """BASELINE.json configs[4]: a 1 GiB file of 128 MiB blocks served by the loopback datanode over
     127.0.0.1 TCP (64 KiB packets, test infrastructure), read end to end through the product's hdfsRead
     (hdfs3_input_read, 4 MiB reads: InputStreamImpl's block walk -> the block reader's receiver ->
     pinned arena -> H2D -> GPU verify -> caller buffer), i.e. PCIe-inclusive: verify on, verify off,
-    and block read-ahead 2 (hdfs3_input_set_readahead); the host API on the same GiB
-    (hdfs3_crc32c_verify: pinned and pageable host buffers, H2D-inclusive). Beside them, the
-    reference CPU path on the same packet stream: RemoteBlockReader's receive -> verifyChecksum ->
-    copy loop on the reading thread with the reference's own HWCrc32c (oracle/_ref; test
-    infrastructure, this baseline leg only; RemoteBlockReader.cpp:226-357), verify on and off. The write
-    direction (compute-on-write: H2D of the data, D2H of the words): hdfsWrite of the GiB into a sink, beside
-    the reference's write loop (OutputStreamImpl::appendInternal + Packet, its HWCrc32c) into the same sink.
-    Every line: one untimed first pass (reported as cold), then `reps` timed passes (median and all);
-    every pass's output buffer is compared with the file, byte for byte."""
+    and block read-ahead 2 (hdfs3_input_set_readahead); 8 concurrent hdfsPreads of one block each (8
+    streams, one thread and one InputStream each); the host API on the same GiB (hdfs3_crc32c_verify:
+    pinned and pageable host buffers, H2D-inclusive). Beside them, the reference CPU path on the same
+    packet stream: RemoteBlockReader's receive -> verifyChecksum -> copy loop on the reading thread with
+    the reference's own HWCrc32c (oracle/_ref; test infrastructure, this baseline leg only;
+    RemoteBlockReader.cpp:226-357), verify on and off, on 1 and on 8 threads. The write direction
+    (compute-on-write: H2D of the data, D2H of the words): hdfsWrite of the GiB into a sink, beside the
+    reference's write loop (OutputStreamImpl::appendInternal + Packet, its HWCrc32c) into the same sink.
+
+    Round 6: the datanode runs in its own process (`dn`, tools/loopback/serve.py, started before this
+    process touched the GPU), so its sender threads are not charged to the client, and every read line
+    carries CPU-seconds per GiB: the client's (this process: time.process_time over the pass, every
+    thread) and the datanode's (the child's getrusage). Every line: one untimed first pass (cold), then
+    `reps` timed passes (median and all); every pass's output buffer is compared with the file, byte
+    for byte. GPU and reference lines of one shape are timed pass by pass alternately (paired)."""
     import ctypes
+    import threading
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from loopback import LoopbackDatanode, reference_read_block
@@ -721,19 +836,25 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
     total = host_data.nbytes
     nblk = total // block_bytes
     crc_host = None
-    dn = LoopbackDatanode(packet_bytes=65536)
+    own_dn = dn is None
+    if own_dn:
+        dn = LoopbackDatanode(packet_bytes=65536)
     outbuf = np.empty(total, dtype=np.uint8)
     lines = {}
     dev = device.index or 0
     try:
         hctx = CrcContext(dev)  # the host API's own ctx (its pinned staging ring)
         crc_host = hctx.compute(host_data, bpc)  # the .meta words the datanode serves (GPU compute)
-        blocks = []
-        for i in range(nblk):
-            dn.add_block(100 + i, host_data[i * block_bytes:(i + 1) * block_bytes],
-                         crc_host[4 * (i * block_bytes // bpc):4 * ((i + 1) * block_bytes // bpc)], bpc)
-            blocks.append((100 + i, block_bytes))
+        blocks = [(100 + i, block_bytes) for i in range(nblk)]
+        if own_dn:
+            for i in range(nblk):
+                dn.add_block(100 + i, host_data[i * block_bytes:(i + 1) * block_bytes],
+                             crc_host[4 * (i * block_bytes // bpc):4 * ((i + 1) * block_bytes // bpc)], bpc)
+        else:
+            dn.share_blocks(host_data, crc_host, [(100 + i, i * block_bytes, block_bytes) for i in range(nblk)], bpc,
+                            tag="c5")
         located = [(b, nb, [("127.0.0.1", dn.port)]) for b, nb in blocks]
+        dn_cpu = (lambda: dn.cpu_seconds()) if not own_dn else (lambda: 0.0)
 
         def hdfs_read(verify, ahead):
             with InputStream(located, device=dev, verify=verify, batch_packets=64) as s:
@@ -746,67 +867,122 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
                         raise SystemExit(f"config5: hdfsRead returned {got} at {pos}")
                     pos += got
 
+        def threads(fn):
+            errs = []
+
+            def one(i):
+                try:
+                    fn(i)
+                except Exception as e:  # noqa: BLE001 - reported below
+                    errs.append(f"block {i}: {e}")
+            th = [threading.Thread(target=one, args=(i,)) for i in range(nblk)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            if errs:
+                raise SystemExit("config5: " + "; ".join(errs))
+
+        def hdfs_pread8(verify):
+            def one(i):
+                with InputStream(located, device=dev, verify=verify, batch_packets=64) as s:
+                    got = s.pread_into(i * block_bytes, outbuf, i * block_bytes, block_bytes)
+                    if got != block_bytes:
+                        raise OSError(f"short pread {got}")
+            threads(one)
+
         def ref_read(verify):
             for i, (b, nb) in enumerate(blocks):
                 reference_read_block(dn.port, b, nb, outbuf, i * block_bytes, verify=verify)
+
+        def ref_read8(verify):
+            threads(lambda i: reference_read_block(dn.port, blocks[i][0], block_bytes, outbuf, i * block_bytes,
+                                                   verify=verify))
 
         def host_api(buf):
             bad = hctx.verify(buf, bpc, crc_host)
             if bad != -1:
                 raise SystemExit(f"PARITY FAILURE: config5 host API reported chunk {bad} on a clean GiB")
 
+        phase_buf = (ctypes.c_uint64 * 8)()
+
+        def reader_phases():  # the block readers closed since the last call (hdfs3_reader_phase_ns)
+            _native.check("hdfs3_reader_phase_ns", _native.lib().hdfs3_reader_phase_ns(phase_buf, 8, 1))
+            return [int(x) for x in phase_buf]
+
+        def one_pass(fn, check_out=True):
+            if check_out:
+                outbuf[::4096] = ~host_data[::4096]  # poison: every pass must rewrite the buffer
+            reader_phases()
+            c0, d0 = time.process_time(), dn_cpu()
+            t0 = time.perf_counter()
+            fn()
+            dt = time.perf_counter() - t0
+            c1, d1 = time.process_time(), dn_cpu()
+            ph = reader_phases()
+            if check_out and not np.array_equal(outbuf, host_data):
+                bad = int(np.nonzero(outbuf != host_data)[0][0])
+                raise SystemExit(f"PARITY FAILURE: config5 delivered a wrong byte at {bad}")
+            gib = total / 2**30
+            return (total / dt / 2**30, (c1 - c0) / gib, (d1 - d0) / gib) + tuple(x * 1e-9 / gib for x in ph)
+
+        phase_names = ("recv", "arena", "launch", "gpu_wait", "copy_out", "rx_wait_free_slot",
+                       "caller_wait_batch", "receiver_cpu")
+
+        def summary(passes):
+            timed = passes[1:]
+            med = lambda k: sorted(x[k] for x in timed)[len(timed) // 2]
+            out = {"gib_s": round(med(0), 2), "gib_s_all": [round(x[0], 2) for x in timed],
+                   "cold_gib_s": round(passes[0][0], 2), "unit": "GiB/s",
+                   "client_cpu_s_per_gib": round(med(1), 4)}
+            if not own_dn:
+                out["datanode_cpu_s_per_gib"] = round(med(2), 4)
+            if any(x[3 + i] for x in timed for i in range(8)):
+                # summed over the pass's block readers (threads): seconds per GiB delivered
+                out["reader_phase_s_per_gib"] = {n: round(med(3 + i), 4) for i, n in enumerate(phase_names)}
+            return out
+
         def measure(fn, check_out=True):
-            rates = []
-            for rep in range(1 + reps):
-                if check_out:
-                    outbuf[::4096] = ~host_data[::4096]  # poison: every pass must rewrite the buffer
-                t0 = time.perf_counter()
-                fn()
-                dt = time.perf_counter() - t0
-                if check_out and not np.array_equal(outbuf, host_data):
-                    bad = int(np.nonzero(outbuf != host_data)[0][0])
-                    raise SystemExit(f"PARITY FAILURE: config5 delivered a wrong byte at {bad}")
-                rates.append(total / dt / 2**30)
-            timed = rates[1:]
-            return {"gib_s": round(sorted(timed)[len(timed) // 2], 2), "gib_s_all": [round(r, 2) for r in timed],
-                    "cold_gib_s": round(rates[0], 2), "unit": "GiB/s"}
+            return summary([one_pass(fn, check_out) for _ in range(1 + reps)])
 
         def measure_paired(fa, fb):
             # the GPU path and the reference loop pass by pass (A B A B ...), so that drift of the box
             # (page cache, clocks, other tenants' load) falls on both alike; each with its untimed first pass
-            ra, rb = [], []
+            pa, pb = [], []
             for rep in range(1 + reps):
-                for fn, rates in ((fa, ra), (fb, rb)):
-                    outbuf[::4096] = ~host_data[::4096]
-                    t0 = time.perf_counter()
-                    fn()
-                    dt = time.perf_counter() - t0
-                    if not np.array_equal(outbuf, host_data):
-                        bad = int(np.nonzero(outbuf != host_data)[0][0])
-                        raise SystemExit(f"PARITY FAILURE: config5 delivered a wrong byte at {bad}")
-                    rates.append(total / dt / 2**30)
-            out = []
-            for rates in (ra, rb):
-                timed = rates[1:]
-                out.append({"gib_s": round(sorted(timed)[len(timed) // 2], 2),
-                            "gib_s_all": [round(r, 2) for r in timed], "cold_gib_s": round(rates[0], 2),
-                            "unit": "GiB/s"})
-            ratios = sorted(a / b for a, b in zip(ra[1:], rb[1:]))
-            return out[0], out[1], round(ratios[len(ratios) // 2], 3)
+                pa.append(one_pass(fa))
+                pb.append(one_pass(fb))
+            ratios = sorted(a[0] / b[0] for a, b in zip(pa[1:], pb[1:]))
+            cpu_ratios = sorted(a[1] / b[1] for a, b in zip(pa[1:], pb[1:]) if b[1] > 0)
+            return summary(pa), summary(pb), {"rate": round(ratios[len(ratios) // 2], 3),
+                                              "client_cpu": round(cpu_ratios[len(cpu_ratios) // 2], 3)
+                                              if cpu_ratios else None}
 
         paired = {}
         if ref_lib() is not None:
             for verify, gk, rk in ((True, "hdfsRead_verify", "reference_cpu_verify"),
                                    (False, "hdfsRead_no_verify", "reference_cpu_no_verify")):
-                g, r, paired[verify] = measure_paired(lambda v=verify: hdfs_read(v, 0), lambda v=verify: ref_read(v))
-                lines[gk] = dict(g, readahead_blocks=0, verify=verify)
-                lines[rk] = dict(r, verify=verify, cores=1, kind="reference")
+                g, r, paired[("1", verify)] = measure_paired(lambda v=verify: hdfs_read(v, 0),
+                                                             lambda v=verify: ref_read(v))
+                lines[gk] = dict(g, readahead_blocks=0, verify=verify, streams=1)
+                lines[rk] = dict(r, verify=verify, streams=1, cores=1, kind="reference")
+            for verify, gk, rk in ((True, "hdfsPread8_verify", "reference_cpu8_verify"),
+                                   (False, "hdfsPread8_no_verify", "reference_cpu8_no_verify")):
+                g, r, paired[("8", verify)] = measure_paired(lambda v=verify: hdfs_pread8(v),
+                                                             lambda v=verify: ref_read8(v))
+                lines[gk] = dict(g, verify=verify, streams=nblk, api="hdfs3_input_pread of one whole block per "
+                                                                     "thread, one InputStream each")
+                lines[rk] = dict(r, verify=verify, streams=nblk, cores=nblk, kind="reference")
         else:
             lines["hdfsRead_verify"] = dict(measure(lambda: hdfs_read(True, 0)), readahead_blocks=0, verify=True)
             lines["hdfsRead_no_verify"] = dict(measure(lambda: hdfs_read(False, 0)), readahead_blocks=0,
                                                verify=False)
+            lines["hdfsPread8_verify"] = dict(measure(lambda: hdfs_pread8(True)), verify=True, streams=nblk)
         lines["hdfsRead_verify_readahead2"] = dict(measure(lambda: hdfs_read(True, 2)), readahead_blocks=2,
                                                    verify=True)
+        if reads_only:  # tools/config5_ab.py: the read lines only
+            return {"lines": lines, "paired": {f"{k[0]}_{'verify' if k[1] else 'no_verify'}": v
+                                               for k, v in paired.items()}}
         hp = ctypes.c_void_p()
         _native.check("hdfs3_host_malloc_pinned", _native.lib().hdfs3_host_malloc_pinned(ctypes.byref(hp), total))
         try:
@@ -827,10 +1003,15 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
         lines.update(write_lines(host_data, bpc, block_bytes, dev, reps))
         hctx.close()
     finally:
-        dn.stop()
+        if own_dn:
+            dn.stop()
     out = {"workload": f"{total >> 20} MiB file = {nblk} x {block_bytes >> 20} MiB blocks, {bpc} B chunks, "
                        f"64 KiB packets from a loopback datanode on 127.0.0.1 (test infrastructure), "
-                       f"{read_mib} MiB hdfsRead calls, one stream",
+                       f"{read_mib} MiB hdfsRead calls (1 stream) or {nblk} concurrent whole-block hdfsPreads",
+           "datanode": ("a child process (tools/loopback/serve.py), started before the bench touched the GPU; "
+                        "its CPU time is datanode_cpu_s_per_gib" if not own_dn else
+                        "in this process (its threads are charged to client_cpu_s_per_gib)"),
+           "cpu_quota_cores": cpu_quota_cores(),
            "lines": lines,
            "reference_cpu": ("RemoteBlockReader's loop on the reading thread (receive a packet, verifyChecksum "
                              "with the reference HWCrc32c built from src/common/HWCrc32c.cpp, copy to the caller; "
@@ -839,10 +1020,15 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
                       "pass); host API passes must report the GiB clean"}
     if "reference_cpu_verify" in lines:
         out["gpu_over_reference_cpu"] = round(lines["hdfsRead_verify"]["gib_s"] / lines["reference_cpu_verify"]["gib_s"], 2)
-        # median over the timed passes of (GPU pass rate / the reference pass run right after it)
-        out["paired_gpu_over_reference_cpu"] = {"verify": paired[True], "no_verify": paired[False],
-                                                "how": "GPU and reference passes alternated; median of the "
-                                                       "per-pair rate ratios"}
+        out["gpu8_over_reference_cpu8"] = round(lines["hdfsPread8_verify"]["gib_s"] /
+                                                lines["reference_cpu8_verify"]["gib_s"], 2)
+        # median over the timed passes of (GPU pass rate / the reference pass run right after it), and of
+        # (GPU pass client CPU per GiB / the reference pass's)
+        out["paired_gpu_over_reference_cpu"] = {
+            "verify": paired[("1", True)], "no_verify": paired[("1", False)],
+            "verify_8_streams": paired[("8", True)], "no_verify_8_streams": paired[("8", False)],
+            "how": "GPU and reference passes alternated; medians of the per-pair ratios (rate: higher is "
+                   "better for the GPU path; client_cpu: CPU-seconds per GiB, lower is better)"}
         out["readahead2_over_reference_cpu"] = round(
             lines["hdfsRead_verify_readahead2"]["gib_s"] / lines["reference_cpu_verify"]["gib_s"], 2)
     return out
@@ -1126,6 +1312,17 @@ def main():
         sys.exit(spawn_ranks(args.gpus))  # nothing in this process has touched a GPU
     if args.plumbing_check:
         return plumbing_check(args)
+    # config 5's loopback datanode in a process of its own, started before anything here touches a GPU
+    # (round 6): its sender threads are then neither charged to the client's CPU time nor competing
+    # inside the client's process unseen
+    dn_child = None
+    if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.mode == "verify" and not args.no_config5 and
+            args.bpc == 512 and not args.pmc_child):
+        import atexit
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from loopback import ChildDatanode
+        dn_child = ChildDatanode(packet_bytes=65536)
+        atexit.register(dn_child.stop)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -1322,7 +1519,7 @@ def main():
         except Exception as e:
             log("batched pass failed:", e)
     if world == 1 and args.mode == "verify" and not args.no_config5 and args.bpc == 512:
-        extra["config5"] = config5_block(torch, device, host_data, args.bpc, block_bytes, reps=5)
+        extra["config5"] = config5_block(torch, device, host_data, args.bpc, block_bytes, reps=5, dn=dn_child)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(work, args.cpu_seconds, args.bpc, data=host_data)

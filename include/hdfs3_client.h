@@ -66,6 +66,12 @@ int64_t hdfs3_block_reader_available(hdfs3_block_reader *r);
 int hdfs3_block_reader_stats(hdfs3_block_reader *r, uint32_t *bytes_per_checksum,
                              uint64_t *packets, uint64_t *gpu_batches);
 int hdfs3_block_reader_close(hdfs3_block_reader *r);
+/* Diagnostics (round 6): nanoseconds summed over every block reader of the process that has closed
+ * since the last reset, n <= 8 values in this order: the receiver's socket reads, arena acquisition,
+ * launches, the caller's waits for GPU verify results, the caller's copies out, the receiver's waits
+ * for a free slot (the caller is behind), the caller's waits for a received batch (the receiver is
+ * behind), and the receiver threads' CPU time. reset != 0 zeroes the sums after reading them. */
+int hdfs3_reader_phase_ns(uint64_t *out, int n, int reset);
 
 /* ------------------------------------------------------------------------------------
  * Input stream: the hdfsRead / hdfsPread / hdfsSeek / hdfsTell / hdfsAvailable surface

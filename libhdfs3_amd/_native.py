@@ -204,6 +204,7 @@ CLIENT_API = {
     "hdfs3_block_reader_read": (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32]),
     "hdfs3_block_reader_available": (c_int64, [c_void_p]),
     "hdfs3_block_reader_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint64), POINTER(c_uint64)]),
+    "hdfs3_reader_phase_ns": (c_int, [POINTER(c_uint64), c_int, c_int]),
     "hdfs3_block_reader_close": (c_int, [c_void_p]),
     "hdfs3_input_open": (c_int, [POINTER(LocatedBlock), c_int, ctypes.c_char_p, POINTER(ReaderOpts),
                                  POINTER(c_void_p)]),

@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime.h>
 #include <sys/socket.h>
+#include <time.h>
 
 #include <algorithm>
 #include <cerrno>
@@ -45,6 +46,15 @@ constexpr int kDefaultBatchPackets = 64;
 constexpr int kDefaultTimeoutMs = 60000;  // input.read.timeout default (SessionConfig.cpp)
 constexpr size_t kMaxResponse = 10u << 20;  // RemoteBlockReader.cpp:116
 constexpr int kSlots = 3;                  // receiving / verifying / delivering
+constexpr int kWaitPollUs = 20;            // the caller's sleep between polls of a batch's event
+constexpr int kPhases = 8;                 // hdfs3_reader_phase_ns
+std::atomic<uint64_t> g_phase_ns[kPhases] = {};
+
+uint64_t thread_cpu_ns() {
+    timespec ts{};
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
 constexpr int kMaxSlots = 64;              // deepest ring (read-ahead of a whole block)
 constexpr int32_t kMaxPacketData = 16 << 20;  // PacketReceiver.MAX_PACKET_SIZE (Hadoop)
 constexpr size_t kArenaCacheMax = 6;       // arenas a ctx keeps for its next reader
@@ -205,7 +215,14 @@ struct hdfs3_block_reader {
     std::string error_msg;
 
     std::atomic<uint64_t> packets{0}, batches{0};
-    std::atomic<uint64_t> t_ns[5] = {};  // receive, alloc, launch, wait, deliver (hdfs3x_block_reader_timing)
+    // receive, alloc, launch, wait, deliver (hdfs3x_block_reader_timing), then (round 6) the receiver's
+    // waits for a free slot, the caller's waits for a ready batch, the receiver thread's CPU time:
+    // summed into g_phase_ns when the reader closes (hdfs3_reader_phase_ns)
+    std::atomic<uint64_t> t_ns[kPhases] = {};
+    // How the caller waits for a batch's verify (round 6): by default it polls the batch's event and
+    // sleeps between polls, so a waiting caller leaves its core to the receivers and the datanode;
+    // HDFS3_READER_WAIT=spin keeps hipEventSynchronize's busy wait (the behaviour before round 6)
+    bool spin_wait = false;
 
     int sticky(int code, const std::string &msg) {
         error = code;
@@ -435,9 +452,16 @@ struct hdfs3_block_reader {
         (void)hipSetDevice(ctx->device);
         // the socket's data lands in host memory here (RemoteBlockReader.cpp:245): on the GPU's node
         bind_thread_to_device(ctx->device);
+        const uint64_t cpu0 = thread_cpu_ns();
+        struct CpuAdd {  // the thread's CPU time, whichever way the loop ends
+            hdfs3_block_reader *r;
+            uint64_t c0;
+            ~CpuAdd() { r->t_ns[7].fetch_add(thread_cpu_ns() - c0, std::memory_order_relaxed); }
+        } cpu_add{this, cpu0};
         for (;;) {
             int s;
             {
+                Timer idle(t_ns[5]);
                 std::unique_lock<std::mutex> lk(mu);
                 cv.wait(lk, [&] { return stop || !free_slots.empty(); });
                 if (stop) break;
@@ -476,7 +500,16 @@ struct hdfs3_block_reader {
     int wait(Batch &b) {
         if (b.verified) return 0;
         Timer tm(t_ns[3]);
-        HIP_OK(hipEventSynchronize(b.a.done));
+        if (spin_wait) {
+            HIP_OK(hipEventSynchronize(b.a.done));
+        } else {
+            for (;;) {
+                const hipError_t q = hipEventQuery(b.a.done);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) HIP_OK(q);
+                std::this_thread::sleep_for(std::chrono::microseconds(kWaitPollUs));
+            }
+        }
         const unsigned long long r = *b.a.h_res;
         if (r && b.dense) {  // the first bad chunk of the batch -> its packet
             const uint64_t chunk = ~r;
@@ -508,6 +541,7 @@ struct hdfs3_block_reader {
         while (total < len) {
             int s;
             {
+                Timer idle(t_ns[6]);
                 std::unique_lock<std::mutex> lk(mu);
                 cv.wait(lk, [&] { return !ready.empty() || recv_done; });
                 if (ready.empty()) {
@@ -593,6 +627,7 @@ struct hdfs3_block_reader {
             rx.join();
         }
         if (ctx) (void)hipStreamSynchronize(ctx->stream);
+        for (int i = 0; i < kPhases; ++i) g_phase_ns[i].fetch_add(t_ns[i].load(), std::memory_order_relaxed);
         // a borrowed ctx keeps up to a ring's worth of arenas for its next reader (a read-ahead
         // reader's deep ring included: the stream's next read-ahead takes them back)
         const size_t cache_max = std::max(kArenaCacheMax, slot.size());
@@ -638,6 +673,10 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
     if (!r) return fail(-ENOMEM, "reader allocation");
     r->slot.resize(size_t(std::min(std::max(slots > 0 ? slots : kSlots, kSlots), kMaxSlots)));
     r->prefetch = slots > 0;
+    {
+        const char *w = getenv("HDFS3_READER_WAIT");
+        r->spin_wait = w && std::strcmp(w, "spin") == 0;
+    }
     const int device = opts ? opts->device : 0;
     r->verify = opts ? opts->verify != 0 : true;
     if (opts && opts->batch_packets > 0) r->batch_packets = opts->batch_packets;
@@ -715,7 +754,7 @@ void hdfs3x_fail_prefetch_arenas(int n) { g_fail_prefetch_arenas = n; }
 
 // measurement hook (libhdfs3_crc_lab.so only): nanoseconds spent per phase so far
 int hdfs3x_block_reader_timing(hdfs3_block_reader *r, uint64_t *out5) {
-    if (!r || !out5) return fail(-EINVAL, "invalid argument");
+    if (!r || !out5) return fail(-EINVAL, "invalid argument");  // the first 5 phases
     for (int i = 0; i < 5; ++i) out5[i] = r->t_ns[i].load();
     return 0;
 }
@@ -723,6 +762,14 @@ int hdfs3x_block_reader_timing(hdfs3_block_reader *r, uint64_t *out5) {
 
 int hdfs3_block_reader_close(hdfs3_block_reader *r) {
     delete r;
+    return 0;
+}
+
+int hdfs3_reader_phase_ns(uint64_t *out, int n, int reset) {
+    if (!out || n < 0 || n > kPhases) return fail(-EINVAL, "invalid argument");
+    for (int i = 0; i < n; ++i) out[i] = reset ? g_phase_ns[i].exchange(0) : g_phase_ns[i].load();
+    if (reset)
+        for (int i = n; i < kPhases; ++i) g_phase_ns[i].store(0);
     return 0;
 }
 

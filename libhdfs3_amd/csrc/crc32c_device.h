@@ -329,13 +329,15 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 // The lane's constant byte offset is the only VGPR operand, so no 64-bit VGPR address
 // temporaries exist that the allocator could alias with in-flight load destinations
 // (which made the compiler drain the previous round's loads before each prefetch).
+// nb: the round's valid bytes (the resource's range; a partial round's lanes past it load zeros
+// without touching memory)
 template <bool NT>
-__device__ __forceinline__ void load_round_buf(Round &r, const uint8_t *base, uint32_t lane_off) {
+__device__ __forceinline__ void load_round_buf(Round &r, const uint8_t *base, uint32_t lane_off, uint32_t nb = 4096) {
     const uint64_t b = reinterpret_cast<uint64_t>(base);
     const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(b));
     const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(b >> 32));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, 4096, 0x00020000);
+        reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, __builtin_amdgcn_readfirstlane(nb), 0x00020000);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + 1024 * t, 0, NT ? 2 : 0);

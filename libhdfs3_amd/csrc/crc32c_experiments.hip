@@ -36,11 +36,10 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             if (a.len % kRoundBytes || units % npk || (upp & (upp - 1)) || a.chunk_base) return hipErrorInvalidValue;
             ChunkLaunch p = a;
             p.npk = npk;
-            p.upp_log2 = 0;
-            while ((uint64_t(1) << p.upp_log2) < upp) ++p.upp_log2;
             p.pitch = upp * kRoundBytes;
             p.crc_pitch = upp * (kRoundBytes / BPC) * 4;
             p.last_len = uint32_t(upp * kRoundBytes);
+            if (!packet_geom(p.pitch, p.last_len, npk, BPC, &p.geom)) return hipErrorInvalidValue;
             return launch_wave3<BPC, V, true, false>(p, tab, fold, grid_cap, s);
         }
         case 115:  // s_setprio by rounds left at every launch size (production: waves of >= 16 rounds)

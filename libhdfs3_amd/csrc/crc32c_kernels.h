@@ -14,6 +14,25 @@ namespace hdfs3crc {
 // (4 per SIMD) keep the CU's memory pipe and LDS busy.
 constexpr int kBlockThreads = 1024;
 
+// The 4 KiB units of a packet stream (PitchWalk, crc32c_wave.h). A packet of whole chunks is
+// ceil(bytes / 4096) units; its last unit may be PARTIAL (the writer's 127-chunk packets at bpc
+// 512: 65,024 B = 15 whole rounds + 3,584 B, OutputStreamImpl.cpp:161-170): its loads are bounded by
+// a buffer resource of ptail bytes, so the lanes past the last whole chunk read zeros and their
+// results are dropped. Unit u -> packet u / upp by a multiply-shift (u < 2^31: q = (u * magic) >>
+// shift, Granlund-Montgomery with N = 31), so upp need not be a power of two.
+struct PacketGeom {
+    uint64_t pk_len = 0;  // data bytes of every packet but the last (whole chunks)
+    uint32_t upp = 0;     // units per packet but the last
+    uint32_t magic = 0, shift = 0;
+    uint32_t ptail = 0;   // valid bytes of such a packet's last unit (4096: whole)
+    uint32_t lunits = 0;  // units of the last packet (its whole chunks only)
+    uint32_t ltail = 0;   // valid bytes of the last packet's last unit
+};
+// Fills g for npk packets of data_len bytes (the last last_len) with chunks of unit_bpc bytes
+// (<= 4096; callers at bpc = R x 4096 pass 4096). False when it does not fit the walk: a non-last
+// packet that ends in a short chunk, no unit at all, or 2^31 units or more.
+bool packet_geom(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32_t unit_bpc, PacketGeom *g);
+
 struct ChunkLaunch {
     const uint8_t *data;      // device pointer to the first chunk
     uint64_t len;             // bytes
@@ -26,11 +45,11 @@ struct ChunkLaunch {
     bool overlap_previous = false;  // HDFS3_LAUNCH_OVERLAP_PREVIOUS: AQL packet without barrier bit
     // Packet stream at a constant pitch (PitchWalk, launch_packet_stream): packet i's data at
     // data + i*pitch, its BE32 words at crc_be/out_be + i*pitch; every packet but the last holds
-    // exactly 1 << upp_log2 whole 4 KiB rounds, the last one last_len <= that many bytes. len is
-    // unused; result keys are (packet << 32) | chunk.
+    // geom.pk_len bytes of whole chunks (geom.upp units), the last one last_len <= that many bytes.
+    // len is unused; result keys are (packet << 32) | chunk.
     uint64_t pitch = 0;
     uint64_t npk = 0;
-    uint32_t upp_log2 = 0;
+    PacketGeom geom;
     uint32_t last_len = 0;
     // pitch mode over independent blocks at constant strides (a [blocks, bytes] tensor and its
     // [blocks, words] tensor): the words' own pitch; 0 = `pitch` (the wire layout of packets)
@@ -53,7 +72,7 @@ struct DevPacket {
 };
 
 // One independent byte range of a segmented launch (a block of a batch, or one packet's
-// data region): device pointers, its whole 4 KiB rounds start at global unit unit_begin,
+// data region): device pointers, its 4 KiB units start at global unit unit_begin,
 // chunk c of it is reported as key_base + c (packets: packet << 32).
 struct DevSegment {
     const uint8_t *data;
@@ -63,10 +82,15 @@ struct DevSegment {
     uint64_t key_base;
 };
 
+// Units of a segment of len bytes at bpc <= 4096: its whole chunks cut into 4 KiB units, the
+// last one partial when the whole chunks end inside a round (PacketGeom); a short last chunk is
+// the kernel's one-lane tail
+constexpr uint64_t seg_units(uint64_t len, uint32_t bpc) { return (len / bpc * bpc + 4095) / 4096; }
+
 // Fills h_seg for n segments (data/crc/len/key_base already set) and returns the total
-// whole-round count; *uniform = units per segment when every segment but the last has
+// unit count (seg_units); *uniform = units per segment when every segment but the last has
 // the same count (direct unit -> segment mapping), else 0 (binary search).
-uint64_t plan_segments(DevSegment *h_seg, size_t n, uint64_t *uniform);
+uint64_t plan_segments(DevSegment *h_seg, size_t n, uint32_t bpc, uint64_t *uniform);
 // True when the segmented wave kernel can take these segments: bpc in {512..4096},
 // every data pointer 16-byte aligned and every CRC pointer 4-byte aligned.
 bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc);
@@ -83,10 +107,10 @@ constexpr uint32_t kMaxInlineSegments = 16;
 // kernel when segments_fast() holds, else the chunk-per-lane packet kernel. Keys are
 // (packet << 32 | chunk).
 // constant-pitch packet streams (ChunkLaunch::pitch): whether the wave kernel's pitch mode
-// takes them (bpc 512..4096, aligned, every packet but the last a power-of-two number of
-// whole rounds), and its launcher (a.pitch/npk/upp_log2/last_len set)
+// takes them (bpc 512..4096 or R x 4096, aligned, every packet but the last whole chunks), and
+// its launcher (a.pitch/npk/geom/last_len set)
 bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32_t bpc, const void *data,
-                      const void *crc, uint64_t pitch, uint32_t *upp_log2);
+                      const void *crc, uint64_t pitch, PacketGeom *geom);
 // Compute mode over a stream whose CRC words sit inside each packet (the wire layout: 512 B of
 // words per 64 KiB packet, 66 KiB apart) writes 8 MiB per GiB as small regions scattered over
 // the arena, interleaved with the read stream: 1 GiB took 213 us against 186 us with the words
@@ -125,13 +149,15 @@ hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc
                                  unsigned long long *result, const uint32_t *d_tables, const uint32_t *d_fold,
                                  int grid_cap, hipStream_t stream, WordScratch *ws = nullptr);
 // bad_index != null: every packet is first checked against [0, arena_len) (hipErrorInvalidValue
-// and *bad_index = the first one outside)
+// and *bad_index = the first one outside). staged != null: set when the launch copies h_stage to the
+// device asynchronously (the caller may reuse h_stage only after that copy ran); false when the
+// kernel's arguments carried everything (the pitch walk, inline descriptors).
 hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                hipStream_t stream, uint64_t arena_len = 0, size_t *bad_index = nullptr,
                                bool overlap_previous = false, WordScratch *ws = nullptr,
-                               PieceScratch *pieces = nullptr);
+                               PieceScratch *pieces = nullptr, bool *staged = nullptr);
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream,

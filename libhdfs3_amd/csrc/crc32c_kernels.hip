@@ -60,25 +60,42 @@ hipError_t launch_pv(const ChunkLaunch &a, bool verify, const uint32_t *tab, con
 
 }  // namespace
 
+bool packet_geom(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32_t unit_bpc, PacketGeom *g) {
+    if (npk == 0 || unit_bpc == 0 || unit_bpc > uint32_t(kRoundBytes) || last_len > data_len) return false;
+    if (npk > 1 && (data_len == 0 || data_len % unit_bpc)) return false;  // only the last packet ends short
+    PacketGeom r;
+    r.pk_len = npk > 1 ? data_len : 0;
+    r.upp = uint32_t(npk > 1 ? (data_len + kRoundBytes - 1) / kRoundBytes : 1);
+    r.ptail = uint32_t(npk > 1 ? data_len - uint64_t(r.upp - 1) * kRoundBytes : kRoundBytes);
+    const uint64_t lw = last_len / unit_bpc * unit_bpc;
+    r.lunits = uint32_t((lw + kRoundBytes - 1) / kRoundBytes);
+    r.ltail = r.lunits ? uint32_t(lw - uint64_t(r.lunits - 1) * kRoundBytes) : 0;
+    const uint64_t units = (npk - 1) * uint64_t(r.upp) + r.lunits;
+    if (units == 0 || units >= (uint64_t(1) << 31)) return false;
+    // q = (u * magic) >> shift = u / upp for every u < 2^31: magic = ceil(2^(31 + l) / upp), l =
+    // ceil(log2 upp), so magic < 2^32 and u * magic < 2^63
+    uint32_t l = 0;
+    while ((uint64_t(1) << l) < r.upp) ++l;
+    r.shift = 31 + l;
+    r.magic = uint32_t(((uint64_t(1) << r.shift) + r.upp - 1) / r.upp);
+    *g = r;
+    return true;
+}
+
 bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32_t bpc, const void *data,
-                      const void *crc, uint64_t pitch, uint32_t *upp_log2) {
-    // bpc 512..4096: the round kernel's pitch walk; R * 4096 (R >= 2) with R dividing the rounds per
-    // packet: the walk's 4096-byte piece CRCs + the combine (launch_stream_pieces, round 4)
+                      const void *crc, uint64_t pitch, PacketGeom *geom) {
+    // bpc 512..4096: the round kernel's pitch walk, a packet's last round partial when its chunks
+    // end inside one (round 6); R * 4096 (R >= 2): the walk's 4096-byte piece CRCs + the combine
+    // (launch_stream_pieces, round 4), every packet but the last whole chunks
     const bool pieces = bpc > kRoundBytes && bpc % kRoundBytes == 0;
     if (bpc != 512 && bpc != 1024 && bpc != 2048 && bpc != 4096 && !pieces) return false;
-    if (pieces && data_len % bpc) return false;
-    if (npk == 0 || data_len == 0 || data_len % kRoundBytes || last_len > data_len) return false;
+    if (npk == 0 || data_len == 0 || last_len > data_len) return false;
     if (npk > 1 && pitch == 0) return false;
     if (npk >= (uint64_t(1) << 31)) return false;  // keys are (packet << 32) | chunk
     if ((reinterpret_cast<uintptr_t>(data) & 15u) || (reinterpret_cast<uintptr_t>(crc) & 3u) || (pitch & 15u))
         return false;
-    const uint64_t upp = data_len / kRoundBytes;
-    if (upp & (upp - 1)) return false;  // rounds per packet: a power of two (64 KiB packets: 16)
-    if (((npk - 1) * upp + last_len / kRoundBytes) == 0) return false;
-    uint32_t l = 0;
-    while ((uint64_t(1) << l) < upp) ++l;
-    *upp_log2 = l;
-    return true;
+    if (pieces && npk > 1 && data_len % bpc) return false;
+    return packet_geom(data_len, last_len, npk, pieces ? uint32_t(kRoundBytes) : bpc, geom);
 }
 
 hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc, bool verify, int check_short_tail,
@@ -94,9 +111,9 @@ hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc
         if (h_seg[i].data != h_seg[0].data + int64_t(i) * dp || h_seg[i].crc != h_seg[0].crc + int64_t(i) * cp ||
             (i + 1 < n && h_seg[i].len != h_seg[0].len) || h_seg[i].len > h_seg[0].len)
             return hipErrorNotSupported;
-    uint32_t upp_log2 = 0;
+    PacketGeom geom;
     if (!packet_stream_ok(h_seg[0].len, h_seg[n - 1].len, n, bpc, h_seg[0].data, h_seg[0].crc, uint64_t(dp),
-                          &upp_log2) ||
+                          &geom) ||
         (cp & 3))
         return hipErrorNotSupported;
     ChunkLaunch a{};
@@ -109,7 +126,7 @@ hipError_t launch_strided_blocks(const DevSegment *h_seg, size_t n, uint32_t bpc
     a.pitch = uint64_t(dp);
     a.crc_pitch = uint64_t(cp);
     a.npk = n;
-    a.upp_log2 = upp_log2;
+    a.geom = geom;
     a.last_len = uint32_t(h_seg[n - 1].len);
     return launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream, ws);
 }
@@ -161,13 +178,12 @@ hipError_t launch_packet_stream(const ChunkLaunch &a, bool verify, const uint32_
     if (g_variant == 55) ws = nullptr;  // A/B: words written in place (no dense scratch)
 #endif
     if (a.bpc > kRoundBytes) {  // chunks of R whole rounds: pieces + combine, or the caller's fallback
-        if (!pieces || a.bpc % kRoundBytes || ((uint64_t(1) << a.upp_log2) % (a.bpc / kRoundBytes)))
-            return hipErrorNotSupported;
+        if (!pieces || a.bpc % kRoundBytes || (a.npk > 1 && a.geom.pk_len % a.bpc)) return hipErrorNotSupported;
         return launch_stream_pieces(a, verify, d_tables, d_fold, grid_cap, stream, pieces);
     }
     if (a.bpc != 512 && a.bpc != 1024 && a.bpc != 2048 && a.bpc != 4096) return hipErrorInvalidValue;
     const uint64_t cpitch = a.crc_pitch ? a.crc_pitch : a.pitch;
-    const uint64_t wpp = (uint64_t(kRoundBytes) << a.upp_log2) / a.bpc * 4;  // word bytes per packet
+    const uint64_t wpp = a.geom.pk_len / a.bpc * 4;  // word bytes per packet
     if (!verify && ws && a.npk > 1 && cpitch > wpp && wpp <= kDenseWordsMaxRegion) {
         const uint64_t last = (uint64_t(a.last_len) + a.bpc - 1) / a.bpc * 4;
         const uint64_t need = (a.npk - 1) * wpp + last;
@@ -335,8 +351,8 @@ hipError_t launch_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_ta
 hipError_t launch_stream_pieces(const ChunkLaunch &a, bool verify, const uint32_t *d_tables, const uint32_t *d_fold,
                                 int grid_cap, hipStream_t stream, PieceScratch *ps) {
     const uint32_t R = a.bpc / kRoundBytes;
-    const uint64_t upp = uint64_t(1) << a.upp_log2;
-    const uint64_t cpp = upp / R;                            // chunks per packet
+    const uint64_t upp = a.geom.upp;
+    const uint64_t cpp = a.geom.pk_len / a.bpc;              // chunks per packet
     const uint64_t lfull = a.last_len / a.bpc;               // whole chunks of the last packet
     const uint64_t nfull = (a.npk - 1) * cpp + lfull;
     const uint64_t npieces = (a.npk - 1) * upp + (uint64_t(a.last_len) + kRoundBytes - 1) / kRoundBytes;
@@ -434,12 +450,12 @@ hipError_t launch_packets(const uint8_t *d_arena, const DevPacket *d_pk, uint64_
     return hipGetLastError();
 }
 
-uint64_t plan_segments(DevSegment *h_seg, size_t n, uint64_t *uniform) {
-    uint64_t units = 0, u0 = n ? h_seg[0].len / kRoundBytes : 0;
+uint64_t plan_segments(DevSegment *h_seg, size_t n, uint32_t bpc, uint64_t *uniform) {
+    uint64_t units = 0, u0 = n ? seg_units(h_seg[0].len, bpc) : 0;
     bool same = true;
     for (size_t i = 0; i < n; ++i) {
         h_seg[i].unit_begin = units;
-        const uint64_t u = h_seg[i].len / kRoundBytes;
+        const uint64_t u = seg_units(h_seg[i].len, bpc);
         if (i + 1 < n && u != u0) same = false;
         units += u;
     }
@@ -456,17 +472,22 @@ bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc) {
 }
 
 template <int BPC>
-hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *fold, int grid,
+hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, const uint32_t *fold, int grid_cap,
                         hipStream_t s) {
 #if HDFS3_LAB
     if (g_variant == 115)
-        return verify ? launch_segments3<BPC, true, kLabPrio>(L, tab, fold, grid, s)
-                      : launch_segments3<BPC, false, kLabPrio>(L, tab, fold, grid, s);
+        return verify ? launch_segments3<BPC, true, kLabPrio>(L, tab, fold, grid_cap, s)
+                      : launch_segments3<BPC, false, kLabPrio>(L, tab, fold, grid_cap, s);
     if (g_variant == 117)
-        return verify ? launch_segments3<BPC, true, kLabNoPrio>(L, tab, fold, grid, s)
-                      : launch_segments3<BPC, false, kLabNoPrio>(L, tab, fold, grid, s);
+        return verify ? launch_segments3<BPC, true, kLabNoPrio>(L, tab, fold, grid_cap, s)
+                      : launch_segments3<BPC, false, kLabNoPrio>(L, tab, fold, grid_cap, s);
+    // 1024-thread workgroups at every size (production before round 6)
+    if (g_variant == 161)
+        return verify ? launch_segments3<BPC, true, 0, 1024>(L, tab, fold, grid_cap, s)
+                      : launch_segments3<BPC, false, 0, 1024>(L, tab, fold, grid_cap, s);
 #endif
-    return verify ? launch_segments3<BPC, true>(L, tab, fold, grid, s) : launch_segments3<BPC, false>(L, tab, fold, grid, s);
+    return verify ? launch_segments3<BPC, true>(L, tab, fold, grid_cap, s)
+                  : launch_segments3<BPC, false>(L, tab, fold, grid_cap, s);
 }
 
 hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,
@@ -492,20 +513,11 @@ hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t unit
         L.seg = nullptr;
         for (uint32_t i = 0; i < nseg; ++i) L.inl[i] = h_inline[i];
     }
-    const uint64_t need = (units + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock);
-    const uint64_t slow_need = (nseg + kBlockThreads - 1) / kBlockThreads;
-    uint64_t g = need > slow_need ? need : slow_need;
-    g = g < uint64_t(grid_cap) ? g : uint64_t(grid_cap);
-    const int grid = int(g > 0 ? g : 1);
-    const uint64_t nwaves = uint64_t(grid) * kWavesPerBlock;
-    if (units / nwaves >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
-    L.kq = uint32_t(units / nwaves);
-    L.kr = uint32_t(units % nwaves);
     switch (bpc) {
-    case 512: return launch_seg_t<512>(L, verify, d_tables, d_fold, grid, stream);
-    case 1024: return launch_seg_t<1024>(L, verify, d_tables, d_fold, grid, stream);
-    case 2048: return launch_seg_t<2048>(L, verify, d_tables, d_fold, grid, stream);
-    case 4096: return launch_seg_t<4096>(L, verify, d_tables, d_fold, grid, stream);
+    case 512: return launch_seg_t<512>(L, verify, d_tables, d_fold, grid_cap, stream);
+    case 1024: return launch_seg_t<1024>(L, verify, d_tables, d_fold, grid_cap, stream);
+    case 2048: return launch_seg_t<2048>(L, verify, d_tables, d_fold, grid_cap, stream);
+    case 4096: return launch_seg_t<4096>(L, verify, d_tables, d_fold, grid_cap, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -514,14 +526,16 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                hipStream_t stream, uint64_t arena_len, size_t *bad_index, bool overlap_previous,
-                               WordScratch *ws, PieceScratch *pieces) {
+                               WordScratch *ws, PieceScratch *pieces, bool *staged) {
+    if (staged) *staged = false;
     if (n == 0) return hipSuccess;
     // one pass: descriptors, the alignment test of segments_fast and the unit plan of
     // plan_segments (16K packets per GiB: the host loop is on the call's critical path)
     bool fast = g_variant != 17 && (bpc == 512 || bpc == 1024 || bpc == 2048 || bpc == 4096);
     // bpc = R * 4096: the pitch walk's pieces + combine when the batch is a constant-pitch stream
     bool aligned = g_variant != 17 && (fast || (pieces && bpc > kRoundBytes && bpc % kRoundBytes == 0));
-    uint64_t units = 0, u0 = h_pk[0].data_len / kRoundBytes;
+    const uint32_t ubpc = bpc <= uint32_t(kRoundBytes) ? bpc : uint32_t(kRoundBytes);
+    uint64_t units = 0, u0 = seg_units(h_pk[0].data_len, ubpc);
     bool same = true;
     // constant pitch: packet i at data_off[0] + i*S, crc_off[0] + i*S, one data length
     // (the last may be shorter) -> the kernel derives every descriptor (SegLaunch::stride)
@@ -546,7 +560,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         }
         const uint8_t *data = d_arena + h_pk[i].data_off;
         const uint8_t *crc = d_arena + h_pk[i].crc_off;
-        const uint64_t u = h_pk[i].data_len / kRoundBytes;
+        const uint64_t u = seg_units(h_pk[i].data_len, ubpc);
         const bool al = ((reinterpret_cast<uintptr_t>(data) & 15u) | (reinterpret_cast<uintptr_t>(crc) & 3u)) == 0;
         fast = fast && al;
         aligned = aligned && al;
@@ -559,10 +573,10 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
                    (i + 1 == n || h_pk[i].data_len == h_pk[0].data_len);
         units += u;
     }
-    uint32_t upp_log2 = 0;
+    PacketGeom geom;
     if (aligned && (strided || dstrided) && n > 1 &&
         packet_stream_ok(h_pk[0].data_len, h_pk[n - 1].data_len, n, bpc, d_arena + h_pk[0].data_off,
-                         d_arena + h_pk[0].crc_off, pitch, &upp_log2)) {
+                         d_arena + h_pk[0].crc_off, pitch, &geom)) {
         ChunkLaunch a{};
         a.data = d_arena + h_pk[0].data_off;
         a.crc_be = d_arena + h_pk[0].crc_off;
@@ -573,7 +587,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         a.pitch = pitch;
         a.crc_pitch = strided ? 0 : cpitch;
         a.npk = n;
-        a.upp_log2 = upp_log2;
+        a.geom = geom;
         a.last_len = h_pk[n - 1].data_len;
         a.overlap_previous = overlap_previous && verify;
         const hipError_t e = launch_packet_stream(a, verify, d_tables, d_fold, grid_cap, stream, ws, pieces);
@@ -592,13 +606,14 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
     for (size_t i = 0; i < n; ++i) {
         h_stage[i] = DevSegment{d_arena + h_pk[i].data_off, const_cast<uint8_t *>(d_arena) + h_pk[i].crc_off,
                                 h_pk[i].data_len, units, uint64_t(i) << 32};
-        units += h_pk[i].data_len / kRoundBytes;
+        units += seg_units(h_pk[i].data_len, ubpc);
     }
     if (fast) {
         const uint64_t uniform = same && u0 > 0 ? u0 : 0;
         if (n > kInlineSegments) {
             hipError_t e = hipMemcpyAsync(d_stage, h_stage, n * sizeof(DevSegment), hipMemcpyHostToDevice, stream);
             if (e != hipSuccess) return e;
+            if (staged) *staged = true;
         }
         if (n <= kInlineSegments)  // no descriptor copy in front of the kernel
             return launch_segments(nullptr, uint32_t(n), units, uniform, bpc, verify, check_short_tail, result,
@@ -611,6 +626,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
     for (size_t i = 0; i < n; ++i) hp[i] = h_pk[i];
     hipError_t e = hipMemcpyAsync(d_stage, hp, n * sizeof(DevPacket), hipMemcpyHostToDevice, stream);
     if (e != hipSuccess) return e;
+    if (staged) *staged = true;
     return launch_packets(d_arena, reinterpret_cast<const DevPacket *>(d_stage), n, bpc, verify, check_short_tail,
                           result, d_tables, grid_cap, stream);
 }

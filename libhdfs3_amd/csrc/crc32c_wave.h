@@ -10,7 +10,7 @@
 // per CU). The round -> data mapping is a WALK:
 //   BlockWalk   one contiguous block (unit u at data + 4096 u);
 //   PitchWalk   a packet stream at a constant pitch, or equal blocks of one 2-D tensor
-//               (unit u = round u & (upp - 1) of packet u >> log2(upp));
+//               (unit u = round u % upp of packet u / upp; a packet's last round may be partial);
 //   SegWalk     a list of independent segments (ragged batches, packets in descriptor lists),
 //               the prefetch stream's current segment cached in scalar registers.
 // Every view a walk returns (data pointer, the round's CRC-word pointer, the key of its first chunk)
@@ -73,11 +73,13 @@ typedef __attribute__((address_space(4))) const SegLaunch CSegLaunch;
 typedef __attribute__((address_space(4))) const DevSegment CDevSegment;
 
 // A round's view: data, CRC words of its first chunk (stored words when verifying, the output when
-// computing), result key of its first chunk.
+// computing), result key of its first chunk, valid bytes (4096, or the whole chunks of a partial
+// last round of a packet or segment: PacketGeom).
 struct WView {
     const uint8_t *p;
     uint8_t *w;
     uint64_t key;
+    uint32_t nb;
 };
 
 // Rounds of one contiguous block: the wave's rounds are units wave, wave + W, ... (W = waves).
@@ -97,13 +99,16 @@ struct BlockWalk {
         const uint64_t u = first + uint64_t(k) * stride;
         const bool in = k < K;
         return WView{in ? data + u * kRoundBytes : dummy, in ? words + 4 * CPU * u : const_cast<uint8_t *>(dummy),
-                     key0 + CPU * u};
+                     key0 + CPU * u, uint32_t(kRoundBytes)};
     }
 };
 
-// A packet stream at one pitch: every packet but the last holds 1 << L whole rounds; its words sit
-// at words + packet * wpitch (the wire layout: in the packet; a [blocks, words] tensor: their own
-// pitch). Keys are (packet << 32) | chunk.
+// A packet stream at one pitch (PacketGeom): every packet but the last holds upp units, the last
+// lunits; a packet's last unit holds ptail (the last packet: ltail) valid bytes. Its words sit at
+// words + packet * wpitch (the wire layout: in the packet; the writer's batches and a [blocks,
+// words] tensor: their own pitch). Keys are (packet << 32) | chunk. Unit indices stay below 2^31
+// (the host's packet_geom), so the packet is a 32 x 32 multiply-shift: SALU for the wave's own
+// views, VALU only for the held stores' lane-varying ones.
 template <int CPU>
 struct PitchWalk {
     static constexpr bool kLaneView = true;
@@ -111,14 +116,18 @@ struct PitchWalk {
     const uint8_t *data;
     uint8_t *words;
     uint64_t dpitch, wpitch, first, stride;
-    uint32_t K, L;
+    uint32_t K;
+    uint32_t upp, magic, shift, ptail, lunits, ltail, lpk;
     const uint8_t *dummy;
     __device__ __forceinline__ WView view(uint32_t k) const {
-        const uint64_t u = first + uint64_t(k) * stride;
-        const uint64_t pk = u >> L, r = u & ((uint64_t(1) << L) - 1);
+        const uint32_t u = uint32_t(first + uint64_t(k) * stride);
+        const uint32_t pk = uint32_t((uint64_t(u) * magic) >> shift), r = u - pk * upp;
+        const bool lastp = pk == lpk;
+        const uint32_t nb = r + 1 == (lastp ? lunits : upp) ? (lastp ? ltail : ptail) : uint32_t(kRoundBytes);
         const bool in = k < K;
-        return WView{in ? data + pk * dpitch + r * kRoundBytes : dummy,
-                     in ? words + pk * wpitch + 4 * CPU * r : const_cast<uint8_t *>(dummy), (pk << 32) | (CPU * r)};
+        return WView{in ? data + uint64_t(pk) * dpitch + uint64_t(r) * kRoundBytes : dummy,
+                     in ? words + uint64_t(pk) * wpitch + 4 * CPU * r : const_cast<uint8_t *>(dummy),
+                     (uint64_t(pk) << 32) | (CPU * r), in ? nb : uint32_t(kRoundBytes)};
     }
 };
 
@@ -141,10 +150,14 @@ struct SegWalk {
     uint32_t K;
     const uint8_t *dummy;
     uint64_t c_begin = 1, c_end = 0, c_key = 0;
+    uint64_t c_wlen = 0;  // the cached segment's whole-chunk bytes (its last unit may be partial)
     const uint8_t *c_data = nullptr;
     uint8_t *c_crc = nullptr;
     uint32_t c_si = ~0u;  // index of the cached segment (~0: none yet)
+    static constexpr uint32_t kBpc = uint32_t(kRoundBytes / CPU);
 
+    __device__ __forceinline__ static uint64_t wlen(uint64_t len) { return len / kBpc * kBpc; }
+    __device__ __forceinline__ static uint64_t units(uint64_t len) { return (wlen(len) + kRoundBytes - 1) / kRoundBytes; }
     __device__ __forceinline__ CDevSegment *segp(uint32_t i) const {
         return L->seg ? (CDevSegment *)(L->seg) + i : L->inl + i;
     }
@@ -163,7 +176,7 @@ struct SegWalk {
         }
     }
     __device__ __forceinline__ WView view(uint32_t k) {
-        if (k >= K) return WView{dummy, const_cast<uint8_t *>(dummy), 0};
+        if (k >= K) return WView{dummy, const_cast<uint8_t *>(dummy), 0, uint32_t(kRoundBytes)};
         const uint64_t u = first + uint64_t(k) * stride;
         if (u < c_begin || u >= c_end) {
             uint32_t si;
@@ -175,28 +188,32 @@ struct SegWalk {
                 // anyway) before the binary search (a chain of dependent loads)
                 const uint32_t nx = c_si + 1;
                 si = nx < L->nseg && u >= rfl64(segp(nx)->unit_begin) &&
-                             u < rfl64(segp(nx)->unit_begin) + rfl64(segp(nx)->len) / kRoundBytes
+                             u < rfl64(segp(nx)->unit_begin) + units(rfl64(segp(nx)->len))
                          ? nx
                          : seg_of(u);
             }
             if (L->stride) {  // packets at one pitch: kernel-argument arithmetic, no descriptor loads
+                const bool lastp = si + 1 >= L->nseg;
                 c_begin = uint64_t(si) * L->uniform;
-                c_end = c_begin + (si + 1 < L->nseg ? L->uniform : L->inl[1].len / kRoundBytes);
+                c_wlen = wlen(lastp ? L->inl[1].len : L->inl[0].len);
+                c_end = c_begin + (lastp ? units(L->inl[1].len) : L->uniform);
                 c_data = L->inl[0].data + uint64_t(si) * L->stride;
                 c_crc = L->inl[0].crc + uint64_t(si) * L->stride;
                 c_key = uint64_t(si) << 32;
             } else {
                 CDevSegment *sd = segp(si);
                 c_begin = rfl64(sd->unit_begin);
-                c_end = c_begin + rfl64(sd->len) / kRoundBytes;
+                c_wlen = wlen(rfl64(sd->len));
+                c_end = c_begin + (c_wlen + kRoundBytes - 1) / kRoundBytes;
                 c_data = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->data)));
                 c_crc = reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->crc)));
                 c_key = rfl64(sd->key_base);
             }
             c_si = si;
         }
-        const uint64_t r = u - c_begin;
-        return WView{c_data + r * kRoundBytes, c_crc + 4 * CPU * r, c_key + CPU * r};
+        const uint64_t r = u - c_begin, left = c_wlen - r * kRoundBytes;
+        return WView{c_data + r * kRoundBytes, c_crc + 4 * CPU * r, c_key + CPU * r,
+                     left < kRoundBytes ? uint32_t(left) : uint32_t(kRoundBytes)};
     }
 };
 
@@ -244,8 +261,8 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     WView cv0 = walk.view(0), cv1 = walk.view(1);
     __builtin_amdgcn_sched_barrier(0);
     Round a0, a1, b0, b1;
-    load_round_buf<true>(a0, cv0.p, lane_off);
-    load_round_buf<true>(a1, cv1.p, lane_off);
+    load_round_buf<true>(a0, cv0.p, lane_off, cv0.nb);
+    load_round_buf<true>(a1, cv1.p, lane_off, cv1.nb);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int f = 0; f < kFillIters; ++f) {
@@ -275,13 +292,15 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         return nf.apply(x);
     };
     const uint32_t woff = 4 * (lane / G);  // this lane's chunk word within a round
+    const uint32_t coff = (lane / G) * BPC;  // its chunk's first byte: the chunk is whole when coff < nb
     WView pv0 = walk.view(2), pv1 = walk.view(3);
 
     // The stored words through a buffer resource on the round's (wave-uniform) word base: the lane's
     // offset is the only VGPR operand. A 64-bit VGPR address temporary may be allocated on registers
     // of a round still in flight, and the waitcnt pass then drains every load at the loop head.
+    // Its range is the round's whole chunks: a partial round's stores past them are dropped.
     auto wrsrc = [](const WView &v) {
-        return __builtin_amdgcn_make_buffer_rsrc(v.w, 0, 4 * (kRoundBytes / BPC), 0x00020000);
+        return __builtin_amdgcn_make_buffer_rsrc(v.w, 0, __builtin_amdgcn_readfirstlane(v.nb / (BPC / 4)), 0x00020000);
     };
     auto want_of = [&](const WView &v) -> uint32_t {
         if constexpr (VERIFY) return __builtin_amdgcn_raw_buffer_load_b32(wrsrc(v), woff, 0, 0);
@@ -315,7 +334,10 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
                     if (hold_addr[i]) *hold_addr[i] = hold[i];
                 } else {
                     const uint32_t kk = 8 * (hold_base + nheld - 1 - i) + (lane >> 3);
-                    if (kk < K) held_store((gu8 *)walk.view(kk).w + 4 * (lane & 7), hold[i]);
+                    if (kk < K) {
+                        const WView v = walk.view(kk);
+                        if ((lane & 7) * BPC < v.nb) held_store((gu8 *)v.w + 4 * (lane & 7), hold[i]);
+                    }
                 }
             }
         }
@@ -410,7 +432,8 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             const uint32_t got = uint32_t(__builtin_amdgcn_ds_bpermute(int(32 * (lane & 7)), int(y)));
             const bool mine = (lane >> 3) == r;
             line = mine ? got : line;
-            if constexpr (kAddr) laddr = mine ? (gu32 *)((gu8 *)v.w + 4 * (lane & 7)) : laddr;
+            if constexpr (kAddr)
+                laddr = mine ? ((lane & 7) * BPC < v.nb ? (gu32 *)((gu8 *)v.w + 4 * (lane & 7)) : nullptr) : laddr;
             if (r == 7 || k + 1 == K) {
 #pragma unroll
                 for (int i = (kHold ? 7 : 0); i > 0; --i) {
@@ -430,8 +453,9 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         const uint32_t c = y;
         if constexpr (VERIFY) {
             // the diagnostics compute wrong CRCs: compare inverted so they do not flag every chunk
-            // (an atomic per chunk would dominate their time)
-            if ((want != c) != kWrong)
+            // (an atomic per chunk would dominate their time); a partial round's lanes past its
+            // whole chunks computed zeros
+            if ((want != c) != kWrong && coff < v.nb)
                 __hip_atomic_fetch_max((gu64 *)result, ~(unsigned long long)(v.key + lane / G), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         } else {
@@ -515,8 +539,8 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         prio(k);
         const uint32_t w0 = want_of(cv0), w1 = want_of(cv1);
         if constexpr (!LATE) {
-            load_round_buf<true>(p0, pv0.p, lane_off);
-            load_round_buf<true>(p1, pv1.p, lane_off);
+            load_round_buf<true>(p0, pv0.p, lane_off, pv0.nb);
+            load_round_buf<true>(p1, pv1.p, lane_off, pv1.nb);
         }
         __builtin_amdgcn_sched_barrier(0);
         regroup(c0);
@@ -526,8 +550,8 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         }
         if constexpr (LATE) {
             __builtin_amdgcn_sched_barrier(0);
-            load_round_buf<true>(p0, pv0.p, lane_off);
-            load_round_buf<true>(p1, pv1.p, lane_off);
+            load_round_buf<true>(p0, pv0.p, lane_off, pv0.nb);
+            load_round_buf<true>(p1, pv1.p, lane_off, pv1.nb);
             __builtin_amdgcn_sched_barrier(0);
         }
         uint32_t x0, x1;
@@ -629,7 +653,25 @@ __device__ __forceinline__ void slow_region(const uint32_t *lds, const uint8_t *
     }
 }
 
-// One block (PITCH = false) or a constant-pitch stream (PITCH = true, ChunkLaunch::pitch/npk/...).
+// The short last chunk (len % BPC bytes) of a run whose whole chunks the walk covered: one lane
+// of workgroup 0.
+template <int BPC, bool VERIFY, int TPB = kBlockThreads>
+__device__ __forceinline__ void short_tail(const uint32_t *lds, const uint8_t *sdata, uint8_t *sw, uint64_t len,
+                                           uint64_t skey, int check_short_tail, unsigned long long *result) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const Lut t(lds);
+    const uint64_t chunk = len / BPC;
+    const bool crc_al4 = (reinterpret_cast<uintptr_t>(sw) & 3u) == 0;
+    const uint32_t c = ~crc_run_lines(t, 0xFFFFFFFFu, sdata + chunk * BPC, uint32_t(len % BPC));
+    if constexpr (VERIFY) {
+        if (check_short_tail && load_be32(sw + 4 * chunk, crc_al4) != c)
+            atomicMax(result, ~(unsigned long long)(skey + chunk));
+    } else {
+        store_be32(sw + 4 * chunk, c, crc_al4);
+    }
+}
+
+// One block (PITCH = false) or a constant-pitch stream (PITCH = true, ChunkLaunch::pitch/npk/geom).
 template <int BPC, bool VERIFY, bool PITCH, bool SOLO, int LAB = 0, int TPB = kBlockThreads>
 __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const uint32_t *__restrict__ g_tab,
                                                                     const uint32_t *__restrict__ g_nib) {
@@ -654,13 +696,14 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
     }
 #endif
     if constexpr (PITCH) {
-        PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves, K, a.upp_log2,
-                          dummy};
+        const PacketGeom &g = a.geom;
+        PitchWalk<kCpu> w{a.data, words, a.pitch, a.crc_pitch ? a.crc_pitch : a.pitch, wave, nwaves, K,
+                          g.upp, g.magic, g.shift, g.ptail, g.lunits, g.ltail, uint32_t(a.npk - 1), dummy};
         wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result);
         const uint64_t lp = a.npk - 1;
-        if (a.last_len % kRoundBytes)  // wave-uniform: a stream of whole rounds has no slow region
-            slow_region<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
-                                     a.check_short_tail, a.result);
+        if (a.last_len % BPC)  // wave-uniform: only the last packet's short chunk is left
+            short_tail<BPC, VERIFY, TPB>(lds, a.data + lp * a.pitch, words + lp * w.wpitch, a.last_len, lp << 32,
+                                         a.check_short_tail, a.result);
     } else {
         BlockWalk<kCpu> w{a.data, words, a.chunk_base, wave, nwaves, K, dummy, a.kq, a.kr};
         wave_rounds<BPC, VERIFY, SOLO, kHold, LAB, TPB>(w, lds, g_tab, g_nib, a.result, lab_mid);
@@ -678,43 +721,42 @@ __global__ __launch_bounds__(TPB) void crc32c_wave_kernel(ChunkLaunch a, const u
 #endif
 }
 
-// A list of segments (blocks of a batch, packets of a descriptor list): the core over a SegWalk,
-// then every segment's leftover chunks and short tail, one chunk per thread spread over the
-// workgroups (item i -> segment i / chunks-per-round, block i % grid).
-template <int BPC, bool VERIFY, bool UNI, int LAB = 0>
-__global__ __launch_bounds__(kBlockThreads) void crc32c_segments_kernel(SegLaunch L, const uint32_t *__restrict__ g_tab,
-                                                                        const uint32_t *__restrict__ g_nib) {
+// A list of segments (blocks of a batch, packets of a descriptor list): the core over a SegWalk
+// (a segment's last unit partial when its whole chunks end inside a round), then every segment's
+// short last chunk, one lane each.
+template <int BPC, bool VERIFY, bool UNI, int LAB = 0, int TPB = kBlockThreads>
+__global__ __launch_bounds__(TPB) void crc32c_segments_kernel(SegLaunch L, const uint32_t *__restrict__ g_tab,
+                                                              const uint32_t *__restrict__ g_nib) {
     static_assert(BPC <= kRoundBytes && BPC % 512 == 0, "one-round units");
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytesWave / 4];
     constexpr int kCpu = kRoundBytes / BPC;
-    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerBlock;
-    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int kWpb = TPB / 64;
+    const uint64_t nwaves = uint64_t(gridDim.x) * kWpb;
+    const uint64_t wave = uint64_t(blockIdx.x) * kWpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     SegWalk<kCpu, UNI> w{(CSegLaunch *)(&L), wave, nwaves, L.kq + (wave < L.kr ? 1u : 0u),
                          reinterpret_cast<const uint8_t *>(g_tab)};
-    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, LAB, kBlockThreads>(w, lds, g_tab, g_nib, L.result);
+    wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, LAB, TPB>(w, lds, g_tab, g_nib, L.result);
 
+    // every whole chunk was in a (possibly partial) round: only the segments' short last chunks
+    // are left, one lane each, item i on workgroup i % grid
     const Lut t(lds);
-    const uint64_t items = uint64_t(L.nseg) * kCpu;
-    for (uint64_t it = uint64_t(threadIdx.x) * gridDim.x + blockIdx.x; it < items;
-         it += uint64_t(gridDim.x) * kBlockThreads) {
-        const uint32_t si = uint32_t(it / kCpu);
+    for (uint64_t si = uint64_t(threadIdx.x) * gridDim.x + blockIdx.x; si < L.nseg;
+         si += uint64_t(gridDim.x) * TPB) {
         DevSegment sd;
         if (L.stride) {
             sd = L.inl[0];
-            sd.data += uint64_t(si) * L.stride;
-            sd.crc += uint64_t(si) * L.stride;
+            sd.data += si * L.stride;
+            sd.crc += si * L.stride;
             sd.len = si + 1 < L.nseg ? L.inl[0].len : L.inl[1].len;
-            sd.key_base = uint64_t(si) << 32;
+            sd.key_base = si << 32;
         } else {
             sd = L.seg ? L.seg[si] : L.inl[si];  // per-thread index: vector loads
         }
-        const uint64_t nfull = sd.len / BPC;
-        const uint64_t c = (sd.len / kRoundBytes) * kCpu + it % kCpu;
-        if (c < nfull + (sd.len % BPC ? 1 : 0)) {
-            const uint32_t sz = c < nfull ? uint32_t(BPC) : uint32_t(sd.len % BPC);
-            const uint32_t v = ~crc_run_lines(t, 0xFFFFFFFFu, sd.data + c * BPC, sz);
+        if (sd.len % BPC) {
+            const uint64_t c = sd.len / BPC;
+            const uint32_t v = ~crc_run_lines(t, 0xFFFFFFFFu, sd.data + c * BPC, uint32_t(sd.len % BPC));
             if constexpr (VERIFY) {
-                if ((sz == uint32_t(BPC) || L.check_short_tail) && load_be32(sd.crc + 4 * c, true) != v)
+                if (L.check_short_tail && load_be32(sd.crc + 4 * c, true) != v)
                     atomicMax(L.result, ~(unsigned long long)(sd.key_base + c));
             } else {
                 store_be32(sd.crc + 4 * c, v, true);
@@ -737,7 +779,7 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     constexpr int G = BPC / 64;
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
     const uint32_t *nib = fold + ((LAB & kLabFull16) ? kFoldAffineOldOff : kFoldAffineOff) + set * kFoldNibbleWords;
-    const uint64_t units = PITCH ? ((a.npk - 1) << a.upp_log2) + a.last_len / kRoundBytes : a.len / kRoundBytes;
+    const uint64_t units = PITCH ? (a.npk - 1) * a.geom.upp + a.geom.lunits : a.len / kRoundBytes;
     const uint64_t need = (units + 2 * (TPB / 64) - 1) / (2 * (TPB / 64));
     int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
     if (grid < 1) grid = 1;
@@ -756,8 +798,9 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     // 7.38 -> 6.45 us barriered, 7.05 -> 6.43 overlapped; 16 MiB 7.95 -> 6.47 / 7.27 -> 5.81; 32 MiB
     // 10.16 -> 9.04 / 8.82 -> 8.53; 64 MiB 14.57 -> 13.90 / 13.36 -> 12.56; the block reader's
     // 64-packet batch (4 MiB, cache-resident) 7.00 -> 4.43. 128 MiB stays at 1024 (256 / 512 threads:
-    // +6.1 / +0.4 us barriered). Compute keeps 1024 threads: its staged words need the whole LDS.
-    if constexpr (V && TPB == 1024 && (LAB & kLabWg1024) == 0) {
+    // +6.1 / +0.4 us barriered). Compute over a contiguous block keeps 1024 threads: its staged words
+    // need the whole LDS; compute over a packet stream (the writer's batches: held stores) does not.
+    if constexpr ((V || PITCH) && TPB == 1024 && (LAB & kLabWg1024) == 0) {
         if (units <= 4096) return launch_wave3<BPC, V, PITCH, SOLO, LAB, 256>(a, tab, fold, grid_cap, s);
         if (units <= 16384) return launch_wave3<BPC, V, PITCH, SOLO, LAB, 512>(a, tab, fold, grid_cap, s);
     }
@@ -786,17 +829,34 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     return hipGetLastError();
 }
 
-template <int BPC, bool V, int LAB = 0>
-hipError_t launch_segments3(const SegLaunch &L, const uint32_t *tab, const uint32_t *fold, int grid, hipStream_t s) {
+// The grid and the waves' round split (SegLaunch::kq/kr) are set here. Small launches take
+// smaller workgroups, as launch_wave3's verifies do (round 6): a 1024-thread workgroup owns a CU's
+// LDS, so a 64-packet batch (1,024 units) ran on 32 CUs.
+template <int BPC, bool V, int LAB = 0, int TPB = kBlockThreads>
+hipError_t launch_segments3(const SegLaunch &in, const uint32_t *tab, const uint32_t *fold, int grid_cap,
+                            hipStream_t s) {
+    if constexpr (TPB == 1024) {
+        if (in.units <= 4096) return launch_segments3<BPC, V, LAB, 256>(in, tab, fold, grid_cap, s);
+        if (in.units <= 16384) return launch_segments3<BPC, V, LAB, 512>(in, tab, fold, grid_cap, s);
+    }
     constexpr int G = BPC / 64;
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
+    constexpr uint64_t kWpb = TPB / 64;
     const uint32_t *nib = fold + ((LAB & kLabFull16) ? kFoldAffineOldOff : kFoldAffineOff) + set * kFoldNibbleWords;
+    SegLaunch L = in;
+    const uint64_t need = (L.units + 2 * kWpb - 1) / (2 * kWpb);
+    const uint64_t tail_need = (L.nseg + TPB - 1) / TPB;
+    uint64_t g = need > tail_need ? need : tail_need;
+    g = g < uint64_t(grid_cap) ? g : uint64_t(grid_cap);
+    const int grid = int(g > 0 ? g : 1);
+    const uint64_t nwaves = uint64_t(grid) * kWpb;
+    if (L.units / nwaves >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
+    L.kq = uint32_t(L.units / nwaves);
+    L.kr = uint32_t(L.units % nwaves);
     if (L.uniform)
-        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, true, LAB>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab,
-                           nib);
+        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, true, LAB, TPB>), dim3(grid), dim3(TPB), 0, s, L, tab, nib);
     else
-        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, false, LAB>), dim3(grid), dim3(kBlockThreads), 0, s, L, tab,
-                           nib);
+        hipLaunchKernelGGL((crc32c_segments_kernel<BPC, V, false, LAB, TPB>), dim3(grid), dim3(TPB), 0, s, L, tab, nib);
     return hipGetLastError();
 }
 

@@ -260,17 +260,22 @@ int packets_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len, 
     // hdfs3_pkt_desc and DevPacket share one layout (asserted above): no conversion copy
     const DevPacket *hp = reinterpret_cast<const DevPacket *>(pk);
     size_t bad = 0;
+    bool staged = false;
     const hipError_t e = launch_packet_batch(d_arena, hp, n, bpc, verify, check_short_tail, d_result, st->h, st->d,
                                              ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, arena_len,
-                                             &bad, overlap, &ctx->words, &ctx->pieces);
+                                             &bad, overlap, &ctx->words, &ctx->pieces, &staged);
     if (e == hipErrorInvalidValue) return fail(-EINVAL, "packet %zu lies outside the %zu-byte arena", bad, arena_len);
     HIP_TRY(e);
     ++ctx->launches;
-    HIP_TRY(hipEventRecord(st->done, ctx->stream));
-    // the launch may have copied its descriptors out of st->h asynchronously (the segmented kernel's
-    // array, the chunk-per-lane kernel's DevPackets): the slot is reused only after that copy ran
-    // (round 5: unarmed, a fifth async batch could overwrite a queued copy's source)
-    st->armed = true;
+    // the launch copied its descriptors out of st->h asynchronously (the segmented kernel's array, the
+    // chunk-per-lane kernel's DevPackets): the slot is reused only after that copy ran (round 5:
+    // unarmed, a fifth async batch could overwrite a queued copy's source). A launch whose arguments
+    // carried everything (the pitch walk: the writer's and the wire-layout batches) records nothing:
+    // an event between barriered launches costs a marker packet, ~3 us of idle GPU (round 6)
+    if (staged) {
+        HIP_TRY(hipEventRecord(st->done, ctx->stream));
+        st->armed = true;
+    }
     return 0;
 }
 
@@ -310,9 +315,9 @@ int packet_stream_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena
         ps->crc_off + 4 * (ps->n > 1 ? chunks : lchunks) > arena_len || lc + 4 * lchunks > arena_len ||
         (ps->n > 1 && ps->pitch == 0))
         return fail(-EINVAL, "the packet stream does not fit the %zu-byte arena", arena_len);
-    uint32_t upp_log2 = 0;
+    PacketGeom geom;
     if (packet_stream_ok(ps->data_len, ps->last_len, ps->n, bpc, d_arena + ps->data_off, d_arena + ps->crc_off,
-                         ps->pitch, &upp_log2)) {
+                         ps->pitch, &geom)) {
         ChunkLaunch a{};
         a.data = d_arena + ps->data_off;
         a.crc_be = d_arena + ps->crc_off;
@@ -322,7 +327,7 @@ int packet_stream_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena
         a.check_short_tail = check_short_tail;
         a.pitch = ps->pitch;
         a.npk = ps->n;
-        a.upp_log2 = upp_log2;
+        a.geom = geom;
         a.last_len = ps->last_len;
         a.overlap_previous = overlap && verify;
         const hipError_t e =
@@ -382,7 +387,7 @@ int blocks_common(hdfs3_crc_ctx *ctx, const hdfs3_dev_block *blocks, size_t n, u
         ++ctx->launches;
     } else if (segments_fast(st->h, n, bpc)) {
         uint64_t uniform = 0;
-        const uint64_t units = plan_segments(st->h, n, &uniform);
+        const uint64_t units = plan_segments(st->h, n, bpc, &uniform);
         if (n <= kMaxInlineSegments) {  // descriptors in the kernel arguments: no copy first
             HIP_TRY(launch_segments(nullptr, uint32_t(n), units, uniform, bpc, verify, check_short_tail, d_result,
                                     ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, st->h));

@@ -215,6 +215,8 @@ class CrcContext:
     # -- packet-stream API ------------------------------------------------------------
     @staticmethod
     def _descs(pk) -> ctypes.Array:
+        if isinstance(pk, ctypes.Array):  # built once by the caller (timed loops)
+            return pk
         arr = (PktDesc * len(pk))()
         for i, (data_off, crc_off, data_len) in enumerate(pk):
             arr[i].data_off, arr[i].crc_off, arr[i].data_len, arr[i].reserved = data_off, crc_off, data_len, 0

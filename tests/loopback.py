@@ -3,6 +3,7 @@
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 
 import numpy as np
@@ -97,6 +98,79 @@ class LoopbackDatanode:
         if self.port:
             self.lb.hdfs3_loopback_stop(self.port)
             self.port = 0
+
+
+class ChildDatanode:
+    """The loopback datanode in a child process (tools/loopback/serve.py; bench.py config 5, round 6).
+    Start it before this process touches a GPU (a plain child: nothing is exec'd from a GPU process).
+    Blocks are served from files both processes map (share_blocks: one file in /dev/shm for the data,
+    one for the words), and cpu_seconds() is the child's own CPU time, so a pass can charge the
+    datanode's sender threads apart from the client's."""
+
+    SERVE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools", "loopback", "serve.py")
+
+    def __init__(self, packet_bytes: int | None = None):
+        import subprocess
+        import sys
+
+        self.p = subprocess.Popen([sys.executable, "-u", self.SERVE], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                  text=True, bufsize=1)
+        reply = self._reply()
+        if not reply.startswith("port "):
+            raise OSError(f"loopback child: {reply}")
+        self.port = int(reply.split()[1])
+        self.pid = self.p.pid
+        self._files = []
+        if packet_bytes:
+            self._cmd(f"packet_bytes {packet_bytes}")
+
+    def _reply(self) -> str:
+        line = self.p.stdout.readline()
+        if not line:
+            raise OSError(f"loopback child exited ({self.p.poll()})")
+        return line.strip()
+
+    def _cmd(self, line: str) -> str:
+        self.p.stdin.write(line + "\n")
+        self.p.stdin.flush()
+        reply = self._reply()
+        if reply.startswith("error"):
+            raise OSError(f"loopback child: {line!r}: {reply}")
+        return reply
+
+    def share_blocks(self, data: np.ndarray, crc: np.ndarray, blocks, bpc: int, tag: str = "blk"):
+        """Serve blocks = [(block_id, data_offset, length)] of `data` (words at 4 * offset / bpc of
+        `crc`). Returns the shared read-only view of the data (the bytes the child serves)."""
+        base = f"/dev/shm/hdfs3_{tag}_{os.getpid()}_{len(self._files)}"
+        paths = (base + "_data", base + "_crc")
+        arrs = []
+        for path, a in zip(paths, (data, crc)):
+            m = np.memmap(path, dtype=np.uint8, mode="w+", shape=(max(1, a.nbytes),))
+            m[:a.nbytes] = a.reshape(-1)
+            m.flush()
+            arrs.append(m)
+        try:
+            for bid, off, n in blocks:
+                self._cmd(f"add {bid} {paths[0]} {off} {n} {paths[1]} {4 * (off // bpc)} {bpc}")
+        finally:
+            for path in paths:  # both processes keep their mappings; the names go now
+                os.unlink(path)
+        self._files.append(arrs)
+        return arrs[0][:data.nbytes]
+
+    def cpu_seconds(self) -> float:
+        return float(self._cmd("cpu").split()[1])
+
+    def stop(self) -> None:
+        if self.p.poll() is None:
+            try:
+                self.p.stdin.write("quit\n")
+                self.p.stdin.flush()
+                self.p.wait(timeout=10)
+            except Exception:  # noqa: BLE001 - a child that does not quit is killed
+                self.p.kill()
+                self.p.wait()
+        self._files.clear()
 
 
 def reference_read_block(port: int, block_id: int, nbytes: int, out: np.ndarray, offset: int = 0, *,
