@@ -170,6 +170,26 @@ def gather_per_rank(dist, world, rank, row, device):
     return t.cpu().tolist()
 
 
+def rank_host_placement(device_index=None):
+    """[effective cores, NUMA node] of this rank: the cores a CPU baseline here may use (min of the
+    affinity and the cgroup quota, as cpu_baseline counts them) and the node of its GPU's PCI function
+    (hdfs3_device_numa_node; -1 when unknown or without a GPU)."""
+    affinity = max(1, len(os.sched_getaffinity(0)))
+    quota = cpu_quota_cores()
+    cores = max(1, min(affinity, int(quota))) if quota else affinity
+    node = -1
+    if device_index is not None:
+        try:
+            import ctypes
+            from libhdfs3_amd import _native
+            n = ctypes.c_int(-1)
+            if _native.lib().hdfs3_device_numa_node(int(device_index), ctypes.byref(n)) == 0:
+                node = n.value
+        except Exception:  # noqa: BLE001 - placement is reported, not required
+            node = -1
+    return [cores, node]
+
+
 def plumbing_check(args):
     """The N-rank entry without GPU work (CPU, gloo): every rank derives its own block set,
     then barrier -> a rank-dependent elapsed -> max over ranks -> per-rank rows on rank 0."""
@@ -185,12 +205,13 @@ def plumbing_check(args):
     elapsed = 1e-3 * (1 + rank)
     emax = max_over_ranks(dist, elapsed, torch.device("cpu")) if dist_ok else elapsed
     rows = gather_per_rank(dist, world, rank, [rank, int(os.environ.get("LOCAL_RANK", "0")), rank_seed(rank),
-                                               elapsed, os.getpid()], torch.device("cpu"))
+                                               elapsed, os.getpid()] + rank_host_placement(), torch.device("cpu"))
     if rank == 0:
         print(json.dumps({"plumbing_check": True, "n_gpus": world, "requested_gpus": args.gpus,
                           "elapsed_max": emax,
                           "per_rank": [{"rank": int(r[0]), "local_rank": int(r[1]), "seed": int(r[2]),
-                                        "elapsed": r[3], "pid": int(r[4])} for r in rows]}), flush=True)
+                                        "elapsed": r[3], "pid": int(r[4]), "cpu_cores": int(r[5]),
+                                        "numa_node": int(r[6])} for r in rows]}), flush=True)
     if dist_ok:
         dist.barrier()
         dist.destroy_process_group()
@@ -914,17 +935,19 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
             if check_out:
                 outbuf[::4096] = ~host_data[::4096]  # poison: every pass must rewrite the buffer
             reader_phases()
-            c0, d0 = time.process_time(), dn_cpu()
+            c0, d0, q0 = time.process_time(), dn_cpu(), cgroup_throttled_s()
             t0 = time.perf_counter()
             fn()
             dt = time.perf_counter() - t0
-            c1, d1 = time.process_time(), dn_cpu()
+            c1, d1, q1 = time.process_time(), dn_cpu(), cgroup_throttled_s()
             ph = reader_phases()
+            throttled = (q1 - q0) / dt if q0 is not None and q1 is not None else 0.0
             if check_out and not np.array_equal(outbuf, host_data):
                 bad = int(np.nonzero(outbuf != host_data)[0][0])
                 raise SystemExit(f"PARITY FAILURE: config5 delivered a wrong byte at {bad}")
             gib = total / 2**30
-            return (total / dt / 2**30, (c1 - c0) / gib, (d1 - d0) / gib) + tuple(x * 1e-9 / gib for x in ph)
+            return ((total / dt / 2**30, (c1 - c0) / gib, (d1 - d0) / gib) + tuple(x * 1e-9 / gib for x in ph) +
+                    (throttled,))
 
         phase_names = ("recv", "arena", "launch", "gpu_wait", "copy_out", "rx_wait_free_slot",
                        "caller_wait_batch", "receiver_cpu")
@@ -937,6 +960,9 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
                    "client_cpu_s_per_gib": round(med(1), 4)}
             if not own_dn:
                 out["datanode_cpu_s_per_gib"] = round(med(2), 4)
+            # the quota's throttling over the pass (cgroup cpu.stat), seconds per second of wall: > 0 means
+            # the box's CPU share, not the datanode or the GPU, held the pass back at times
+            out["cgroup_throttled_s_per_s"] = round(med(11), 4)
             if any(x[3 + i] for x in timed for i in range(8)):
                 # summed over the pass's block readers (threads): seconds per GiB delivered
                 out["reader_phase_s_per_gib"] = {n: round(med(3 + i), 4) for i, n in enumerate(phase_names)}
@@ -1185,6 +1211,21 @@ def cpu_quota_cores():
         return None
 
 
+def cgroup_throttled_s():
+    """CPU time this cgroup's tasks were throttled by its quota, in seconds (cpu.stat: cgroup v2
+    throttled_usec, v1 throttled_time in ns), or None when unknown."""
+    for path, key, scale in (("/sys/fs/cgroup/cpu.stat", "throttled_usec", 1e-6),
+                             ("/sys/fs/cgroup/cpu/cpu.stat", "throttled_time", 1e-9)):
+        try:
+            for line in open(path):
+                k, v = line.split()
+                if k == key:
+                    return int(v) * scale
+        except Exception:
+            continue
+    return None
+
+
 def cpu_baseline(work, seconds, bpc, data=None, crc=None):
     """Reference CPU path on this host, a bounded streaming sample of the same workload: the
     rank's whole block set (8 x 128 MiB = 1 GiB, host copies of the blocks and their CRC arrays),
@@ -1427,7 +1468,8 @@ def main():
     props = torch.cuda.get_device_properties(torch.cuda.current_device())
     pci = [getattr(props, "pci_domain_id", -1), getattr(props, "pci_bus_id", -1), getattr(props, "pci_device_id", -1)]
     rows = gather_per_rank(dist, world, rank, [rank, torch.cuda.current_device(), rank_seed(rank), elapsed,
-                                               host_elapsed, my_rate] + pci, coll_device)
+                                               host_elapsed, my_rate] + pci +
+                           rank_host_placement(torch.cuda.current_device()), coll_device)
     dist_world = dist.get_world_size() if dist.is_initialized() else 1
     elapsed_max = max(r[3] for r in rows)
     host_max = max(r[4] for r in rows)
@@ -1551,7 +1593,9 @@ def main():
         "roofline": roofline, "cpu_baseline": cpu,
         "per_rank": [{"rank": int(r[0]), "current_device": int(r[1]), "pci": [int(x) for x in r[6:9]],
                       "seed": int(r[2]), "ms_per_step": round(r[3] / K * 1e3, 4), "value": round(r[5], 2),
-                      "frac": round(alg_bytes * K / r[3] / 1e9 / HBM_PEAK_GBPS, 4)} for r in rows],
+                      "frac": round(alg_bytes * K / r[3] / 1e9 / HBM_PEAK_GBPS, 4),
+                      # the cores a CPU baseline on this rank's host share may use, and its GPU's NUMA node
+                      "cpu_cores": int(r[9]), "numa_node": int(r[10])} for r in rows],
         "distinct_devices": distinct,
     }
     if "barriered" in extra:

@@ -46,7 +46,6 @@ constexpr int kDefaultBatchPackets = 64;
 constexpr int kDefaultTimeoutMs = 60000;  // input.read.timeout default (SessionConfig.cpp)
 constexpr size_t kMaxResponse = 10u << 20;  // RemoteBlockReader.cpp:116
 constexpr int kSlots = 3;                  // receiving / verifying / delivering
-constexpr int kWaitPollUs = 20;            // the caller's sleep between polls of a batch's event
 constexpr int kPhases = 8;                 // hdfs3_reader_phase_ns
 std::atomic<uint64_t> g_phase_ns[kPhases] = {};
 
@@ -166,7 +165,7 @@ int grow(PacketArena &a, size_t cap, size_t descs) {
     if (!a.d_res) {
         HIP_OK(hipMalloc(reinterpret_cast<void **>(&a.d_res), sizeof(unsigned long long)));
         HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&a.h_res), sizeof(unsigned long long), pinned_host_flags()));
-        HIP_OK(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&a.done, hipEventDisableTiming | hipEventBlockingSync));
     }
     return 0;
 }
@@ -219,9 +218,10 @@ struct hdfs3_block_reader {
     // waits for a free slot, the caller's waits for a ready batch, the receiver thread's CPU time:
     // summed into g_phase_ns when the reader closes (hdfs3_reader_phase_ns)
     std::atomic<uint64_t> t_ns[kPhases] = {};
-    // How the caller waits for a batch's verify (round 6): by default it polls the batch's event and
-    // sleeps between polls, so a waiting caller leaves its core to the receivers and the datanode;
-    // HDFS3_READER_WAIT=spin keeps hipEventSynchronize's busy wait (the behaviour before round 6)
+    // How the caller waits for a batch's verify (round 6): the batch's event is a blocking-sync event, so
+    // a waiting caller sleeps until the GPU signals and leaves its core to the receivers and the
+    // datanode; HDFS3_READER_WAIT=spin (measurement knob) polls the event in a busy loop, as
+    // hipEventSynchronize did on the spinning events before round 6
     bool spin_wait = false;
 
     int sticky(int code, const std::string &msg) {
@@ -501,14 +501,13 @@ struct hdfs3_block_reader {
         if (b.verified) return 0;
         Timer tm(t_ns[3]);
         if (spin_wait) {
-            HIP_OK(hipEventSynchronize(b.a.done));
-        } else {
             for (;;) {
                 const hipError_t q = hipEventQuery(b.a.done);
                 if (q == hipSuccess) break;
                 if (q != hipErrorNotReady) HIP_OK(q);
-                std::this_thread::sleep_for(std::chrono::microseconds(kWaitPollUs));
             }
+        } else {
+            HIP_OK(hipEventSynchronize(b.a.done));
         }
         const unsigned long long r = *b.a.h_res;
         if (r && b.dense) {  // the first bad chunk of the batch -> its packet
@@ -671,7 +670,10 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
     *out = nullptr;
     hdfs3_block_reader *r = new (std::nothrow) hdfs3_block_reader();
     if (!r) return fail(-ENOMEM, "reader allocation");
-    r->slot.resize(size_t(std::min(std::max(slots > 0 ? slots : kSlots, kSlots), kMaxSlots)));
+    int nslots = slots > 0 ? slots : kSlots;
+    if (const char *e = getenv("HDFS3_READER_SLOTS"); e && slots <= 0)  // measurement knob (config5_ab)
+        nslots = std::atoi(e);
+    r->slot.resize(size_t(std::min(std::max(nslots, kSlots), kMaxSlots)));
     r->prefetch = slots > 0;
     {
         const char *w = getenv("HDFS3_READER_WAIT");
@@ -680,6 +682,10 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
     const int device = opts ? opts->device : 0;
     r->verify = opts ? opts->verify != 0 : true;
     if (opts && opts->batch_packets > 0) r->batch_packets = opts->batch_packets;
+    if (const char *bp = getenv("HDFS3_READER_BATCH_PACKETS")) {  // measurement knob (tools/config5_ab.py)
+        const int v = std::atoi(bp);
+        if (v > 0 && v <= 1024) r->batch_packets = v;
+    }
     if (opts && opts->timeout_ms > 0) r->timeout_ms = opts->timeout_ms;
     r->block.pool_id = blk->pool_id ? blk->pool_id : "";
     r->block.block_id = blk->block_id;

@@ -112,6 +112,10 @@ struct HdfsFileInternalWrapper {
     BlockTable prefix;               // append: the file's blocks before the pipeline's first one
     std::string path;
     int64_t block_size = 0;          // the write's block size (the file's, for FileStatus)
+    // the size is the file's own: a create, a size registered for the path, or one a file of two or
+    // more blocks states; an append to a one-block file of unknown size only guessed it,
+    // and a guess is not recorded as the file's block size
+    bool block_size_known = false;
 };
 
 extern "C" {
@@ -240,6 +244,7 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
         if (write) {
             hdfs3_writer_opts o = fs->wopts;
             if (blocksize > 0) o.block_size = blocksize;
+            bool size_known = !append;  // a create sets the file's block size
             if (append) {
                 // the reference appends with the file's own block size (FileStatus::getBlockSize,
                 // OutputStreamImpl.cpp:196-230): the size registered for the path (hdfs3_fs_set_block_size,
@@ -257,6 +262,7 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
                         return nullptr;
                     }
                     o.block_size = fbs;
+                    size_known = true;
                 }
                 for (size_t i = 0; i < lbs.size(); ++i) {
                     const int64_t nb = int64_t(lbs[i].block.num_bytes);
@@ -303,6 +309,7 @@ hdfsFile hdfsOpenFile(hdfsFS fs, const char *path, int flags, int bufferSize, sh
             if (e.pipeline || (last && !e.sink)) {  // datanodes: PipelineImpl behind the stream
                 file->path = path;
                 file->block_size = o.block_size;
+                file->block_size_known = size_known;
                 BlockTable t;
                 std::vector<hdfs3_located_block> pb;
                 if (last) pb.push_back(*last);  // its replicas are the append pipeline's nodes
@@ -374,7 +381,7 @@ void complete_written_file(hdfsFS fs, hdfsFile file) {
     FileEntry &slot = fs->files[file->path];
     slot.located_blocks.assign(all.data(), int(all.size()));
     slot.located = true;
-    slot.block_size = file->block_size;  // what FileStatus reports for the file from now on
+    if (file->block_size_known) slot.block_size = file->block_size;  // what FileStatus reports from now on
 }
 }  // namespace
 

@@ -2,6 +2,7 @@
 
 #include <arpa/inet.h>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <fcntl.h>
 #include <netdb.h>
@@ -108,6 +109,8 @@ int read_fully(int fd, void *buf, size_t n, int timeout_ms) {
         if (errno == EINTR) continue;
         if (errno != EAGAIN && errno != EWOULDBLOCK) return -errno;
         if (n >= kWaitAllMin && timeout_ms > 0) {
+            // the socket's SO_RCVTIMEO is this call's timeout (the connection's one timeout: callers
+            // pass the same value on every read of a socket)
             timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
             if (setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv)) == 0) {
                 const ssize_t w = ::recv(fd, p, n, MSG_WAITALL);
@@ -118,58 +121,14 @@ int read_fully(int fd, void *buf, size_t n, int timeout_ms) {
                 }
                 if (w == 0) return -ECONNRESET;
                 if (errno == EINTR) continue;
-                // EAGAIN: SO_RCVTIMEO expired with nothing, or the socket is non-blocking after all:
-                // the poll below decides (ready: read on; its own timeout: -ETIMEDOUT)
-                if (errno != EAGAIN && errno != EWOULDBLOCK) return -errno;
+                // EAGAIN with nothing read: SO_RCVTIMEO expired, the whole timeout has passed (ADVICE
+                // r5: waiting again in poll doubled it)
+                if (errno == EAGAIN || errno == EWOULDBLOCK) return -ETIMEDOUT;
+                return -errno;
             }
         }
         // poll: a blocking recv without SO_RCVTIMEO would ignore the timeout
         if (const int rc = wait_fd(fd, POLLIN, timeout_ms)) return rc;
-    }
-    return 0;
-}
-
-int read_fully2(int fd, void *a, size_t na, void *b, size_t nb, int timeout_ms) {
-    iovec v[2] = {{a, na}, {b, nb}};
-    int first = na ? 0 : 1;
-    while (first < 2) {
-        msghdr m{};
-        m.msg_iov = v + first;
-        m.msg_iovlen = size_t(2 - first);
-        const size_t want = v[first].iov_len + (first == 0 ? v[1].iov_len : 0);
-        ssize_t r = ::recvmsg(fd, &m, MSG_DONTWAIT);
-        if (r < 0 && errno == EINTR) continue;
-        if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-            r = 0;
-            if (want >= kWaitAllMin && timeout_ms > 0) {
-                timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
-                if (setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv)) == 0) {
-                    r = ::recvmsg(fd, &m, MSG_WAITALL);
-                    if (r < 0 && errno == EINTR) continue;
-                    if (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK) return -errno;
-                    if (r == 0) return -ECONNRESET;
-                    if (r < 0) r = 0;
-                }
-            }
-            if (r == 0) {
-                if (const int rc = wait_fd(fd, POLLIN, timeout_ms)) return rc;
-                continue;
-            }
-        } else if (r < 0) {
-            return -errno;
-        } else if (r == 0) {
-            return -ECONNRESET;
-        }
-        // advance over what arrived
-        size_t got = size_t(r);
-        while (got && first < 2) {
-            const size_t take = got < v[first].iov_len ? got : v[first].iov_len;
-            v[first].iov_base = static_cast<char *>(v[first].iov_base) + take;
-            v[first].iov_len -= take;
-            got -= take;
-            if (v[first].iov_len == 0) ++first;
-        }
-        while (first < 2 && v[first].iov_len == 0) ++first;
     }
     return 0;
 }

@@ -16,15 +16,17 @@ int connect_tcp(const char *host, int port, int timeout_ms);
 int listen_tcp(int port, int *bound_port);
 // 0 on success, -errno on failure (-ETIMEDOUT, -ECONNRESET on EOF)
 int read_fully(int fd, void *buf, size_t n, int timeout_ms);
-// na bytes into a, then nb bytes into b, in as few recvmsg calls as the data allows (one when it is
-// buffered or arrives within the timeout): a packet's checksums and data into two places
-int read_fully2(int fd, void *a, size_t na, void *b, size_t nb, int timeout_ms);
 // Blocking reads for a socket whose SO_RCVTIMEO was set once (set_recv_timeout): one recv/recvmsg with
 // MSG_WAITALL per message when it arrives within the timeout, the way RemoteBlockReader's reading thread
 // does it — no poll or setsockopt per call (round 5: the block reader's receiver spent ~4 syscalls per
 // packet on them). -ETIMEDOUT when the timeout passes with the message incomplete, -ECONNRESET at EOF.
 int set_recv_timeout(int fd, int timeout_ms);
 int recv_fully(int fd, void *buf, size_t n);
+// na bytes into a, then nb bytes into b (a packet's checksums and data into two places). Round 6
+// measured a non-blocking spin before the blocking receive (a receiver polling for data it expects
+// instead of sleeping until the sender wakes it): 50 / 200 us of spin took one loopback stream from
+// 6.0-7.4 to 3.9-4.5 GiB/s and raised the datanode's CPU per GiB by half (profiles/r06/r6g_*): a
+// receiver that takes each packet in one MSG_WAITALL receive is the cheapest for the sender too.
 int recv_fully2(int fd, void *a, size_t na, void *b, size_t nb);
 int write_fully(int fd, const void *buf, size_t n, int timeout_ms);
 // protobuf varint32 length prefix, as BufferedSocketReader::readVarint32

@@ -590,7 +590,7 @@ struct Footprint {
 };
 
 // what a ctx holds beyond its tables: pinned host and device bytes of its staging slots, cached
-// arenas, descriptor stagings, word scratch and result word
+// arenas (with their piece scratch), descriptor stagings, word and piece scratch and result word
 Footprint footprint(hdfs3_crc_ctx *ctx) {
     Footprint f;
     for (const Slot &s : ctx->slot) {
@@ -602,7 +602,8 @@ Footprint footprint(hdfs3_crc_ctx *ctx) {
         for (const PacketArena &a : ctx->arena_cache) {
             const uint64_t desc = a.desc_cap * sizeof(DevSegment) + (a.h_res ? sizeof(unsigned long long) : 0);
             f.pinned += a.cap + desc;
-            f.device += a.cap + desc;
+            // the arena's own piece scratch (bpc = R x 4096 batches) stays allocated while it is cached
+            f.device += a.cap + desc + a.pieces.cap[0] + a.pieces.cap[1];
         }
     }
     for (const auto &st : ctx->seg_ring) {
@@ -610,7 +611,7 @@ Footprint footprint(hdfs3_crc_ctx *ctx) {
         f.device += st.cap * sizeof(DevSegment);
     }
     f.pinned += sizeof(unsigned long long);
-    f.device += ctx->words.cap + sizeof(unsigned long long);
+    f.device += ctx->words.cap + ctx->pieces.cap[0] + ctx->pieces.cap[1] + sizeof(unsigned long long);
     for (int p = 0; p < 2; ++p) f.device += sizeof(host_images()[p].t) + kFoldUploadBytes;
     return f;
 }

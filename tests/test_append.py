@@ -409,3 +409,32 @@ def test_gpu_hdfs_append_one_block_file_uses_its_own_block_size(nodes):
         assert not f and ctypes.get_errno() == errno.EINVAL
     finally:
         h.close()
+
+
+@pytest.mark.gpu
+def test_gpu_hdfs_append_guessed_block_size_is_not_recorded(nodes):
+    """an append to a one-block file of unknown block size only guesses the size (the
+    caller's, else the session's). A clean close must not record that guess as the file's FileStatus
+    block size: a later append with another caller size is not refused for "block size differs", and
+    appends with that caller's size."""
+    h = Hdfs()
+    try:
+        chain = [(HOST, d.port) for d in nodes]
+        path = b"/append/guess"
+        one, data = existing_file(nodes, 3000, 990, 71)
+        h.add_file(path, [(bid, n, chain) for bid, n in one])
+        a1, a2 = splitmix_bytes(700, 72), splitmix_bytes(900, 73)
+        assert h.lib.hdfs3_fs_set_append_stamp(h.fs, path, 40) == 0
+        f = h.lib.hdfsOpenFile(h.fs, path, os.O_WRONLY | os.O_APPEND, 0, 0, BS)  # a guess: 1 MiB
+        assert f, h.lib.hdfsGetLastError()
+        assert h.lib.hdfsWrite(h.fs, f, a1.ctypes.data, a1.nbytes) == a1.nbytes
+        assert h.lib.hdfsCloseFile(h.fs, f) == 0, h.lib.hdfsGetLastError()
+        assert h.lib.hdfs3_fs_set_append_stamp(h.fs, path, 41) == 0
+        f = h.lib.hdfsOpenFile(h.fs, path, os.O_WRONLY | os.O_APPEND, 0, 0, BS // 2)  # another guess
+        assert f, h.lib.hdfsGetLastError()
+        assert h.lib.hdfsWrite(h.fs, f, a2.ctypes.data, a2.nbytes) == a2.nbytes
+        assert h.lib.hdfsCloseFile(h.fs, f) == 0, h.lib.hdfsGetLastError()
+        whole = np.concatenate([data, a1, a2])
+        assert np.array_equal(h.read_file(path, whole.size), whole)
+    finally:
+        h.close()

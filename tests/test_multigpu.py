@@ -47,6 +47,20 @@ def test_bench_gpus_4_spawns_four_ranks_cpu():
     assert j["n_gpus"] == 4 and len({r["seed"] for r in j["per_rank"]}) == 4
 
 
+def test_bench_gpus_8_spawns_eight_ranks_cpu():
+    """The driver's N = 8 shape (configs[3]: one 128 MiB block set per GPU) through the real entry: 8
+    rank processes, 8 distinct block sets, the max-over-ranks time, and every rank's host placement
+    (the cores its CPU baseline may use, its GPU's NUMA node: -1 without a GPU) in per_rank."""
+    j = _bench("--gpus", "8", "--plumbing-check", timeout=240)
+    ranks = j["per_rank"]
+    assert j["n_gpus"] == 8 and [r["rank"] for r in ranks] == list(range(8))
+    assert [r["local_rank"] for r in ranks] == list(range(8))
+    assert len({r["seed"] for r in ranks}) == 8 and len({r["pid"] for r in ranks}) == 8
+    assert j["elapsed_max"] == pytest.approx(max(r["elapsed"] for r in ranks))
+    for r in ranks:
+        assert r["cpu_cores"] >= 1 and r["numa_node"] == -1
+
+
 @pytest.mark.gpu
 def test_bench_gpus_2_real_run_on_one_gpu():
     """`--gpus 2` end to end on the box: two ranks (both on cuda:0 here, one per GPU on a
@@ -78,6 +92,7 @@ def _check_scaling_fields(j, n):
     assert r["aggregate_frac"] == pytest.approx(n * alg / (j["ms_per_step"] * 1e-3) / 1e9 / (n * 8000.0), rel=tol)
     for p in j["per_rank"]:
         assert p["frac"] == pytest.approx(alg / (p["ms_per_step"] * 1e-3) / 1e9 / 8000.0, rel=tol)
+        assert p["cpu_cores"] >= 1 and p["numa_node"] >= -1
     # the whole job's fraction is the slowest rank's (weak scaling, max-over-ranks time)
     assert min(p["frac"] for p in j["per_rank"]) == pytest.approx(r["aggregate_frac"], abs=1.5e-4)
     assert j["distinct_devices"]["checked"] is False and "visible GPU" in j["distinct_devices"]["why"]
