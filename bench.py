@@ -888,14 +888,18 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
                         raise SystemExit(f"config5: hdfsRead returned {got} at {pos}")
                     pos += got
 
+        caller_cpu = [0.0]  # CPU seconds of the threads that called the read API in the current pass
+
         def threads(fn):
             errs = []
 
             def one(i):
+                t0 = time.thread_time()
                 try:
                     fn(i)
                 except Exception as e:  # noqa: BLE001 - reported below
                     errs.append(f"block {i}: {e}")
+                caller_cpu[0] += time.thread_time() - t0  # (+= of floats under the GIL)
             th = [threading.Thread(target=one, args=(i,)) for i in range(nblk)]
             for t in th:
                 t.start()
@@ -935,10 +939,13 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
             if check_out:
                 outbuf[::4096] = ~host_data[::4096]  # poison: every pass must rewrite the buffer
             reader_phases()
+            caller_cpu[0] = 0.0
             c0, d0, q0 = time.process_time(), dn_cpu(), cgroup_throttled_s()
+            m0 = time.thread_time()
             t0 = time.perf_counter()
             fn()
             dt = time.perf_counter() - t0
+            m1 = time.thread_time()
             c1, d1, q1 = time.process_time(), dn_cpu(), cgroup_throttled_s()
             ph = reader_phases()
             throttled = (q1 - q0) / dt if q0 is not None and q1 is not None else 0.0
@@ -946,8 +953,10 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
                 bad = int(np.nonzero(outbuf != host_data)[0][0])
                 raise SystemExit(f"PARITY FAILURE: config5 delivered a wrong byte at {bad}")
             gib = total / 2**30
+            # the calling threads' own CPU: the pass's worker threads, or this thread for a one-stream pass
+            callers = caller_cpu[0] + (m1 - m0)
             return ((total / dt / 2**30, (c1 - c0) / gib, (d1 - d0) / gib) + tuple(x * 1e-9 / gib for x in ph) +
-                    (throttled,))
+                    (throttled, callers / gib))
 
         phase_names = ("recv", "arena", "launch", "gpu_wait", "copy_out", "rx_wait_free_slot",
                        "caller_wait_batch", "receiver_cpu")
@@ -963,6 +972,9 @@ def config5_block(torch, device, host_data, bpc, block_bytes, reps=3, read_mib=4
             # the quota's throttling over the pass (cgroup cpu.stat), seconds per second of wall: > 0 means
             # the box's CPU share, not the datanode or the GPU, held the pass back at times
             out["cgroup_throttled_s_per_s"] = round(med(11), 4)
+            # of client_cpu_s_per_gib: the threads that called the read API (hdfsRead / hdfsPread, or the
+            # reference loop's own), the rest being the library's receivers and the HIP runtime's threads
+            out["caller_threads_cpu_s_per_gib"] = round(med(12), 4)
             if any(x[3 + i] for x in timed for i in range(8)):
                 # summed over the pass's block readers (threads): seconds per GiB delivered
                 out["reader_phase_s_per_gib"] = {n: round(med(3 + i), 4) for i, n in enumerate(phase_names)}

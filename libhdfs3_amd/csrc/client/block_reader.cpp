@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <time.h>
 
 #include <algorithm>
@@ -194,6 +195,13 @@ struct hdfs3_block_reader {
     std::atomic<bool> local_fault{false};  // the failure is this host's GPU/memory, not the replica
     bool have_pending_hdr = false;
     wire::PacketHeader pending_hdr;
+    // Header read-ahead (round 6): every data packet is followed on the wire by another packet's fixed
+    // 31-byte header (the next data packet's, or the empty last packet's, RemoteBlockReader.cpp:274-286),
+    // so a packet's payload receive takes that header too: one receive per packet instead of two.
+    // HDFS3_READER_HEADER_AHEAD=0 (measurement knob) reads each header on its own as before.
+    bool header_ahead = true;
+    bool have_next_raw = false;
+    uint8_t next_raw[wire::kPacketHeaderSize];
 
     // shared between receiver and caller, under mu
     std::mutex mu;
@@ -273,6 +281,11 @@ struct hdfs3_block_reader {
             have_pending_hdr = false;
             return 0;
         }
+        if (have_next_raw) {  // received with the previous packet's payload
+            have_next_raw = false;
+            if (!h.decode(next_raw, sizeof(next_raw))) return rx_fail(-EPROTO, "Invalid PacketHeader");
+            return 0;
+        }
         uint8_t buf[wire::kPacketHeaderSize];
         if (int rc = net::recv_fully(fd, buf, sizeof(buf)))
             return rx_fail(rc, "RemoteBlockReader: failed to read block header");
@@ -327,9 +340,11 @@ struct hdfs3_block_reader {
                     break;
                 }
                 // the packet's checksums and data in one scatter read (:244-245 reads them as one buffer)
-                if (int rc = net::recv_fully2(fd, b.a.h + b.words_used, crc_len, b.a.h + b.d0 + b.data_used,
-                                              size_t(h.data_len)))
+                iovec v[3] = {{b.a.h + b.words_used, crc_len}, {b.a.h + b.d0 + b.data_used, size_t(h.data_len)},
+                              {next_raw, header_ahead ? sizeof(next_raw) : 0}};
+                if (int rc = net::recv_fully_iov(fd, v, 3))
                     return rx_fail(rc, "RemoteBlockReader: failed to read packet payload");
+                have_next_raw = header_ahead;
                 last_seqno = h.seqno;
                 packets.fetch_add(1, std::memory_order_relaxed);
                 int64_t ahead = recv_cursor - h.offset_in_block;
@@ -361,8 +376,10 @@ struct hdfs3_block_reader {
                 if (int rc = grow(b.a, size + 64, size_t(batch_packets))) return rx_fail(rc, "arena growth failed");
                 off = ((crc_len + 15) & ~uint64_t(15)) - crc_len;
             }
-            if (int rc = net::recv_fully(fd, b.a.h + off, size))
+            iovec v[2] = {{b.a.h + off, size}, {next_raw, header_ahead ? sizeof(next_raw) : 0}};
+            if (int rc = net::recv_fully_iov(fd, v, 2))
                 return rx_fail(rc, "RemoteBlockReader: failed to read packet payload");
+            have_next_raw = header_ahead;
             last_seqno = h.seqno;
             packets.fetch_add(1, std::memory_order_relaxed);
             int64_t ahead = recv_cursor - h.offset_in_block;
@@ -678,6 +695,8 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
     {
         const char *w = getenv("HDFS3_READER_WAIT");
         r->spin_wait = w && std::strcmp(w, "spin") == 0;
+        const char *ha = getenv("HDFS3_READER_HEADER_AHEAD");
+        r->header_ahead = !(ha && ha[0] == '0');
     }
     const int device = opts ? opts->device : 0;
     r->verify = opts ? opts->verify != 0 : true;

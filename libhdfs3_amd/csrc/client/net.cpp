@@ -138,13 +138,13 @@ int set_recv_timeout(int fd, int timeout_ms) {
     return setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv)) == 0 ? 0 : -errno;
 }
 
-int recv_fully2(int fd, void *a, size_t na, void *b, size_t nb) {
-    iovec v[2] = {{a, na}, {b, nb}};
-    int first = na ? 0 : 1;
-    while (first < 2 && v[first].iov_len) {
+int recv_fully_iov(int fd, iovec *v, int n) {
+    int first = 0;
+    while (first < n && v[first].iov_len == 0) ++first;
+    while (first < n) {
         msghdr m{};
         m.msg_iov = v + first;
-        m.msg_iovlen = size_t(2 - first);
+        m.msg_iovlen = size_t(n - first);
         const ssize_t r = ::recvmsg(fd, &m, MSG_WAITALL);
         if (r < 0) {
             if (errno == EINTR) continue;
@@ -152,16 +152,21 @@ int recv_fully2(int fd, void *a, size_t na, void *b, size_t nb) {
         }
         if (r == 0) return -ECONNRESET;
         size_t got = size_t(r);
-        while (got && first < 2) {
+        while (got && first < n) {
             const size_t take = got < v[first].iov_len ? got : v[first].iov_len;
             v[first].iov_base = static_cast<char *>(v[first].iov_base) + take;
             v[first].iov_len -= take;
             got -= take;
             if (v[first].iov_len == 0) ++first;
         }
-        while (first < 2 && v[first].iov_len == 0) ++first;
+        while (first < n && v[first].iov_len == 0) ++first;
     }
     return 0;
+}
+
+int recv_fully2(int fd, void *a, size_t na, void *b, size_t nb) {
+    iovec v[2] = {{a, na}, {b, nb}};
+    return recv_fully_iov(fd, v, 2);
 }
 
 int recv_fully(int fd, void *buf, size_t n) { return recv_fully2(fd, buf, n, nullptr, 0); }

@@ -7,6 +7,8 @@
 #include <cstdint>
 #include <string>
 
+#include <sys/uio.h>
+
 namespace hdfs3crc {
 namespace net {
 
@@ -28,6 +30,9 @@ int recv_fully(int fd, void *buf, size_t n);
 // 6.0-7.4 to 3.9-4.5 GiB/s and raised the datanode's CPU per GiB by half (profiles/r06/r6g_*): a
 // receiver that takes each packet in one MSG_WAITALL receive is the cheapest for the sender too.
 int recv_fully2(int fd, void *a, size_t na, void *b, size_t nb);
+// n pieces in order, as few MSG_WAITALL receives as the data allows (the block reader takes a packet's
+// checksums, its data and the NEXT packet's fixed 31-byte header in one: one receive per packet)
+int recv_fully_iov(int fd, iovec *v, int n);
 int write_fully(int fd, const void *buf, size_t n, int timeout_ms);
 // protobuf varint32 length prefix, as BufferedSocketReader::readVarint32
 int read_varint32(int fd, uint32_t *out, int timeout_ms);

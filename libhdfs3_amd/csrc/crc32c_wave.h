@@ -45,6 +45,7 @@ constexpr int kLabStorePlain = 8192;  // compute, staged words: plain global sto
 constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every launch size (production before round 4)
 constexpr int kLabNoTabLoad = 2097152;  // diagnostic: the table images are not loaded (made up from t: wrong results)
 constexpr int kLabFull16 = 8388608;  // the round-4 chains: 16 table steps per chain, the fold on the finished state
+constexpr int kLabOneRound = 4194304;  // launches of <= 4096 units: one round per wave (twice the workgroups)
 constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = fill done | first data << 21 | kernel
                                      // arguments landed << 42, each - start, 21 bits of 10 ns
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
@@ -780,7 +781,8 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     constexpr int set = G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3;
     const uint32_t *nib = fold + ((LAB & kLabFull16) ? kFoldAffineOldOff : kFoldAffineOff) + set * kFoldNibbleWords;
     const uint64_t units = PITCH ? (a.npk - 1) * a.geom.upp + a.geom.lunits : a.len / kRoundBytes;
-    const uint64_t need = (units + 2 * (TPB / 64) - 1) / (2 * (TPB / 64));
+    const uint64_t rpw = (LAB & kLabOneRound) != 0 && units <= 4096 ? 1 : 2;  // rounds per wave planned
+    const uint64_t need = (units + rpw * (TPB / 64) - 1) / (rpw * (TPB / 64));
     int grid = int(need < uint64_t(grid_cap) ? need : uint64_t(grid_cap));
     if (grid < 1) grid = 1;
     // units over the grid's waves: wave w takes kq rounds, plus one when w < kr (32-bit round counts:

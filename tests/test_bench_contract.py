@@ -59,4 +59,19 @@ def test_bench_json_line(mode):
         assert c5["reference_cpu_verify"]["kind"] == "reference" and c5["reference_cpu_verify"]["gib_s"] > 0
         assert c5["reference_cpu_write_sink"]["gib_s"] > 0 and "checked" in c5["hdfsWrite_sink"]
         pr = j["config5"]["paired_gpu_over_reference_cpu"]
-        assert pr["verify"] > 0 and pr["no_verify"] > 0
+        for k in ("verify", "no_verify", "verify_8_streams", "no_verify_8_streams"):
+            assert pr[k]["rate"] > 0 and pr[k]["client_cpu"] > 0, k
+        # round 6: 8 concurrent streams on both paths, CPU-seconds per GiB on every read line, the
+        # datanode in its own process (its CPU apart), the reader's phases on the GPU lines
+        for k in ("hdfsPread8_verify", "reference_cpu8_verify"):
+            assert c5[k]["gib_s"] > 0 and c5[k]["streams"] == 8, k
+        for k in ("hdfsRead_verify", "reference_cpu_verify", "hdfsPread8_verify", "reference_cpu8_verify"):
+            assert c5[k]["client_cpu_s_per_gib"] > 0 and c5[k]["datanode_cpu_s_per_gib"] > 0, k
+            assert "cgroup_throttled_s_per_s" in c5[k], k
+        ph = c5["hdfsPread8_verify"]["reader_phase_s_per_gib"]
+        assert ph["recv"] > 0 and ph["receiver_cpu"] > 0
+        assert j["config5"]["datanode"].startswith("a child process")
+    # round 6: the output stream's own 64-packet batch (127-chunk packets at bpc 512), device-resident
+    wb = j["packets"]["writer_batch"]
+    assert wb["chunks_per_packet"] == 127 and wb["packet_data_bytes"] == 65024 and wb["packets_per_batch"] == 64
+    assert wb["compute_us"] > 0 and 0 < wb["compute_frac"] < 1 and wb["reader_dense_us"] > 0
