@@ -48,6 +48,7 @@ constexpr int kDefaultTimeoutMs = 60000;  // input.read.timeout default (Session
 constexpr size_t kMaxResponse = 10u << 20;  // RemoteBlockReader.cpp:116
 constexpr int kSlots = 3;                  // receiving / verifying / delivering
 constexpr int kPhases = 8;                 // hdfs3_reader_phase_ns
+constexpr int kWaitPollUs = 20;            // the caller's sleep between queries of a batch's event
 std::atomic<uint64_t> g_phase_ns[kPhases] = {};
 
 uint64_t thread_cpu_ns() {
@@ -226,11 +227,12 @@ struct hdfs3_block_reader {
     // waits for a free slot, the caller's waits for a ready batch, the receiver thread's CPU time:
     // summed into g_phase_ns when the reader closes (hdfs3_reader_phase_ns)
     std::atomic<uint64_t> t_ns[kPhases] = {};
-    // How the caller waits for a batch's verify (round 6): the batch's event is a blocking-sync event, so
-    // a waiting caller sleeps until the GPU signals and leaves its core to the receivers and the
-    // datanode; HDFS3_READER_WAIT=spin (measurement knob) polls the event in a busy loop, as
-    // hipEventSynchronize did on the spinning events before round 6
-    bool spin_wait = false;
+    // How the caller waits for a batch's verify (round 6). Default: it queries the batch's event and
+    // sleeps kWaitPollUs between queries, leaving its core to the receivers and the datanode. Measured
+    // on config 5 (profiles/r06): a blocking-sync hipEventSynchronize still spun inside the runtime (the
+    // 8-stream callers burnt 0.165 CPU-s per GiB, 0.057 of it copying), and a busy query loop, the
+    // behaviour before round 6, more. HDFS3_READER_WAIT=block / spin (measurement knobs) select those.
+    enum WaitMode { kWaitPoll, kWaitBlock, kWaitSpin } wait_mode = kWaitPoll;
 
     int sticky(int code, const std::string &msg) {
         error = code;
@@ -517,14 +519,15 @@ struct hdfs3_block_reader {
     int wait(Batch &b) {
         if (b.verified) return 0;
         Timer tm(t_ns[3]);
-        if (spin_wait) {
+        if (wait_mode == kWaitBlock) {
+            HIP_OK(hipEventSynchronize(b.a.done));  // a blocking-sync event (grow())
+        } else {
             for (;;) {
                 const hipError_t q = hipEventQuery(b.a.done);
                 if (q == hipSuccess) break;
                 if (q != hipErrorNotReady) HIP_OK(q);
+                if (wait_mode == kWaitPoll) std::this_thread::sleep_for(std::chrono::microseconds(kWaitPollUs));
             }
-        } else {
-            HIP_OK(hipEventSynchronize(b.a.done));
         }
         const unsigned long long r = *b.a.h_res;
         if (r && b.dense) {  // the first bad chunk of the batch -> its packet
@@ -694,7 +697,10 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
     r->prefetch = slots > 0;
     {
         const char *w = getenv("HDFS3_READER_WAIT");
-        r->spin_wait = w && std::strcmp(w, "spin") == 0;
+        r->wait_mode = !w                            ? hdfs3_block_reader::kWaitPoll
+                       : std::strcmp(w, "spin") == 0  ? hdfs3_block_reader::kWaitSpin
+                       : std::strcmp(w, "block") == 0 ? hdfs3_block_reader::kWaitBlock
+                                                      : hdfs3_block_reader::kWaitPoll;
         const char *ha = getenv("HDFS3_READER_HEADER_AHEAD");
         r->header_ahead = !(ha && ha[0] == '0');
     }
