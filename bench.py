@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     # 1000 warmup launches (~25 ms): the GPU needs ~25 ms of sustained load to leave its
     # idle power state; with 10 warmup launches the first ~1000 timed launches run ~15 %
-    # slower (W=10 27.0 us/launch, W=100 24.2, W>=1000 23.3, same box)
+    # slower (docs/DESIGN_HISTORY.md §5: W=10 27.0 us/launch, W=100 24.2, W>=1000 23.3, same box)
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=1000)
     p.add_argument("--bpc", type=int, default=512)
@@ -72,7 +72,7 @@ def parse():
     p.add_argument("--sweep", action="store_true", help="extra diagnostics on stderr")
     p.add_argument("--graph", action="store_true",
                    help="replay the K steps from captured HIP graphs instead of launching them eagerly "
-                        "(no consistent gain measured: DESIGN.md §5)")
+                        "(no consistent gain measured: docs/DESIGN_HISTORY.md §5)")
     p.add_argument("--no-overlap", action="store_true",
                    help="barrier every timed launch (no HDFS3_LAUNCH_OVERLAP_PREVIOUS); the overlapped "
                         "run is the default and the barriered one is reported beside it")
@@ -229,7 +229,7 @@ class Workload:
         self.data = torch.randint(0, 256, (blocks, block_bytes), dtype=torch.uint8, device=device, generator=g)
         self.crc = torch.empty((blocks, 4 * self.nchunks), dtype=torch.uint8, device=device)
         # device pointers resolved once: the timed loops index plain lists, not tensors (a tensor
-        # index costs the box's host several us per launch, DESIGN.md §5 "short timed regions")
+        # index costs the box's host several us per launch, docs/DESIGN_HISTORY.md §5 "short timed regions")
         self._dp = [self.data[b].data_ptr() for b in range(blocks)]
         self._cp = [self.crc[b].data_ptr() for b in range(blocks)]
         for b in range(blocks):  # stored CRCs written by the GPU compute path, checked below
@@ -308,7 +308,7 @@ def batched_rate(torch, work, ctx, mode, reps=100, warm=300):
     """Secondary measurement (never `value`): the same `blocks` blocks per call through the
     multi-block batch API (hdfs3_crc32c_{verify,compute}_blocks_dev*, one launch of the
     segmented wave kernel; each block keeps its own data, CRC array and (block, chunk)
-    result key). Amortises the per-launch head and dispatch gap."""
+    result key). Amortises the per-launch head and dispatch gap (docs/DESIGN_HISTORY.md §5)."""
     blocks = [(work.data_ptr(b), work.crc_ptr(b), work.block_bytes) for b in range(work.blocks)]
     nbytes = work.block_bytes * work.blocks
     res = torch.zeros(reps, dtype=torch.int64, device=work.data.device)
@@ -346,7 +346,7 @@ class StepGraphs:
     stream; the library shares torch's HIP runtime). Graph i holds `per` consecutive steps
     with exactly the eager loop's block rotation and result slots; a shorter graph covers
     K % per. Each step is still one launch verifying one whole block — the graph only
-    removes per-launch CPU submission and shrinks the dispatch gap."""
+    removes per-launch CPU submission and shrinks the dispatch gap (docs/DESIGN_HISTORY.md §5)."""
 
     def __init__(self, torch, work, ctx, mode, K, result, stream, per=64):
         self.torch = torch
@@ -698,7 +698,7 @@ def paired_regions(torch, work, ctx, stream, n, overlap, dst, reps=3):
     """Compute against verify in identical timed regions: per rep, a verify region then a compute
     region, each 50 warmup launches, settle, n timed launches (first barriered, the rest overlapped
     when `overlap`); medians of the per-launch times. Two 20-launch regions timed minutes apart on
-    a box differ by up to 12 % (the driver's form); a ratio of paired regions does not
+    a box differ by up to 12 % (docs/DESIGN_HISTORY.md §5, the driver's form); a ratio of paired regions does not
     carry that."""
     res = torch.zeros(256, dtype=torch.int64, device=work.data.device)
     rp, dp, cp, nb, bb, bpc = res.data_ptr(), work._dp, work._cp, work.blocks, work.block_bytes, work.bpc
@@ -1419,7 +1419,7 @@ def main():
     # (0) diagnostic pass, before the warmup: max(K, 2000) launches eagerly, each bracketed
     # by HIP events on the launch stream (per-launch duration including dispatch, averaged
     # over the last K). Running it first also takes the GPU out of its idle power state
-    # (~25 ms of load), so short --warmup values still time a steady GPU
+    # (docs/DESIGN_HISTORY.md §5: ~25 ms of load), so short --warmup values still time a steady GPU
     D = max(K, 2000)
     events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * D)]
     run_steps(work, ctx, args.mode, D, result, events)

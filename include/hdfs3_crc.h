@@ -95,7 +95,7 @@ int hdfs3_crc_pool_stats_get(hdfs3_crc_pool_stats *out);
  * are not affected. Returns the number destroyed. */
 int hdfs3_crc_pool_trim(void);
 
-/* NUMA-local placement, opt-in with HDFS3_NUMA=1: every thread the library runs for
+/* NUMA-local placement (docs/DESIGN_HISTORY.md §6), opt-in with HDFS3_NUMA=1: every thread the library runs for
  * a device (the multi-device workers, the block readers' receivers, the local readers' loaders)
  * binds itself to the CPUs of that device's NUMA node, intersected with the process's allowed CPUs,
  * and allocates its pinned staging there. Off by default: on a one-GPU box it slowed loopback reads
@@ -152,7 +152,7 @@ int64_t hdfs3_crc_decode_result(uint64_t result_word);
  * HDFS3_LAUNCH_OVERLAP_PREVIOUS: the kernel may start before the PREVIOUS operation on
  * the ctx stream has completed (its AQL packet is launched without the barrier bit), so
  * back-to-back verifies of resident blocks overlap one launch's tail with the next one's
- * head instead of draining the GPU between them. The caller guarantees:
+ * head instead of draining the GPU between them (docs/DESIGN_HISTORY.md §5). The caller guarantees:
  *   - the previous operation enqueued on the stream is itself a verify launch of this
  *     library (either form), and
  *   - this launch's data, CRC words and zeroed result word were ready before that
@@ -179,7 +179,7 @@ int hdfs3_crc32c_compute_dev_async_ex(hdfs3_crc_ctx *ctx, const void *d_data, si
  * computed in ONE launch of the segmented wave kernel — the batch form of the calls
  * above, for callers holding several resident blocks (a block scanner, a multi-block
  * read). Each block is checked exactly as hdfs3_crc32c_verify_dev would check it alone;
- * the launch amortises the per-launch head and dispatch gap.
+ * the launch amortises the per-launch head and dispatch gap (docs/DESIGN_HISTORY.md §5).
  * Mismatch key = (block << 32) | chunk: the sync form returns the lexicographically
  * first bad (block, chunk) or -1/-1; the async form leaves ~key (0 when clean) in the
  * caller-zeroed *d_result (hdfs3_crc_decode_result returns the key). */
@@ -261,7 +261,7 @@ int hdfs3_crc32c_compute_packets_dev_async(hdfs3_crc_ctx *ctx, void *d_arena, si
  * data_off + i*pitch, data_len bytes each except the last (last_len <= data_len).
  * ONE launch with O(1) host work and no descriptor array: when data_len is a power-of-two
  * number of 4 KiB rounds (64 KiB packets: 16) at bpc 512..4096 with 16-B aligned data, the
- * wave kernel walks the packets directly; any other stream is expanded into
+ * wave kernel walks the packets directly (docs/DESIGN_HISTORY.md §4.2); any other stream is expanded into
  * descriptors once and takes the asynchronous descriptor path. Same result key; flags as
  * hdfs3_crc32c_verify_dev_async_ex (HDFS3_LAUNCH_OVERLAP_PREVIOUS under the same contract). */
 typedef struct hdfs3_pkt_stream {

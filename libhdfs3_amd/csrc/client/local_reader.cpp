@@ -20,7 +20,7 @@
 // one copy per byte. HDFS3_LOCAL_MMAP=1 also maps verified reads: each window's page-cache pages
 // are registered with HIP (pinned in place) and DMA'd directly, then copied out of the mapping;
 // registration pins at ~23 GiB/s and serialises across threads in the runtime, so it is an
-// opt-in. HDFS3_LOCAL_MMAP=0 disables mapping altogether. Any mmap or
+// opt-in (docs/DESIGN_HISTORY.md §5.1). HDFS3_LOCAL_MMAP=0 disables mapping altogether. Any mmap or
 // registration failure falls back to the pread path for that window or reader.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
@@ -56,7 +56,7 @@ namespace {
 constexpr int kMetaHeader = 7;             // HEADER_SIZE: version 2 + type 1 + bpc 4
 constexpr int kSlots = 3;
 constexpr int32_t kDefaultBuffer = 1 << 20;  // input.localread.default.buffersize
-constexpr int kDefaultWindowBuffers = 4;  // 4 MiB windows: first delivery sooner
+constexpr int kDefaultWindowBuffers = 4;  // 4 MiB windows: first delivery sooner (docs/DESIGN_HISTORY.md §5.1)
 constexpr int32_t kMaxBuffer = 1 << 30;     // largest local buffer / window
 
 // Window events: HDFS3_LOCAL_BLOCKING_SYNC=1 makes the consumer sleep in hipEventSynchronize
@@ -83,7 +83,7 @@ int hip_err(hipError_t e, const char *what) {
 // Reader resources — a ctx (stream, table images) and kSlots pinned + device windows —
 // are pooled per process. The reference opens one LocalBlockReader per block
 // (InputStreamImpl::setupBlockReader), and creating a ctx and pinning the windows costs
-// more than reading a 128 MiB block from the page cache.
+// more than reading a 128 MiB block from the page cache (docs/DESIGN_HISTORY.md §5.1).
 struct LocalResources {
     hdfs3_crc_ctx *ctx = nullptr;
     PacketArena a[kSlots];

@@ -13,7 +13,7 @@
 // exactly as the output stream built them (their CRCs computed on the GPU), each acked by a
 // PipelineAckProto carrying one status per node (processAck, :680-722).
 //
-// Not rebuilt (outside the checksum path): pipeline recovery
+// Not rebuilt (outside the checksum path, docs/DESIGN_HISTORY.md §8): pipeline recovery
 // (buildForAppendOrRecovery / resend, :610-619, a namenode RPC round), heartbeat packets and
 // block tokens. A failure is therefore sticky: the stream fails with -EIO and the message the
 // reference would have thrown before it started recovery.

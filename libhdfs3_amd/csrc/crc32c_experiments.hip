@@ -1,9 +1,9 @@
 // Kernel variants kept for in-process A/B and diagnostics (hdfs3x_set_variant, tools/ab.py;
-// DESIGN.md §5.0), and the read-ceiling kernels of the bench. Linked into the measurement
+// docs/DESIGN_HISTORY.md §5.0), and the read-ceiling kernels of the bench. Linked into the measurement
 // library libhdfs3_crc_lab.so only (HDFS3_LAB=1); the product libhdfs3_crc.so never sees it.
 // Bit-exact variants are parity-tested (tests/test_gpu_parity.py); the diagnostic one gives
 // wrong results on purpose. The designs that lost their A/B were removed in round 3; their
-// numbers stay in DESIGN.md §5 and profiles/.
+// numbers stay in docs/DESIGN_HISTORY.md §5 and profiles/.
 #include "crc32c_wave.h"
 
 namespace hdfs3crc {

@@ -114,7 +114,7 @@ bool packet_stream_ok(uint64_t data_len, uint64_t last_len, uint64_t npk, uint32
 // Compute mode over a stream whose CRC words sit inside each packet (the wire layout: 512 B of
 // words per 64 KiB packet, 66 KiB apart) writes 8 MiB per GiB as small regions scattered over
 // the arena, interleaved with the read stream: 1 GiB took 213 us against 186 us with the words
-// written densely (tools/compute_layout_probe.py). With a WordScratch the words
+// written densely (tools/compute_layout_probe.py, docs/DESIGN_HISTORY.md §4.3). With a WordScratch the words
 // go densely into it and one copy kernel scatters them to the packets afterwards.
 struct WordScratch {
     uint8_t *d = nullptr;

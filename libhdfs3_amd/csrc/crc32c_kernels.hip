@@ -44,6 +44,10 @@ hipError_t launch_p(const ChunkLaunch &a, const uint32_t *tab, const uint32_t *f
     if (g_variant == 132) return launch_wave3<BPC, V, true, true, 0, 256>(a, tab, fold, grid_cap, s);
     if (g_variant == 134) return launch_wave3<BPC, V, true, true, 0, 512>(a, tab, fold, grid_cap, s);
     if (g_variant == 137) return launch_wave3<BPC, V, true, true, kLabWg1024>(a, tab, fold, grid_cap, s);
+    // compute: each round's words stored at once instead of held (round 6, the writer's small batches)
+    if (g_variant == 163) return launch_wave3<BPC, V, true, true, kLabNoHold>(a, tab, fold, grid_cap, s);
+    // one round per wave for launches of <= 4096 units (round 6)
+    if (g_variant == 162) return launch_wave3<BPC, V, true, true, kLabOneRound>(a, tab, fold, grid_cap, s);
 #endif
     // the solo last step for overlapped launches up to 256 MiB, as the block walk (round 4): 128 MiB of
     // 64 KiB packets at the block reader's 66,048-byte pitch 22.53 -> 20.98 us overlapped against 20.97

@@ -524,7 +524,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
     // views are resolved at the end.
     // LATE (production): the prefetch goes out once this step's rounds have landed, so at most 8 KiB
     // are in flight per wave (128 KiB per CU), not 16: more requests in flight lower the DRAM
-    // efficiency. kLabEarly (lab A/B): issued at the start of the step.
+    // efficiency (docs/DESIGN_HISTORY.md §5.0). kLabEarly (lab A/B): issued at the start of the step.
     // priority by rounds left (kPrioMinRounds); wave-uniform, so the branches are SALU
     const bool use_prio = (LAB & kLabPrio) != 0 || ((LAB & kLabNoPrio) == 0 && K >= kPrioMinRounds);
     auto prio = [&](uint32_t k) {

@@ -1,4 +1,4 @@
-// NUMA-local placement of each GPU's host-side work (numa.h).
+// NUMA-local placement of each GPU's host-side work (numa.h, docs/DESIGN_HISTORY.md §6).
 #include "numa.h"
 
 #include <hip/hip_runtime.h>

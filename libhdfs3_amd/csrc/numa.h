@@ -1,4 +1,4 @@
-// Internal: NUMA-local placement of the host side of each GPU's work. On a
+// Internal: NUMA-local placement of the host side of each GPU's work (docs/DESIGN_HISTORY.md §6). On a
 // 2-socket 8-GPU node, data that lands in host memory (a datanode socket, RemoteBlockReader.cpp:245;
 // a block file, LocalBlockReader.cpp) and goes H2D crosses the socket interconnect for the GPUs of
 // the other socket unless the thread that receives it, and the pinned buffer it lands in, sit on the

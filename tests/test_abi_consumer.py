@@ -83,7 +83,7 @@ def test_config5_1gib_file_through_hdfsRead():
     through hdfsWrite (64 KiB packets, every packet's words checked against the oracle), served
     over loopback TCP by two replicas (block 1 of the first corrupt), read back through
     hdfsRead in 4 MiB calls: every byte CheckBuffer'd, one failover, then EIO from the corrupt
-    replica alone. Prints the end-to-end rates."""
+    replica alone. Prints the end-to-end rates (docs/DESIGN_HISTORY.md §5.1)."""
     j = _hdfs_consumer("128", "8", timeout=115)
     assert j["hdfs_consumer"] == "ok" and j["blocks"] == 8 and j["bytes"] == 1 << 30
     print(j)

@@ -1,4 +1,4 @@
-"""NUMA-local placement policy (libhdfs3_amd/csrc/numa.cpp) checked on fake sysfs
+"""NUMA-local placement policy (docs/DESIGN_HISTORY.md §6, libhdfs3_amd/csrc/numa.cpp) checked on fake sysfs
 trees: a device's PCI function -> its NUMA node (bus/pci/devices/<bdf>/numa_node) -> that node's
 CPUs (devices/system/node/node<N>/cpulist). The worker, receiver and loader threads of a device bind
 to those CPUs (intersected with the process's allowed CPUs) before they pin their staging."""

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Multi-block batch API A/B: 8 x 128 MiB device-resident blocks per call
+"""Multi-block batch API A/B (docs/DESIGN_HISTORY.md §4.2): 8 x 128 MiB device-resident blocks per call
 through hdfs3_crc32c_verify_blocks_dev_async, with the wave kernel's pitch mode for blocks at constant strides (variant 0)
 and with the segmented kernel forced (variant 54), against one contiguous 1 GiB verify of the
 same bytes. HIP events on one stream, rounds interleaved; medians per case."""

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Where compute mode loses time on packet streams: 1 GiB of 64 KiB packets at
+"""Where compute mode loses time on packet streams (docs/DESIGN_HISTORY.md §4.3): 1 GiB of 64 KiB packets at
 bpc 512, CRC words written (a) into one contiguous array, (b) into each packet's own 512 B region
 of the wire layout. The data layout (contiguous vs 66,048 B pitch) and the word layout are varied
 independently through the multi-block API (constant strides -> the wave kernel's pitch mode), so

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""BASELINE.json configs the bench line does not cover, GPU side:
+"""BASELINE.json configs the bench line does not cover, GPU side (docs/DESIGN_HISTORY.md §5):
   config 0  one 64 KiB HDFS packet (128 x 512 B chunks): latency of a single verify through
             the host-buffer API (H2D + kernel + result) and the packets API; the reference CPU
             timing of the same packet is bench.py's cpu_baseline.config0_packet_us
@@ -44,7 +44,7 @@ def main():
                 ctx.verify_dev_async(data.data_ptr(), n, bpc, crc.data_ptr(), res.data_ptr() + 8 * (i % 64))
 
         launch("compute", 0)
-        # the GPU needs ~25 ms of sustained load to leave its idle power state:
+        # the GPU needs ~25 ms of sustained load to leave its idle power state (docs/DESIGN_HISTORY.md §5):
         # ramp with back-to-back launches, then time batches of BATCH back-to-back launches
         BATCH = 5
         for mode in ("compute", "verify"):

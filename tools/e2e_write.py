@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Write path, PCIe-inclusive: hdfsWrite (hdfs3_output_write) of a 1 GiB
+"""Write path, PCIe-inclusive (docs/DESIGN_HISTORY.md §5.1): hdfsWrite (hdfs3_output_write) of a 1 GiB
 host buffer in 1 MiB writes, 128 MiB blocks, 512 B chunks — user bytes copied into pinned
 packet arenas, H2D, GPU compute of every chunk's CRC, D2H of the words, packets assembled
 and handed to a C sink that reads every packet byte (a stand-in for the pipeline socket).

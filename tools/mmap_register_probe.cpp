@@ -1,4 +1,4 @@
-// Probe for the short-circuit reader: can a block file's page-cache pages be
+// Probe for the short-circuit reader (docs/DESIGN_HISTORY.md §5.1): can a block file's page-cache pages be
 // DMA'd to the GPU directly? mmap the file, hipHostRegister the mapping (pins the page-cache
 // pages), time the registration, an H2D copy from it, and the unregister; compare with pread
 // into pinned memory + H2D, and with a plain read() of the file.

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-open cost of the client drop-ins: libhdfs3 opens one input stream
+"""Per-open cost of the client drop-ins (docs/DESIGN_HISTORY.md §5.1): libhdfs3 opens one input stream
 per file (hdfsOpenFile) and one block reader per block, so small-file reads pay that cost
 every time. Times (ms, mean of N):
   ctx          hdfs3_crc_ctx_create + destroy (public API, never pooled)

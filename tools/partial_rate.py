@@ -20,12 +20,18 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 
 def main():
+    import argparse
+
     import torch
     from libhdfs3_amd import _native
     from libhdfs3_amd.engine import CrcContext
 
-    lib = _native.lib()
-    ctx = CrcContext(0)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="", help="lab variants for the writer-batch row (lab library)")
+    args = ap.parse_args()
+    variants = [int(v) for v in args.variants.split(",") if v]
+    lib = _native.lab() if variants else _native.lib()
+    ctx = CrcContext(0, lib=lib)
     stream = torch.cuda.Stream()
     ctx.set_stream(stream.cuda_stream)
     torch.cuda.set_stream(stream)
@@ -65,17 +71,35 @@ def main():
         ctx.compute_packets_dev_async(ab + b * span, span, descs, bpc)
         ctx.compute_dev(db + b * dense.shape[1] + 32768, 4 << 20, bpc, db + b * dense.shape[1])
     torch.cuda.synchronize()
-    tc = timed(lambda i: ctx.compute_packets_dev_async(ab + (i % nbat) * span, span, descs, bpc))
-    tv = timed(lambda i: ctx.verify_packets_dev_async(ab + (i % nbat) * span, span, descs, bpc, rp + 8 * (i % 512)))
-    td = timed(lambda i: ctx.verify_dev_async(db + (i % nbat) * dense.shape[1] + 32768, 4 << 20, bpc,
-                                              db + (i % nbat) * dense.shape[1], rp + 8 * (i % 512)))
-    torch.cuda.synchronize()
-    assert not bool(res.any().item()), "writer batch: clean verify reported a bad chunk"
-    alg = npk * cpp * (bpc + 4)
-    print(json.dumps({"row": "writer_batch", "bpc": bpc, "packets": npk, "chunks_per_packet": cpp,
-                      "compute_us": round(tc, 2), "verify_us": round(tv, 2), "reader_dense_verify_us": round(td, 2),
-                      "compute_GBps": round(alg / tc / 1e3, 1), "compute_vs_reader_dense": round(tc / td, 3)}),
-          flush=True)
+    for rnd in range(2 if variants else 1):
+        for v in variants or [0]:
+            if variants:
+                lib.hdfs3x_set_variant(v)
+            tc = timed(lambda i: ctx.compute_packets_dev_async(ab + (i % nbat) * span, span, descs, bpc))
+            tv = timed(lambda i: ctx.verify_packets_dev_async(ab + (i % nbat) * span, span, descs, bpc,
+                                                              rp + 8 * (i % 512)))
+            td = timed(lambda i: ctx.verify_dev_async(db + (i % nbat) * dense.shape[1] + 32768, 4 << 20, bpc,
+                                                      db + (i % nbat) * dense.shape[1], rp + 8 * (i % 512)))
+            torch.cuda.synchronize()
+            assert not bool(res.any().item()), "writer batch: clean verify reported a bad chunk"
+            alg = npk * cpp * (bpc + 4)
+            print(json.dumps({"row": "writer_batch", "variant": v, "round": rnd, "bpc": bpc, "packets": npk,
+                              "chunks_per_packet": cpp, "compute_us": round(tc, 2), "verify_us": round(tv, 2),
+                              "reader_dense_verify_us": round(td, 2), "compute_GBps": round(alg / tc / 1e3, 1),
+                              "compute_vs_reader_dense": round(tc / td, 3)}), flush=True)
+    if variants:
+        for v in variants:  # every variant's words verify under production
+            lib.hdfs3x_set_variant(v)
+            arena[:, crc_region:crc_region + 4 * cpp * npk] = 0
+            for b in range(nbat):
+                ctx.compute_packets_dev_async(ab + b * span, span, descs, bpc)
+            lib.hdfs3x_set_variant(0)
+            res.zero_()
+            for b in range(nbat):
+                ctx.verify_packets_dev_async(ab + b * span, span, descs, bpc, rp + 8 * b)
+            torch.cuda.synchronize()
+            assert not bool(res.any().item()), f"variant {v}: computed words fail to verify"
+        return
     del arena, dense
 
     # wire streams of ~1 GiB payload

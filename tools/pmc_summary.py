@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-dispatch averages of the counters collected by tools/pmc.sh for one kernel (default: the
-512 B verify wave kernel), plus the derived per-round figures DESIGN.md §5 quotes.
+512 B verify wave kernel), plus the derived per-round figures docs/DESIGN_HISTORY.md §5 quotes.
 
     python tools/pmc_summary.py <pmc_out_dir> [kernel-name-substring] [rounds_per_wave]
 """

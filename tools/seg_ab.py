@@ -59,7 +59,7 @@ def main():
 
     cases = {"contiguous": contiguous, "blocks": blk(0), "one_segment": one_segment, "ragged": ragged_v(0)}
     samples = {k: [] for k in cases}
-    for f in cases.values():  # ramp the clocks (~25 ms of load)
+    for f in cases.values():  # ramp the clocks (docs/DESIGN_HISTORY.md §5: ~25 ms of load)
         for i in range(100):
             f(i)
     torch.cuda.synchronize()
