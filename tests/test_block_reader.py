@@ -176,7 +176,7 @@ def test_datanode_drop_mid_block_is_an_io_error(dn):
         node.stop()
 
 
-@pytest.mark.parametrize("bpc", [512, 4096, 8192, 12288, 16384, 65536])
+@pytest.mark.parametrize("bpc", [512, 4096, 8192, 12288, 16384, 20480, 65536])
 def test_dense_batches_every_chunk_size(dn, bpc):
     """Round 5: batches land densely (the packets' words back to back, their data back to back from a
     4 KiB boundary) and verify as ONE contiguous block: the round kernel at 512 / 4096, the

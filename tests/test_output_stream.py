@@ -71,7 +71,9 @@ def random_ops(rng, total, flush_p=0.1):
     (8192, 65536, 4 << 20, 64),      # ... and chunks above 4 KiB: pieces + combine
     (16384, 65536, 8 << 20, 16),
     (65536, 65536, 4 << 20, 64),
-    (12288, 65536, 3 << 20, 8),      # 6 chunks = 18 rounds per packet: not a pitch stream
+    (12288, 65536, 3 << 20, 8),      # 6 chunks = 18 rounds per packet (round 6: the pitch walk's pieces)
+    (20480, 65536, 5 << 20, 8),      # 4 chunks = 20 rounds per packet (round 6)
+    (512, 65536, 8 << 20, 64),       # round 6: 127-chunk packets, a partial last round per packet
 ])
 def test_packets_identical_to_reference_model(bpc, packet_size, block_size, batch):
     rng = random.Random(bpc * 7 + batch)
@@ -225,7 +227,7 @@ def test_append_to_full_last_block_is_eio():
     assert ei.value.rc == -errno.EIO
 
 
-@pytest.mark.parametrize("bpc", [1024, 4096, 8192, 16384, 65536])
+@pytest.mark.parametrize("bpc", [512, 1024, 4096, 8192, 12288, 16384, 20480, 65536])
 def test_long_writes_whole_batches_above_512(bpc):
     """Round 5: long writes with rare flushes, so that most GPU batches are full batches of 64 KiB
     writer packets at one data pitch with their words dense (the pitch walk with its own word pitch;
