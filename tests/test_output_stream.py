@@ -236,7 +236,7 @@ def test_long_writes_whole_batches_above_512(bpc):
     rng = random.Random(bpc)
     data = splitmix_bytes(24 << 20, 77 + bpc)
     ops = random_ops(rng, data.nbytes, flush_p=0.004)
-    want, got = run_both(ops, data, bytes_per_checksum=bpc, packet_size=65536, block_size=8 << 20,
+    want, got = run_both(ops, data, bytes_per_checksum=bpc, packet_size=65536, block_size=(8 << 20) // bpc * bpc,
                          batch_packets=32)
     assert len(got) == len(want)
     for i, ((gp, gi), (wp, wi)) in enumerate(zip(got, want)):

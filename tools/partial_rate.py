@@ -78,6 +78,8 @@ def main():
             tc = timed(lambda i: ctx.compute_packets_dev_async(ab + (i % nbat) * span, span, descs, bpc))
             tv = timed(lambda i: ctx.verify_packets_dev_async(ab + (i % nbat) * span, span, descs, bpc,
                                                               rp + 8 * (i % 512)))
+            if variants:  # the reader's contiguous batch under production (the variants are pitch-walk ones)
+                lib.hdfs3x_set_variant(0)
             td = timed(lambda i: ctx.verify_dev_async(db + (i % nbat) * dense.shape[1] + 32768, 4 << 20, bpc,
                                                       db + (i % nbat) * dense.shape[1], rp + 8 * (i % 512)))
             torch.cuda.synchronize()
