@@ -327,8 +327,13 @@ struct hdfs3_block_reader {
                 // own .meta-style word array, and the GPU verifies it with the contiguous round kernel
                 // (launch()): no packet pitch, no 4 KiB rounds straddling packets. Same bytes on the
                 // wire, same delivery (PacketRef), same ChecksumException semantics.
-                if (b.pk.empty()) {  // geometry from the batch's first packet
-                    b.d0 = (uint64_t(batch_packets) * crc_len + 4095) & ~uint64_t(4095);
+                if (b.pk.empty()) {
+                    // room for batch_packets packets' words, sized for the largest packet expected (a
+                    // datanode's 64 KiB, or this one if larger): a short first packet must not
+                    // shrink the word region and close the batch after a few packets
+                    const uint64_t exp_data = std::max<uint64_t>(uint64_t(h.data_len), uint64_t(64) << 10);
+                    const uint64_t max_crc = (exp_data + chunk_size - 1) / chunk_size * checksum_size;
+                    b.d0 = (uint64_t(batch_packets) * max_crc + 4095) & ~uint64_t(4095);
                     // the arena as acquired holds the batch (64 KiB packets: 32 KiB of words + 4 MiB of
                     // data in the 64 x 66,064 B the ring is sized for); larger packets close the batch
                     // early, as in the wire layout, and only a single packet that does not fit grows it

@@ -68,8 +68,6 @@ hipError_t launch_exp(int variant, const ChunkLaunch &a, const uint32_t *tab, co
             return launch_wave3<BPC, V, false, true, kLabNoTabLoad>(a, tab, fold, grid_cap, s);
         case 137:  // verify: 1024-thread workgroups at every launch size (production before round 4)
             return launch_wave3<BPC, V, false, true, kLabWg1024>(a, tab, fold, grid_cap, s);
-        case 166:  // compute: staged words written round by round by the round's last wave (kLabEager, round 6)
-            return launch_wave3<BPC, V, false, true, kLabEager>(a, tab, fold, grid_cap, s);
         case 162:  // launches of <= 4096 units (16 MiB): one round per wave, twice the workgroups (round 6)
             return launch_wave3<BPC, V, false, true, kLabOneRound>(a, tab, fold, grid_cap, s);
         case 132:  // 256-thread workgroups (4 waves each): small launches spread over 4x the CUs

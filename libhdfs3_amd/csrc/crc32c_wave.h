@@ -46,8 +46,6 @@ constexpr int kLabWg1024 = 16384;    // verify: 1024-thread workgroups at every 
 constexpr int kLabNoTabLoad = 2097152;  // diagnostic: the table images are not loaded (made up from t: wrong results)
 constexpr int kLabFull16 = 8388608;  // the round-4 chains: 16 table steps per chain, the fold on the finished state
 constexpr int kLabOneRound = 4194304;  // launches of <= 4096 units: one round per wave (twice the workgroups)
-constexpr int kLabEager = 16777216;  // compute, staged words: the last wave to finish round k writes the workgroup's
-                                     // round-k words at once (no end-of-workgroup flush)
 constexpr int kLabMid = 1048576;     // with kLabClock: word 2 of a wave's stamp = fill done | first data << 21 | kernel
                                      // arguments landed << 42, each - start, 21 bits of 10 ns
 // Not a lab bit: launch_wave3 sets it for compute over a contiguous block at bpc 1024 / 2048, and at
@@ -280,10 +278,6 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             *reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + (byte_t ^ uint32_t(16 * r))) = u32x4{w, w, w, w};
         if constexpr (kHalfFold) {
             reinterpret_cast<u32x4 *>(lds + kHalfFoldOff / 4)[tt] = n0[f];
-            // kLabEager: the per-round arrival counters, the staging region's last 32 words
-            if constexpr ((LAB & kLabEager) != 0 && !VERIFY) {
-                if (tt < 32) lds[kLdsBytesWave / 4 - 32 + tt] = 0u;
-            }
         } else {
             u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(lds) + kFoldLdsOff) + 2 * tt;
             dst[0] = n0[f];
@@ -410,31 +404,6 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             }
         }
     };
-    // kLabEager (round 6 lab): no end-of-workgroup flush. After staging its round-k words each wave counts
-    // itself in for round k (an LDS atomic; the LDS executes a wave's ds operations in order, so the words
-    // precede the count); the wave that completes the count - all of the workgroup's waves that have a
-    // round k - writes the workgroup's round-k words, 16 consecutive units' worth, at once. The words thus
-    // leave while later rounds' data is in flight, not in the launch's tail. Launches of <= 24 rounds per
-    // wave (the counters sit in the staging region's last 32 words).
-    constexpr bool kEager = kStage && (LAB & kLabEager) != 0;
-    uint32_t *const cnt = lds + kLdsBytesWave / 4 - 32;
-    auto eager_round = [&](uint32_t k) {
-        if constexpr (kEager) {
-            asm volatile("" ::: "memory");
-            uint32_t old = 0;
-            if (lane == 0) old = __hip_atomic_fetch_add(cnt + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            old = __builtin_amdgcn_readfirstlane(old);
-            asm volatile("" ::: "memory");
-            const uint64_t wg_first = walk.first - slot;  // the global wave (unit) of slot 0
-            const uint32_t extra = walk.kr > wg_first ? uint32_t(walk.kr - wg_first < 16 ? walk.kr - wg_first : 16) : 0u;
-            const uint32_t expected = k < walk.kq ? 16u : extra;
-            if (old + 1 == expected) {
-                const uint32_t nw = expected * kCpw;
-                gu8 *dst = (gu8 *)walk.words + 4 * kCpw * (wg_first + uint64_t(k) * walk.stride);
-                for (uint32_t t = lane; t < nw; t += 64) stage_store(dst + 4 * t, stage[k * 16 * kCpw + t]);
-            }
-        }
-    };
     // compute at bpc 4096 (one word per round) over one contiguous block: lane k % 64 keeps round k's
     // word, and one store per 64 rounds writes them, instead of a 4-byte store per round into the read
     // stream: 128 MiB 23.63 -> 22.54 us overlapped, 25.24 -> 24.51 barriered, 1 GiB 160.6 -> 158.8
@@ -455,9 +424,6 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
         }
         if constexpr (kStage) {
             if (k < K && j == 0) stage[((k % kSR) * 16 + slot) * kCpw + lane / G] = y;
-            if constexpr (kEager) {
-                if (k < K) eager_round(k);
-            }
             return;
         }
         if constexpr (kHold) {
@@ -645,7 +611,7 @@ __device__ __forceinline__ void wave_rounds(Walk &walk, uint32_t *lds, const uin
             step(b0, b1, a0, a1, k + 2);
         }
     }
-    if constexpr (kStage && !kEager) {
+    if constexpr (kStage) {
         lds_barrier();  // every wave of the workgroup runs wave_rounds to its end
         const uint64_t wg_first = walk.first - slot;
         const uint32_t wb = walk.kq ? kSR * (kq_flush / kSR) : 0u;  // the last window's first round
@@ -850,13 +816,8 @@ hipError_t launch_wave3(const ChunkLaunch &a, const uint32_t *tab, const uint32_
     if constexpr (!V && BPC <= 2048 && !PITCH && TPB == 1024 &&
                   (LAB & (kStageWords | kLabNoStage | kLabNoHold)) == 0) {
         const bool words_fit = units * uint64_t(4 * (kRoundBytes / BPC)) < (uint64_t(1) << 31);  // stage_store
-        if constexpr ((LAB & kLabEager) != 0) {
-            if (words_fit && b.kq + (b.kr ? 1u : 0u) <= 24)
-                return launch_wave3<BPC, V, PITCH, SOLO, LAB | kStageWords, TPB>(a, tab, fold, grid_cap, s);
-        }
         if (words_fit && (b.kq + (b.kr ? 1u : 0u) <= kStageMaxRounds(BPC) || BPC != 512 || (LAB & kLabStageWin) != 0))
-            return launch_wave3<BPC, V, PITCH, SOLO, (LAB & ~kLabEager) | kStageWords, TPB>(a, tab, fold, grid_cap,
-                                                                                           s);
+            return launch_wave3<BPC, V, PITCH, SOLO, LAB | kStageWords, TPB>(a, tab, fold, grid_cap, s);
     }
     if (a.overlap_previous) {  // AQL packet without the barrier bit (HDFS3_LAUNCH_OVERLAP_PREVIOUS)
         if constexpr (SOLO) {
