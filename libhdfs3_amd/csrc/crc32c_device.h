@@ -653,6 +653,10 @@ struct SegLaunch {
     // constant pitch in one arena need no descriptor array at all.
     uint64_t stride;
     uint32_t kq, kr;  // a wave's round count: kq + (wave < kr), split on the host (launch_segments)
+    // non-null (bpc = R x 4096 descriptor lists, round 6): unit u's words go to dense_words + 4 * CPU * u
+    // instead of the segment's own array (the 4096-byte piece CRCs a combine folds), and the segments'
+    // short tails are left to the caller
+    uint8_t *dense_words;
     DevSegment inl[kInlineSegments];
 };
 

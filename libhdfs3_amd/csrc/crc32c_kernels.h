@@ -99,7 +99,8 @@ bool segments_fast(const DevSegment *h_seg, size_t n, uint32_t bpc);
 hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,
                            uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
                            const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream,
-                           const DevSegment *h_inline = nullptr, uint64_t stride = 0);
+                           const DevSegment *h_inline = nullptr, uint64_t stride = 0,
+                           uint8_t *dense_words = nullptr);
 constexpr uint32_t kMaxInlineSegments = 16;
 
 // Packet batch (packets API, block reader, output stream): descriptors in host memory;

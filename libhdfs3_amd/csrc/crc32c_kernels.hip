@@ -497,9 +497,10 @@ hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, co
 hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,
                            uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
                            const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream,
-                           const DevSegment *h_inline, uint64_t stride) {
+                           const DevSegment *h_inline, uint64_t stride, uint8_t *dense_words) {
     if (nseg == 0) return hipSuccess;
     SegLaunch L{};
+    L.dense_words = dense_words;
     L.seg = d_seg;
     L.nseg = nseg;
     L.units = units;
@@ -525,6 +526,120 @@ hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t unit
     default: return hipErrorInvalidValue;
     }
 }
+
+namespace {
+
+// Descriptor lists at bpc = R x 4096 that are not one constant-pitch stream (round 6): the segmented
+// kernel computes every 4096-byte piece of every segment densely (segment i's pieces from piece
+// unit_begin_i, SegLaunch::dense_words), then this combine folds each chunk from its R pieces
+// (crc32c_combine_pieces_kernel's fold) and compares with / writes the segment's own word c, key
+// key_base + c. One wave per segment at a time (grid-stride), its lanes over the segment's chunks: a
+// datanode packet holds few chunks at these sizes (5 of 12 KiB, 1 of 64 KiB).
+template <bool VERIFY>
+__global__ __launch_bounds__(256) void crc32c_combine_segment_pieces_kernel(const DevSegment *__restrict__ seg,
+                                                                            uint32_t n,
+                                                                            const uint8_t *__restrict__ piece_be,
+                                                                            uint32_t bpc,
+                                                                            const uint32_t *__restrict__ g_fold,
+                                                                            unsigned long long *result) {
+    uint32_t col[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) col[i] = g_fold[kFoldAdvance4096 + i];
+    const uint32_t K = gf2_apply4(col, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+    const uint32_t R = bpc / kRoundBytes;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nwaves = uint64_t(gridDim.x) * 4;
+    for (uint64_t si = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); si < n; si += nwaves) {
+        const DevSegment sd = seg[si];
+        const uint64_t nfull = sd.len / bpc;
+        for (uint64_t c = lane; c < nfull; c += 64) {
+            const uint32_t *y = reinterpret_cast<const uint32_t *>(piece_be) + sd.unit_begin + c * R;
+            uint32_t st = 0xFFFFFFFFu;
+            for (uint32_t i = 0; i < R; ++i) st = gf2_apply4(col, st) ^ __builtin_bswap32(y[i]) ^ K;
+            const uint32_t v = ~st;
+            if constexpr (VERIFY) {
+                if (__builtin_bswap32(*reinterpret_cast<const uint32_t *>(sd.crc + 4 * c)) != v)
+                    atomicMax(result, ~(unsigned long long)(sd.key_base + c));
+            } else {
+                *reinterpret_cast<uint32_t *>(sd.crc + 4 * c) = __builtin_bswap32(v);
+            }
+        }
+    }
+}
+
+// the segments' short last chunks (len % bpc bytes), one thread each
+template <bool VERIFY>
+__global__ __launch_bounds__(kBlockThreads) void crc32c_segment_tails_kernel(const DevSegment *__restrict__ seg,
+                                                                             uint32_t n, uint32_t bpc,
+                                                                             int check_short_tail,
+                                                                             unsigned long long *result,
+                                                                             const uint32_t *__restrict__ g_tab) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+    fill_tables(lds, g_tab);
+    lds_barrier();
+    const Lut t(lds);
+    for (uint64_t i = uint64_t(blockIdx.x) * kBlockThreads + threadIdx.x; i < n;
+         i += uint64_t(gridDim.x) * kBlockThreads) {
+        const DevSegment sd = seg[i];
+        const uint32_t tail = uint32_t(sd.len % bpc);
+        if (!tail) continue;
+        const uint64_t c = sd.len / bpc;
+        const uint32_t v = ~crc_run_any(t, 0xFFFFFFFFu, sd.data + c * bpc, tail);
+        const bool al = (reinterpret_cast<uintptr_t>(sd.crc) & 3u) == 0;
+        if constexpr (VERIFY) {
+            if (check_short_tail && load_be32(sd.crc + 4 * c, al) != v)
+                atomicMax(result, ~(unsigned long long)(sd.key_base + c));
+        } else {
+            store_be32(sd.crc + 4 * c, v, al);
+        }
+    }
+}
+
+// h_stage[0..n) planned at 4096-byte units (unit_begin = the segment's first piece); the descriptors go
+// to d_stage (always: the combine and the tails read them), *staged is set
+hipError_t launch_segment_pieces(DevSegment *h_stage, DevSegment *d_stage, size_t n, uint64_t pieces_total,
+                                 uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
+                                 const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
+                                 hipStream_t stream, PieceScratch *ps, uint64_t max_chunks, bool any_tail,
+                                 bool *staged) {
+    unsigned b = 0;
+    if (hipError_t e = piece_buffer(ps, (pieces_total ? pieces_total : 1) * 4, stream, &b); e != hipSuccess)
+        return e;
+    hipError_t e = hipMemcpyAsync(d_stage, h_stage, n * sizeof(DevSegment), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    if (staged) *staged = true;
+    if (pieces_total) {
+        e = launch_segments(d_stage, uint32_t(n), pieces_total, 0, kRoundBytes, false, 1, nullptr, d_tables, d_fold,
+                            grid_cap, stream, nullptr, 0, ps->d[b]);
+        if (e != hipSuccess) return e;
+    }
+    if (max_chunks) {
+        const uint64_t want = (n + 3) / 4;  // 4 waves per workgroup, a segment per wave
+        const int grid = int(want < 2048 ? want : 2048);
+        if (verify)
+            hipLaunchKernelGGL(crc32c_combine_segment_pieces_kernel<true>, dim3(grid), dim3(256), 0, stream, d_stage,
+                               uint32_t(n), ps->d[b], bpc, d_fold, result);
+        else
+            hipLaunchKernelGGL(crc32c_combine_segment_pieces_kernel<false>, dim3(grid), dim3(256), 0, stream,
+                               d_stage, uint32_t(n), ps->d[b], bpc, d_fold, result);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    e = hipEventRecord(ps->used[b], stream);
+    if (e != hipSuccess) return e;
+    if (!any_tail) return hipSuccess;
+    const uint64_t blocks = (n + kBlockThreads - 1) / kBlockThreads;
+    const int grid = int(blocks < uint64_t(grid_cap) ? blocks : uint64_t(grid_cap));
+    if (verify)
+        hipLaunchKernelGGL(crc32c_segment_tails_kernel<true>, dim3(grid), dim3(kBlockThreads), 0, stream, d_stage,
+                           uint32_t(n), bpc, check_short_tail, result, d_tables);
+    else
+        hipLaunchKernelGGL(crc32c_segment_tails_kernel<false>, dim3(grid), dim3(kBlockThreads), 0, stream, d_stage,
+                           uint32_t(n), bpc, 0, result, d_tables);
+    return hipGetLastError();
+}
+
+}  // namespace
 
 hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, size_t n, uint32_t bpc, bool verify,
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
@@ -611,6 +726,21 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         h_stage[i] = DevSegment{d_arena + h_pk[i].data_off, const_cast<uint8_t *>(d_arena) + h_pk[i].crc_off,
                                 h_pk[i].data_len, units, uint64_t(i) << 32};
         units += seg_units(h_pk[i].data_len, ubpc);
+    }
+    // bpc = R x 4096, aligned, not one constant-pitch stream: piece CRCs over the segment list + the combine
+    // (round 6; the chunk-per-lane packet kernel before, ~1 TiB/s)
+    if (!fast && aligned && pieces && bpc > kRoundBytes && bpc % kRoundBytes == 0 && n < (size_t(1) << 31)) {
+        uint64_t pieces_total = 0, max_chunks = 0;
+        bool any_tail = false;
+        for (size_t i = 0; i < n; ++i) {
+            h_stage[i].unit_begin = pieces_total;
+            pieces_total += h_stage[i].len / kRoundBytes;
+            const uint64_t nf = h_stage[i].len / bpc;
+            max_chunks = nf > max_chunks ? nf : max_chunks;
+            any_tail = any_tail || (h_stage[i].len % bpc) != 0;
+        }
+        return launch_segment_pieces(h_stage, d_stage, n, pieces_total, bpc, verify, check_short_tail, result,
+                                     d_tables, d_fold, grid_cap, stream, pieces, max_chunks, any_tail, staged);
     }
     if (fast) {
         const uint64_t uniform = same && u0 > 0 ? u0 : 0;

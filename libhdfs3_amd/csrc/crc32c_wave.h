@@ -199,7 +199,7 @@ struct SegWalk {
                 c_wlen = wlen(lastp ? L->inl[1].len : L->inl[0].len);
                 c_end = c_begin + (lastp ? units(L->inl[1].len) : L->uniform);
                 c_data = L->inl[0].data + uint64_t(si) * L->stride;
-                c_crc = L->inl[0].crc + uint64_t(si) * L->stride;
+                c_crc = L->dense_words ? L->dense_words + 4 * CPU * c_begin : L->inl[0].crc + uint64_t(si) * L->stride;
                 c_key = uint64_t(si) << 32;
             } else {
                 CDevSegment *sd = segp(si);
@@ -207,7 +207,8 @@ struct SegWalk {
                 c_wlen = wlen(rfl64(sd->len));
                 c_end = c_begin + (c_wlen + kRoundBytes - 1) / kRoundBytes;
                 c_data = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->data)));
-                c_crc = reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->crc)));
+                c_crc = L->dense_words ? L->dense_words + 4 * CPU * c_begin
+                                       : reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sd->crc)));
                 c_key = rfl64(sd->key_base);
             }
             c_si = si;
@@ -739,7 +740,8 @@ __global__ __launch_bounds__(TPB) void crc32c_segments_kernel(SegLaunch L, const
     wave_rounds<BPC, VERIFY, false, !VERIFY && BPC == 512, LAB, TPB>(w, lds, g_tab, g_nib, L.result);
 
     // every whole chunk was in a (possibly partial) round: only the segments' short last chunks
-    // are left, one lane each, item i on workgroup i % grid
+    // are left, one lane each, item i on workgroup i % grid (piece CRCs for a combine: the caller's)
+    if (L.dense_words) return;
     const Lut t(lds);
     for (uint64_t si = uint64_t(threadIdx.x) * gridDim.x + blockIdx.x; si < L.nseg;
          si += uint64_t(gridDim.x) * TPB) {

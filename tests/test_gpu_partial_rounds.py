@@ -240,3 +240,29 @@ def test_segments_variant_1024_threads_same_keys(lab_ctx):
             check_batch(lab_ctx, arena, pk, bpc, [(4, 61440 + 3583), (10, 4096 * 2 + 512 * 4)])
     finally:
         lib.hdfs3x_set_variant(0)
+
+
+@pytest.mark.parametrize("bpc", [8192, 12288, 20480, 65536])
+def test_ragged_descriptor_list_chunks_above_4k(gpu_ctx, bpc):
+    """Round 6: a descriptor list at bpc = R x 4096 that is not one constant-pitch stream (ragged lengths,
+    gaps between packets) takes the segmented kernel's 4096-byte piece CRCs and a per-segment combine,
+    the short last chunks one lane each (before: the chunk-per-lane packet kernel). Keys and every
+    computed word against the oracle, remote and local tail semantics, flips in whole chunks and in
+    short tails; packets shorter than one chunk, and of exactly one chunk."""
+    rng = np.random.default_rng(bpc + 1)
+    sizes = [3 * bpc, bpc + 777, 61440 // bpc * bpc or bpc, 500, bpc, 2 * bpc + 4096, 7 * bpc - 1]
+    sizes += [int(x) for x in rng.integers(1, 6 * bpc, size=12)]
+    arena = np.zeros(sum(s + 4 * (-(-s // bpc)) + 96 for s in sizes) + 64, np.uint8)
+    pk, off = [], 16
+    for i, s in enumerate(sizes):
+        d = splitmix_bytes(s, 9000 + i + bpc)
+        w = oracle_compute(d, bpc)
+        arena[off:off + w.nbytes] = w
+        doff = off + w.nbytes
+        doff += (-doff) % 16
+        arena[doff:doff + s] = d
+        pk.append((doff, off, s))
+        off = doff + s + 16 * int(rng.integers(1, 4))
+    flips = [(0, 2 * bpc + 5), (1, bpc + 700), (3, 499), (5, 2 * bpc + 4000), (6, 7 * bpc - 2),
+             (len(sizes) - 1, sizes[-1] - 1)]
+    check_batch(gpu_ctx, arena, pk, bpc, flips)

@@ -5,6 +5,8 @@
     slots at a 65,568-byte stride, words compact after them), compute and verify through the
     packets API (descriptors, as output_stream.cpp launches it), barriered, against the reader's
     dense 4 MiB batch verify (one contiguous block);
+  * ragged_<bpc>: ~1 GiB descriptor lists of 2-5-chunk packets at irregular offsets (not one
+    constant-pitch stream) at bpc 12 KiB / 64 KiB: segment piece CRCs + per-segment combine;
   * stream_<bpc>: 1 GiB-class wire streams ([words][data] per packet) whose packets do not hold a
     power-of-two number of whole rounds: 127-chunk packets at bpc 512, and 60 KiB packets of 12 KiB /
     20 KiB chunks (5 / 3 chunks, 15 rounds: the pitch walk's pieces + combine), verify and compute
@@ -101,8 +103,44 @@ def main():
                 ctx.verify_packets_dev_async(ab + b * span, span, descs, bpc, rp + 8 * b)
             torch.cuda.synchronize()
             assert not bool(res.any().item()), f"variant {v}: computed words fail to verify"
-        return
     del arena, dense
+
+    # ragged descriptor lists (not one constant-pitch stream) at bpc = R x 4096, ~1 GiB: the segmented
+    # kernel's piece CRCs + the per-segment combine (round 6); with --variants 0,17 beside the
+    # chunk-per-lane packet kernel it replaced (lab 17)
+    import numpy as np
+    for bpc in (12288, 65536):
+        rng = np.random.default_rng(bpc)
+        descs_l, off = [], 16
+        while off < (1 << 30):
+            s = int(rng.integers(2, 6)) * bpc
+            wb = 4 * (s // bpc)
+            doff = off + wb
+            doff += (-doff) % 16
+            descs_l.append((doff, off, s))
+            off = doff + s + 16 * int(rng.integers(0, 3))
+        arena = torch.randint(0, 256, (off + 64,), dtype=torch.uint8, device="cuda")
+        d = CrcContext._descs(descs_l)
+        ap_ = arena.data_ptr()
+        payload = sum(x[2] for x in descs_l)
+        ctx.compute_packets_dev_async(ap_, arena.numel(), d, bpc)
+        torch.cuda.synchronize()
+        for v in (variants or [0]):
+            if variants:
+                lib.hdfs3x_set_variant(v)
+            res.zero_()
+            tv = timed(lambda i: ctx.verify_packets_dev_async(ap_, arena.numel(), d, bpc, rp + 8 * (i % 512)),
+                       n=10, warm=3, reps=3)
+            tc = timed(lambda i: ctx.compute_packets_dev_async(ap_, arena.numel(), d, bpc), n=10, warm=3, reps=3)
+            torch.cuda.synchronize()
+            assert not bool(res.any().item()), f"ragged bpc {bpc} variant {v}: clean verify reported a bad chunk"
+            print(json.dumps({"row": f"ragged_{bpc}", "variant": v, "bpc": bpc, "packets": len(descs_l),
+                              "payload_bytes": payload, "verify_us": round(tv, 1), "compute_us": round(tc, 1),
+                              "verify_TiBps": round(payload / tv / 1e-6 / 2**40, 3),
+                              "compute_TiBps": round(payload / tc / 1e-6 / 2**40, 3)}), flush=True)
+        if variants:
+            lib.hdfs3x_set_variant(0)
+        del arena
 
     # wire streams of ~1 GiB payload
     for bpc, cpp in ((512, 127), (12288, 5), (20480, 3)):
