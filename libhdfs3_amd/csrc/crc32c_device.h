@@ -657,6 +657,9 @@ struct SegLaunch {
     // instead of the segment's own array (the 4096-byte piece CRCs a combine folds), and the segments'
     // short tails are left to the caller
     uint8_t *dense_words;
+    // non-null (long descriptor lists, round 6): unit u lies in segment unit_seg[u] (one scalar load
+    // instead of a binary search per round; crc32c_unit_map_kernel builds it)
+    const uint32_t *unit_seg;
     DevSegment inl[kInlineSegments];
 };
 

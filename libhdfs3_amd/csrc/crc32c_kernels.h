@@ -100,7 +100,7 @@ hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t unit
                            uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
                            const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream,
                            const DevSegment *h_inline = nullptr, uint64_t stride = 0,
-                           uint8_t *dense_words = nullptr);
+                           uint8_t *dense_words = nullptr, const uint32_t *unit_seg = nullptr);
 constexpr uint32_t kMaxInlineSegments = 16;
 
 // Packet batch (packets API, block reader, output stream): descriptors in host memory;

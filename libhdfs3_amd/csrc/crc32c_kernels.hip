@@ -497,10 +497,12 @@ hipError_t launch_seg_t(const SegLaunch &L, bool verify, const uint32_t *tab, co
 hipError_t launch_segments(const DevSegment *d_seg, uint32_t nseg, uint64_t units, uint64_t uniform,
                            uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
                            const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap, hipStream_t stream,
-                           const DevSegment *h_inline, uint64_t stride, uint8_t *dense_words) {
+                           const DevSegment *h_inline, uint64_t stride, uint8_t *dense_words,
+                           const uint32_t *unit_seg) {
     if (nseg == 0) return hipSuccess;
     SegLaunch L{};
     L.dense_words = dense_words;
+    L.unit_seg = unit_seg;
     L.seg = d_seg;
     L.nseg = nseg;
     L.units = units;
@@ -567,6 +569,28 @@ __global__ __launch_bounds__(256) void crc32c_combine_segment_pieces_kernel(cons
     }
 }
 
+// unit -> segment map of a long descriptor list (SegLaunch::unit_seg): one wave per segment at a time,
+// its lanes over the segment's units (seg_units at ubpc: its whole chunks in 4 KiB units). A segmented
+// kernel's wave steps nwaves units per round, past dozens of short segments, so without the map every
+// round began with a binary search, a chain of ~15 dependent scalar loads (25k segments): 1 GiB of
+// 12 KiB-chunk packets 327.3 -> 253.2 us verify, the pieces kernel 252 -> 166 us (profiles/r06/r6x_*,
+// r6za_*). A 16-ary search (15 scalar loads per level) measured slower (430 us): the compiler issued
+// them two at a time
+__global__ __launch_bounds__(256) void crc32c_unit_map_kernel(const DevSegment *__restrict__ seg, uint32_t n,
+                                                              uint32_t ubpc, uint32_t *__restrict__ map) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nwaves = uint64_t(gridDim.x) * 4;
+    for (uint64_t si = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); si < n; si += nwaves) {
+        const uint64_t ub = seg[si].unit_begin, len = seg[si].len;
+        const uint64_t nu = (len / ubpc * ubpc + kRoundBytes - 1) / kRoundBytes;
+        for (uint64_t t = lane; t < nu; t += 64) map[ub + t] = uint32_t(si);
+    }
+}
+
+// Lists longer than this take the unit map (below it the search is a few loads and the map's launch
+// is not worth it)
+constexpr size_t kUnitMapMinSegments = 256;
+
 // the segments' short last chunks (len % bpc bytes), one thread each
 template <bool VERIFY>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_segment_tails_kernel(const DevSegment *__restrict__ seg,
@@ -603,14 +627,25 @@ hipError_t launch_segment_pieces(DevSegment *h_stage, DevSegment *d_stage, size_
                                  hipStream_t stream, PieceScratch *ps, uint64_t max_chunks, bool any_tail,
                                  bool *staged) {
     unsigned b = 0;
-    if (hipError_t e = piece_buffer(ps, (pieces_total ? pieces_total : 1) * 4, stream, &b); e != hipSuccess)
+    // the piece words, then (long lists) the unit -> segment map
+    const bool map = n > kUnitMapMinSegments && pieces_total;
+    if (hipError_t e = piece_buffer(ps, (pieces_total ? pieces_total : 1) * (map ? 8 : 4), stream, &b);
+        e != hipSuccess)
         return e;
     hipError_t e = hipMemcpyAsync(d_stage, h_stage, n * sizeof(DevSegment), hipMemcpyHostToDevice, stream);
     if (e != hipSuccess) return e;
     if (staged) *staged = true;
+    uint32_t *unit_seg = nullptr;
+    if (map) {
+        unit_seg = reinterpret_cast<uint32_t *>(ps->d[b] + pieces_total * 4);
+        const uint64_t want = (n + 3) / 4;
+        hipLaunchKernelGGL(crc32c_unit_map_kernel, dim3(int(want < 2048 ? want : 2048)), dim3(256), 0, stream,
+                           d_stage, uint32_t(n), uint32_t(kRoundBytes), unit_seg);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (pieces_total) {
         e = launch_segments(d_stage, uint32_t(n), pieces_total, 0, kRoundBytes, false, 1, nullptr, d_tables, d_fold,
-                            grid_cap, stream, nullptr, 0, ps->d[b]);
+                            grid_cap, stream, nullptr, 0, ps->d[b], unit_seg);
         if (e != hipSuccess) return e;
     }
     if (max_chunks) {
@@ -752,6 +787,23 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
         if (n <= kInlineSegments)  // no descriptor copy in front of the kernel
             return launch_segments(nullptr, uint32_t(n), units, uniform, bpc, verify, check_short_tail, result,
                                    d_tables, d_fold, grid_cap, stream, h_stage);
+        if (!uniform && n > kUnitMapMinSegments && pieces && units) {
+            // a long ragged list: the unit -> segment map in the piece scratch (4 B per 4 KiB unit)
+            // instead of a binary search per round; 1 GiB of 32-64 KiB packets at bpc 512: 313.6 ->
+            // 219.7 us verify (profiles/r06/r6za_partial_rate.jsonl, r6zb_partial_rate.jsonl)
+            unsigned b = 0;
+            if (hipError_t e = piece_buffer(pieces, units * 4, stream, &b); e != hipSuccess) return e;
+            uint32_t *unit_seg = reinterpret_cast<uint32_t *>(pieces->d[b]);
+            const uint64_t want = (n + 3) / 4;
+            hipLaunchKernelGGL(crc32c_unit_map_kernel, dim3(int(want < 2048 ? want : 2048)), dim3(256), 0, stream,
+                               d_stage, uint32_t(n), ubpc, unit_seg);
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess)
+                e = launch_segments(d_stage, uint32_t(n), units, 0, bpc, verify, check_short_tail, result, d_tables,
+                                    d_fold, grid_cap, stream, nullptr, 0, nullptr, unit_seg);
+            if (e == hipSuccess) e = hipEventRecord(pieces->used[b], stream);
+            return e;
+        }
         return launch_segments(d_stage, uint32_t(n), units, uniform, bpc, verify, check_short_tail, result,
                                d_tables, d_fold, grid_cap, stream);
     }

@@ -188,10 +188,14 @@ struct SegWalk {
                 // lands in the next one: try that first (one descriptor load, which the view needs
                 // anyway) before the binary search (a chain of dependent loads)
                 const uint32_t nx = c_si + 1;
-                si = nx < L->nseg && u >= rfl64(segp(nx)->unit_begin) &&
-                             u < rfl64(segp(nx)->unit_begin) + units(rfl64(segp(nx)->len))
-                         ? nx
-                         : seg_of(u);
+                if (nx < L->nseg && u >= rfl64(segp(nx)->unit_begin) &&
+                    u < rfl64(segp(nx)->unit_begin) + units(rfl64(segp(nx)->len)))
+                    si = nx;
+                else if (L->unit_seg)
+                    si = __builtin_amdgcn_readfirstlane(
+                        ((__attribute__((address_space(4))) const uint32_t *)(L->unit_seg))[u]);
+                else
+                    si = seg_of(u);
             }
             if (L->stride) {  // packets at one pitch: kernel-argument arithmetic, no descriptor loads
                 const bool lastp = si + 1 >= L->nseg;

@@ -266,3 +266,29 @@ def test_ragged_descriptor_list_chunks_above_4k(gpu_ctx, bpc):
     flips = [(0, 2 * bpc + 5), (1, bpc + 700), (3, 499), (5, 2 * bpc + 4000), (6, 7 * bpc - 2),
              (len(sizes) - 1, sizes[-1] - 1)]
     check_batch(gpu_ctx, arena, pk, bpc, flips)
+
+
+@pytest.mark.parametrize("bpc", [512, 4096, 12288])
+def test_long_ragged_descriptor_list_unit_map(gpu_ctx, bpc):
+    """Round 6: descriptor lists of more than 256 packets that are not one constant-pitch stream take a
+    unit -> segment map built on the device (one scalar load per round in place of a binary search):
+    700 packets of ragged lengths (under one chunk, whole chunks, short tails, several rounds), every
+    word and the first bad (packet, chunk) against the oracle, flips early, in the middle and last."""
+    rng = np.random.default_rng(bpc + 7)
+    sizes = [int(x) for x in rng.integers(1, 12 * max(bpc, 4096) // 4, size=700)]
+    sizes[5] = bpc - 1
+    sizes[6] = bpc
+    sizes[400] = 8 * 4096
+    arena = np.zeros(sum(s + 4 * (-(-s // bpc)) + 64 for s in sizes) + 64, np.uint8)
+    pk, off = [], 16
+    for i, s in enumerate(sizes):
+        d = splitmix_bytes(s, 13000 + i + bpc)
+        w = oracle_compute(d, bpc)
+        arena[off:off + w.nbytes] = w
+        doff = off + w.nbytes
+        doff += (-doff) % 16
+        arena[doff:doff + s] = d
+        pk.append((doff, off, s))
+        off = doff + s + 16 * int(rng.integers(0, 3))
+    flips = [(2, sizes[2] // 2), (400, 5 * 4096 + 3), (699, sizes[699] - 1)]
+    check_batch(gpu_ctx, arena, pk, bpc, flips)

@@ -5,8 +5,9 @@
     slots at a 65,568-byte stride, words compact after them), compute and verify through the
     packets API (descriptors, as output_stream.cpp launches it), barriered, against the reader's
     dense 4 MiB batch verify (one contiguous block);
-  * ragged_<bpc>: ~1 GiB descriptor lists of 2-5-chunk packets at irregular offsets (not one
-    constant-pitch stream) at bpc 12 KiB / 64 KiB: segment piece CRCs + per-segment combine;
+  * ragged_<bpc>: ~1 GiB descriptor lists of packets at irregular offsets (not one constant-pitch
+    stream): 64-127 chunks at bpc 512 (the segmented kernel), 2-5 chunks at bpc 12 KiB / 64 KiB
+    (segment piece CRCs + per-segment combine);
   * stream_<bpc>: 1 GiB-class wire streams ([words][data] per packet) whose packets do not hold a
     power-of-two number of whole rounds: 127-chunk packets at bpc 512, and 60 KiB packets of 12 KiB /
     20 KiB chunks (5 / 3 chunks, 15 rounds: the pitch walk's pieces + combine), verify and compute
@@ -109,11 +110,11 @@ def main():
     # kernel's piece CRCs + the per-segment combine (round 6); with --variants 0,17 beside the
     # chunk-per-lane packet kernel it replaced (lab 17)
     import numpy as np
-    for bpc in (12288, 65536):
+    for bpc in (512, 12288, 65536):
         rng = np.random.default_rng(bpc)
         descs_l, off = [], 16
         while off < (1 << 30):
-            s = int(rng.integers(2, 6)) * bpc
+            s = int(rng.integers(2, 6)) * bpc if bpc > 4096 else int(rng.integers(64, 128)) * bpc
             wb = 4 * (s // bpc)
             doff = off + wb
             doff += (-doff) % 16
