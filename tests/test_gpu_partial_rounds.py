@@ -292,3 +292,32 @@ def test_long_ragged_descriptor_list_unit_map(gpu_ctx, bpc):
         off = doff + s + 16 * int(rng.integers(0, 3))
     flips = [(2, sizes[2] // 2), (400, 5 * 4096 + 3), (699, sizes[699] - 1)]
     check_batch(gpu_ctx, arena, pk, bpc, flips)
+
+
+@pytest.mark.parametrize("bpc", [512, 4096, 8192])
+@pytest.mark.parametrize("shape", ["tails_only", "one_long_among_tails", "long_last"])
+def test_long_list_zero_unit_segments(gpu_ctx, bpc, shape):
+    """Lists of more than 256 packets whose packets mostly hold no whole round (shorter than one chunk):
+    the unit map has entries only for the packets that do (none, one in the middle, the last), and the
+    segments' short chunks go one lane each. Every word and the first bad (packet, chunk)."""
+    n = 300
+    sizes = [100 + (i * 37) % (bpc - 100) for i in range(n)]
+    if shape == "one_long_among_tails":
+        sizes[150] = 16 * 4096 + bpc // 2
+    elif shape == "long_last":
+        sizes[-1] = 9 * 4096
+    arena = np.zeros(sum(s + 4 * (-(-s // bpc)) + 48 for s in sizes) + 64, np.uint8)
+    pk, off = [], 16
+    for i, s in enumerate(sizes):
+        d = splitmix_bytes(s, 17000 + i + bpc)
+        w = oracle_compute(d, bpc)
+        arena[off:off + w.nbytes] = w
+        doff = off + w.nbytes
+        doff += (-doff) % 16
+        arena[doff:doff + s] = d
+        pk.append((doff, off, s))
+        off = doff + s + 16 * (i % 3)
+    flips = [(0, 5), (n - 1, sizes[-1] - 1)]
+    if shape == "one_long_among_tails":
+        flips.append((150, 4096 * 8 + 1))
+    check_batch(gpu_ctx, arena, pk, bpc, flips)
