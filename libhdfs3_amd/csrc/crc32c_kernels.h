@@ -127,6 +127,14 @@ struct WordScratch {
 // kernel computes the CRC of every 4096-byte piece into a ctx-owned scratch (two buffers used in
 // turn, so a launch that overlaps its predecessor never writes the words that predecessor's combine
 // still reads), then a combine kernel folds each chunk's R piece CRCs (launch_chunks, pieces != null).
+// Where a long descriptor list's host-to-device copy runs (round 6): on `side`, beside the launch before
+// it, with `stream` waiting for `copied`; in `stream` itself when null or below kSideCopyMinBytes
+struct DescCopy {
+    hipStream_t side = nullptr;
+    hipEvent_t copied = nullptr;
+};
+constexpr size_t kSideCopyMinBytes = size_t(256) << 10;
+
 struct PieceScratch {
     uint8_t *d[2] = {nullptr, nullptr};
     uint64_t cap[2] = {0, 0};
@@ -158,7 +166,8 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                hipStream_t stream, uint64_t arena_len = 0, size_t *bad_index = nullptr,
                                bool overlap_previous = false, WordScratch *ws = nullptr,
-                               PieceScratch *pieces = nullptr, bool *staged = nullptr);
+                               PieceScratch *pieces = nullptr, bool *staged = nullptr,
+                               const DescCopy *dc = nullptr);
 
 hipError_t launch_chunks(const ChunkLaunch &a, bool verify, const uint32_t *d_tables,
                          const uint32_t *d_fold, int grid_cap, hipStream_t stream,

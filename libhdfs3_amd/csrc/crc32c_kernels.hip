@@ -591,6 +591,18 @@ __global__ __launch_bounds__(256) void crc32c_unit_map_kernel(const DevSegment *
 // is not worth it)
 constexpr size_t kUnitMapMinSegments = 256;
 
+// the descriptors' H2D copy: in-stream, or for long lists on the side stream so it runs under the previous
+// launch (1 GiB of 32-64 KiB packets: 872 KB of descriptors)
+hipError_t copy_descs(void *d, const void *h, size_t bytes, hipStream_t stream, const DescCopy *dc) {
+    if (dc && dc->side && dc->copied && bytes >= kSideCopyMinBytes) {
+        hipError_t e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, dc->side);
+        if (e == hipSuccess) e = hipEventRecord(dc->copied, dc->side);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, dc->copied, 0);
+        return e;
+    }
+    return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
+}
+
 // the segments' short last chunks (len % bpc bytes), one thread each
 template <bool VERIFY>
 __global__ __launch_bounds__(kBlockThreads) void crc32c_segment_tails_kernel(const DevSegment *__restrict__ seg,
@@ -625,14 +637,14 @@ hipError_t launch_segment_pieces(DevSegment *h_stage, DevSegment *d_stage, size_
                                  uint32_t bpc, bool verify, int check_short_tail, unsigned long long *result,
                                  const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                  hipStream_t stream, PieceScratch *ps, uint64_t max_chunks, bool any_tail,
-                                 bool *staged) {
+                                 bool *staged, const DescCopy *dc) {
     unsigned b = 0;
     // the piece words, then (long lists) the unit -> segment map
     const bool map = n > kUnitMapMinSegments && pieces_total;
     if (hipError_t e = piece_buffer(ps, (pieces_total ? pieces_total : 1) * (map ? 8 : 4), stream, &b);
         e != hipSuccess)
         return e;
-    hipError_t e = hipMemcpyAsync(d_stage, h_stage, n * sizeof(DevSegment), hipMemcpyHostToDevice, stream);
+    hipError_t e = copy_descs(d_stage, h_stage, n * sizeof(DevSegment), stream, dc);
     if (e != hipSuccess) return e;
     if (staged) *staged = true;
     uint32_t *unit_seg = nullptr;
@@ -680,7 +692,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
                                int check_short_tail, unsigned long long *result, DevSegment *h_stage,
                                DevSegment *d_stage, const uint32_t *d_tables, const uint32_t *d_fold, int grid_cap,
                                hipStream_t stream, uint64_t arena_len, size_t *bad_index, bool overlap_previous,
-                               WordScratch *ws, PieceScratch *pieces, bool *staged) {
+                               WordScratch *ws, PieceScratch *pieces, bool *staged, const DescCopy *dc) {
     if (staged) *staged = false;
     if (n == 0) return hipSuccess;
     // one pass: descriptors, the alignment test of segments_fast and the unit plan of
@@ -775,12 +787,12 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
             any_tail = any_tail || (h_stage[i].len % bpc) != 0;
         }
         return launch_segment_pieces(h_stage, d_stage, n, pieces_total, bpc, verify, check_short_tail, result,
-                                     d_tables, d_fold, grid_cap, stream, pieces, max_chunks, any_tail, staged);
+                                     d_tables, d_fold, grid_cap, stream, pieces, max_chunks, any_tail, staged, dc);
     }
     if (fast) {
         const uint64_t uniform = same && u0 > 0 ? u0 : 0;
         if (n > kInlineSegments) {
-            hipError_t e = hipMemcpyAsync(d_stage, h_stage, n * sizeof(DevSegment), hipMemcpyHostToDevice, stream);
+            hipError_t e = copy_descs(d_stage, h_stage, n * sizeof(DevSegment), stream, dc);
             if (e != hipSuccess) return e;
             if (staged) *staged = true;
         }
@@ -810,7 +822,7 @@ hipError_t launch_packet_batch(const uint8_t *d_arena, const DevPacket *h_pk, si
     // variant 17 (A/B) or unaligned / other chunk sizes: one wave per packet
     DevPacket *hp = reinterpret_cast<DevPacket *>(h_stage);
     for (size_t i = 0; i < n; ++i) hp[i] = h_pk[i];
-    hipError_t e = hipMemcpyAsync(d_stage, hp, n * sizeof(DevPacket), hipMemcpyHostToDevice, stream);
+    hipError_t e = copy_descs(d_stage, hp, n * sizeof(DevPacket), stream, dc);
     if (e != hipSuccess) return e;
     if (staged) *staged = true;
     return launch_packets(d_arena, reinterpret_cast<const DevPacket *>(d_stage), n, bpc, verify, check_short_tail,

@@ -127,7 +127,10 @@ struct hdfs3_crc_ctx {
         size_t cap = 0;
         hipEvent_t done = nullptr;
         bool armed = false;  // done recorded after a copy out of h that may still be pending
+        hipEvent_t copied = nullptr;  // the descriptors' copy on desc_stream (DescCopy)
     } seg_ring[4];
+    // long descriptor lists copy on this stream, beside the previous launch (DescCopy; created on first use)
+    hipStream_t desc_stream = nullptr;
     unsigned seg_next = 0;
     hdfs3crc::WordScratch words;  // dense CRC words of compute over in-packet word regions
     hdfs3crc::PieceScratch pieces;  // 4096-byte piece CRCs of chunks above 4 KiB (launch_chunks)

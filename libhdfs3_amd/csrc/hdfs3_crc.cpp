@@ -261,9 +261,18 @@ int packets_async(hdfs3_crc_ctx *ctx, const uint8_t *d_arena, size_t arena_len, 
     const DevPacket *hp = reinterpret_cast<const DevPacket *>(pk);
     size_t bad = 0;
     bool staged = false;
+    // a long list's descriptors copy on the ctx's side stream, under the launch before (the slot's
+    // host and device halves are free: stage_segments waited for its last launch)
+    DescCopy dc;
+    if (n * sizeof(DevSegment) >= kSideCopyMinBytes) {
+        if (!ctx->desc_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->desc_stream, hipStreamNonBlocking));
+        if (!st->copied) HIP_TRY(hipEventCreateWithFlags(&st->copied, hipEventDisableTiming));
+        dc.side = ctx->desc_stream;
+        dc.copied = st->copied;
+    }
     const hipError_t e = launch_packet_batch(d_arena, hp, n, bpc, verify, check_short_tail, d_result, st->h, st->d,
                                              ctx->d_tables, ctx->d_fold, ctx->grid_cap, ctx->stream, arena_len,
-                                             &bad, overlap, &ctx->words, &ctx->pieces, &staged);
+                                             &bad, overlap, &ctx->words, &ctx->pieces, &staged, &dc);
     if (e == hipErrorInvalidValue) return fail(-EINVAL, "packet %zu lies outside the %zu-byte arena", bad, arena_len);
     HIP_TRY(e);
     ++ctx->launches;
@@ -535,6 +544,11 @@ void hdfs3_crc_ctx_destroy(hdfs3_crc_ctx *ctx) {
         if (st.h) (void)hipHostFree(st.h);
         if (st.d) (void)hipFree(st.d);
         if (st.done) (void)hipEventDestroy(st.done);
+        if (st.copied) (void)hipEventDestroy(st.copied);
+    }
+    if (ctx->desc_stream) {
+        (void)hipStreamSynchronize(ctx->desc_stream);
+        (void)hipStreamDestroy(ctx->desc_stream);
     }
     ctx->words.release();
     ctx->pieces.release();
