@@ -186,7 +186,8 @@ struct SegWalk {
             } else {
                 // the walk only moves forward, and with segments longer than the walk's stride it
                 // lands in the next one: try that first (one descriptor load, which the view needs
-                // anyway) before the binary search (a chain of dependent loads)
+                // anyway), then the unit map of a long list (one load), else the binary search (a chain
+                // of dependent loads)
                 const uint32_t nx = c_si + 1;
                 if (nx < L->nseg && u >= rfl64(segp(nx)->unit_begin) &&
                     u < rfl64(segp(nx)->unit_begin) + units(rfl64(segp(nx)->len)))
