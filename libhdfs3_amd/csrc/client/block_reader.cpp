@@ -32,6 +32,7 @@
 #include <thread>
 #include <vector>
 
+#include "../copy_pool.h"
 #include "../ctx.h"
 #include "../numa.h"
 #include "block_reader.h"
@@ -233,6 +234,9 @@ struct hdfs3_block_reader {
     // 8-stream callers burnt 0.165 CPU-s per GiB, 0.057 of it copying), and a busy query loop, the
     // behaviour before round 6, more. HDFS3_READER_WAIT=block / spin (measurement knobs) select those.
     enum WaitMode { kWaitPoll, kWaitBlock, kWaitSpin } wait_mode = kWaitPoll;
+    // HDFS3_READER_COPY_NT=1 (measurement knob, round 6): the copy-out with streaming stores, so the
+    // caller's destination lines are written without being read first (x86 with AVX2)
+    bool copy_nt = false;
 
     int sticky(int code, const std::string &msg) {
         error = code;
@@ -599,7 +603,10 @@ struct hdfs3_block_reader {
                     const PacketRef &p = b.pk[b.dpkt];
                     const size_t avail = p.deliver - b.doff;
                     const size_t n = std::min<size_t>(avail, size_t(len - total));
-                    std::memcpy(out + total, b.a.h + p.data_off + p.skip + b.doff, n);
+                    if (copy_nt && n >= 4096)
+                        memcpy_stream(out + total, b.a.h + p.data_off + p.skip + b.doff, n);
+                    else
+                        std::memcpy(out + total, b.a.h + p.data_off + p.skip + b.doff, n);
                     total += int32_t(n);
                     b.doff += n;
                     delivered += int64_t(n);
@@ -708,6 +715,10 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
                                                       : hdfs3_block_reader::kWaitPoll;
         const char *ha = getenv("HDFS3_READER_HEADER_AHEAD");
         r->header_ahead = !(ha && ha[0] == '0');
+#if HDFS3_COPY_NT_AVAILABLE
+        const char *nt = getenv("HDFS3_READER_COPY_NT");
+        r->copy_nt = nt && nt[0] == '1' && __builtin_cpu_supports("avx2");
+#endif
     }
     const int device = opts ? opts->device : 0;
     r->verify = opts ? opts->verify != 0 : true;
