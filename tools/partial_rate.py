@@ -161,6 +161,25 @@ def main():
         tv = timed(lambda i: ctx.verify_packet_stream_async(a.data_ptr(), a.numel(), ps, bpc, rp + 8 * (i % 512)),
                    n=20, warm=5, reps=3)
         tc = timed(lambda i: ctx.compute_packet_stream_async(a.data_ptr(), a.numel(), ps, bpc), n=20, warm=5, reps=3)
+        tcv = {}
+        for v in variants:  # lab variants of the stream compute, interleaved twice, their words checked
+            for _ in range(2):
+                lib.hdfs3x_set_variant(v)
+                tcv.setdefault(v, []).append(
+                    timed(lambda i: ctx.compute_packet_stream_async(a.data_ptr(), a.numel(), ps, bpc),
+                          n=20, warm=5, reps=3))
+                lib.hdfs3x_set_variant(0)
+                tcv.setdefault(0, []).append(
+                    timed(lambda i: ctx.compute_packet_stream_async(a.data_ptr(), a.numel(), ps, bpc),
+                          n=20, warm=5, reps=3))
+            lib.hdfs3x_set_variant(v)
+            ctx.compute_packet_stream_async(a.data_ptr(), a.numel(), ps, bpc)
+            lib.hdfs3x_set_variant(0)
+            torch.cuda.synchronize()
+            res.zero_()
+            ctx.verify_packet_stream_async(a.data_ptr(), a.numel(), ps, bpc, rp)
+            torch.cuda.synchronize()
+            assert not bool(res.any().item()), f"stream bpc {bpc} variant {v}: computed words fail to verify"
         tb = timed(lambda i: ctx.verify_dev_async(blk.data_ptr(), blk.numel(), bpc, bw.data_ptr(), rp + 8 * (i % 512)),
                    n=20, warm=5, reps=3)
         torch.cuda.synchronize()
@@ -170,7 +189,9 @@ def main():
                           "verify_us": round(tv, 1), "compute_us": round(tc, 1), "contiguous_verify_us": round(tb, 1),
                           "verify_TiBps": round(payload / tv / 1e-6 / 2**40, 3),
                           "compute_TiBps": round(payload / tc / 1e-6 / 2**40, 3),
-                          "contiguous_verify_TiBps": round(payload / tb / 1e-6 / 2**40, 3)}), flush=True)
+                          "contiguous_verify_TiBps": round(payload / tb / 1e-6 / 2**40, 3),
+                          "compute_us_by_variant": {str(k): [round(x, 1) for x in v] for k, v in tcv.items()}}),
+              flush=True)
         del a, blk, bw
     ctx.set_stream(None)
 
