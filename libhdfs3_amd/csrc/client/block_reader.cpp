@@ -237,6 +237,17 @@ struct hdfs3_block_reader {
     // HDFS3_READER_COPY_NT=1 (measurement knob, round 6): the copy-out with streaming stores, so the
     // caller's destination lines are written without being read first (x86 with AVX2)
     bool copy_nt = false;
+    // A caller whose whole range has one destination (pread, fetchBlockByteRange) may pass it at open
+    // (measurement knob HDFS3_READER_EAGER_COPY=1, round 6): the receiver copies each packet's bytes there
+    // right after its receive, while they are hot in cache, and read() skips the copy for output that
+    // lands where they already are. Delivery and errors are unchanged: read() still returns only verified
+    // bytes; bytes past a bad packet may already sit in the caller's buffer beyond the count returned.
+    uint8_t *dest = nullptr;
+    int64_t rx_out = 0;  // receiver: bytes of the range copied to dest so far
+    void eager(const uint8_t *src, int64_t useful) {
+        if (dest && useful > 0 && rx_out + useful <= end_offset - start) std::memcpy(dest + rx_out, src, size_t(useful));
+        rx_out += useful;
+    }
 
     int sticky(int code, const std::string &msg) {
         error = code;
@@ -364,6 +375,7 @@ struct hdfs3_block_reader {
                     std::max<int64_t>(0, std::min<int64_t>(h.data_len - ahead, end_offset - recv_cursor));
                 b.pk.push_back(PacketRef{b.d0 + b.data_used, b.words_used, uint32_t(h.data_len), uint32_t(ahead),
                                          uint32_t(useful)});
+                eager(b.a.h + b.d0 + b.data_used + ahead, useful);
                 b.chunk0.push_back(b.words_used / 4);
                 b.words_used += crc_len;
                 b.data_used += uint64_t(h.data_len);
@@ -397,6 +409,7 @@ struct hdfs3_block_reader {
             ahead = ahead > 0 ? ahead : 0;
             const int64_t useful = std::max<int64_t>(0, std::min<int64_t>(h.data_len - ahead, end_offset - recv_cursor));
             b.pk.push_back(PacketRef{off + crc_len, off, uint32_t(h.data_len), uint32_t(ahead), uint32_t(useful)});
+            eager(b.a.h + off + crc_len + ahead, useful);
             b.used = off + size;
             const int64_t reached = recv_cursor + h.data_len - ahead;
             recv_cursor = reached;
@@ -603,7 +616,9 @@ struct hdfs3_block_reader {
                     const PacketRef &p = b.pk[b.dpkt];
                     const size_t avail = p.deliver - b.doff;
                     const size_t n = std::min<size_t>(avail, size_t(len - total));
-                    if (copy_nt && n >= 4096)
+                    if (dest && out + total == dest + delivered)
+                        ;  // the receiver already put these bytes here
+                    else if (copy_nt && n >= 4096)
                         memcpy_stream(out + total, b.a.h + p.data_off + p.skip + b.doff, n);
                     else
                         std::memcpy(out + total, b.a.h + p.data_off + p.skip + b.doff, n);
@@ -697,7 +712,7 @@ int64_t block_reader_arena_bytes(const hdfs3_reader_opts *opts) {
 
 int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int64_t start, int64_t len,
                       const char *client_name, const hdfs3_reader_opts *opts, hdfs3_crc_ctx *shared_ctx,
-                      hdfs3_block_reader **out, int slots) {
+                      hdfs3_block_reader **out, int slots, uint8_t *dest) {
     if (!out || !host || !blk || start < 0 || len < 0) return fail(-EINVAL, "invalid argument");
     *out = nullptr;
     hdfs3_block_reader *r = new (std::nothrow) hdfs3_block_reader();
@@ -734,6 +749,7 @@ int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int
     r->block.num_bytes = blk->num_bytes;
     r->start = r->recv_cursor = start;
     r->end_offset = start + len;
+    r->dest = dest;
     if (shared_ctx) {
         r->ctx = shared_ctx;
         r->own_ctx = false;

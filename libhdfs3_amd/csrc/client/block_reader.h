@@ -12,7 +12,7 @@ namespace hdfs3crc {
 // default 3; the input stream's block read-ahead asks for up to a whole block's worth)
 int open_block_reader(const char *host, int port, const hdfs3_block_id *blk, int64_t start, int64_t len,
                       const char *client_name, const hdfs3_reader_opts *opts, hdfs3_crc_ctx *shared_ctx,
-                      hdfs3_block_reader **out, int slots = 0);
+                      hdfs3_block_reader **out, int slots = 0, uint8_t *dest = nullptr);
 
 // bytes of one batch arena of a reader with these options (the read-ahead ring depth unit)
 int64_t block_reader_batch_bytes(const hdfs3_reader_opts *opts);

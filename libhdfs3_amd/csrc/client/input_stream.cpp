@@ -10,6 +10,7 @@
 // read(), failover and EIO behave exactly as for a reader opened on demand.
 #include <algorithm>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <new>
@@ -173,7 +174,8 @@ struct hdfs3_input_stream {
     }
 
     // setupBlockReader (:364-450) for [start, start+len) of block b; -errno
-    int setup(const Block &b, int64_t start, int64_t len, hdfs3_block_reader **out, Node *node) {
+    int setup(const Block &b, int64_t start, int64_t len, hdfs3_block_reader **out, Node *node,
+              uint8_t *dest = nullptr) {
         std::string why;
         for (;;) {
             const Node *n = best_node(b);
@@ -185,7 +187,7 @@ struct hdfs3_input_stream {
             hdfs3_block_id id = b.id;
             id.pool_id = b.pool.c_str();
             const int rc = open_block_reader(n->host.c_str(), n->port, &id, start, len, client_name.c_str(), &opts,
-                                             ctx, out);
+                                             ctx, out, 0, dest);
             if (rc == 0) {
                 *node = *n;
                 ++opened;
@@ -264,7 +266,10 @@ struct hdfs3_input_stream {
         for (;;) {
             hdfs3_block_reader *r = nullptr;
             Node node;
-            if ((rc = setup(b, start, len, &r, &node))) break;
+            // the range's one destination goes to the reader (HDFS3_READER_EAGER_COPY=1, measurement knob)
+            const char *ev = getenv("HDFS3_READER_EAGER_COPY");
+            const bool eager = ev && ev[0] == '1';
+            if ((rc = setup(b, start, len, &r, &node, eager ? out : nullptr))) break;
             int64_t got = 0;
             int32_t n = 0;
             while (got < len) {
