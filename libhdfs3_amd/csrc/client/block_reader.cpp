@@ -237,10 +237,10 @@ struct hdfs3_block_reader {
     // HDFS3_READER_COPY_NT=1 (measurement knob, round 6): the copy-out with streaming stores, so the
     // caller's destination lines are written without being read first (x86 with AVX2)
     bool copy_nt = false;
-    // A caller whose whole range has one destination (pread, fetchBlockByteRange) may pass it at open
-    // (measurement knob HDFS3_READER_EAGER_COPY=1, round 6): the receiver copies each packet's bytes there
-    // right after its receive, while they are hot in cache, and read() skips the copy for output that
-    // lands where they already are. Delivery and errors are unchanged: read() still returns only verified
+    // A caller whose whole range has one destination (pread: fetchBlockByteRange) passes it at open
+    // (round 6; the input stream does unless HDFS3_READER_EAGER_COPY=0): the receiver copies each
+    // packet's bytes there right after its receive, while they are hot in cache, and read() skips the
+    // copy for output that lands where they already are. Delivery and errors are unchanged: read() still returns only verified
     // bytes; bytes past a bad packet may already sit in the caller's buffer beyond the count returned.
     uint8_t *dest = nullptr;
     int64_t rx_out = 0;  // receiver: bytes of the range copied to dest so far

@@ -266,9 +266,12 @@ struct hdfs3_input_stream {
         for (;;) {
             hdfs3_block_reader *r = nullptr;
             Node node;
-            // the range's one destination goes to the reader (HDFS3_READER_EAGER_COPY=1, measurement knob)
+            // the range's one destination goes to the reader, which copies each packet there while it is hot
+            // (round 6; 8 concurrent preads: client CPU per GiB 1.28-1.41x -> 0.98-1.16x the reference
+            // loop's, rate within the spread, profiles/r06/r6eg_config5_eager_ab.jsonl).
+            // HDFS3_READER_EAGER_COPY=0 (measurement knob) leaves the copy to read()
             const char *ev = getenv("HDFS3_READER_EAGER_COPY");
-            const bool eager = ev && ev[0] == '1';
+            const bool eager = !(ev && ev[0] == '0');
             if ((rc = setup(b, start, len, &r, &node, eager ? out : nullptr))) break;
             int64_t got = 0;
             int32_t n = 0;
